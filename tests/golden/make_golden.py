@@ -1,0 +1,225 @@
+"""Generates the golden fixtures in tests/golden/ by running the REFERENCE (p1atdev/vision-pt at
+/root/reference) on CPU in the survey container. Only the resulting tensors are committed (no
+reference source travels). Re-run: `python tests/golden/make_golden.py` (needs /root/reference).
+
+Import recipe: SURVEY.md Appendix A (Recipe A for the denoiser/config/class encoder, Recipe B
+stubs for train/jit/arb_class_to_image.py to reach JiTModel.image_to_velocity).
+
+Fixtures:
+  jit_micro.safetensors  micro JiT (D=192, 3 heads, depth 3, context from block 1, ctx_dim 64,
+                         2 x 64x48 images, 8 context tokens, one padded) — fp32 reference forward,
+                         image- and velocity-target losses, full gradients of the small
+                         parameters and (norm, sum, first 64) of every parameter gradient.
+  jit_c1.safetensors     BASELINE config 1 (D=256, 4 heads, depth 2, ctx_dim 256, context in both
+                         blocks, 4 x 256^2): loss, output checksums, per-parameter grad norms.
+  ops.safetensors        timestep embedding (t = 0..9999 subsample + fractional), RoPE tables of
+                         the 7 benchmark buckets (checksums + head/tail rows), tokenizer ids/masks,
+                         bucket lists.
+Weights are not stored: they are regenerated from oracle.jit_oracle.make_weights(cfg, seed).
+"""
+
+from __future__ import annotations
+
+import ast
+import importlib
+import importlib.machinery
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from safetensors.torch import save_file
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, ROOT)
+from oracle.jit_oracle import OracleConfig, make_weights  # noqa: E402
+from tests.golden.golden_configs import c1_config, make_batch, micro_config  # noqa: E402
+
+torch.set_num_threads(8)
+
+
+def import_reference():
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, REF)
+
+    def stub(name, **attrs):
+        m = types.ModuleType(name)
+        m.__spec__ = importlib.machinery.ModuleSpec(name, None)
+        m.__dict__.update(attrs)
+        sys.modules[name] = m
+        return m
+
+    class _Any:
+        def __init__(self, *a, **k):
+            pass
+
+    stub("wandb", Image=_Any)
+    stub("imagesize", get=lambda p: (0, 0))
+    stub("polars")
+    stub("src.dataset.text_to_image", TextToImageDatasetConfig=object)
+    stub("src.dataset.square_class_image", SquareClassImageDatasetConfig=object)
+    stub("src.utils.grid", images_to_grid_image=None)
+    bnb = stub("bitsandbytes")
+    bnb.__path__ = []
+    bnb.nn = stub("bitsandbytes.nn", Linear4bit=nn.Linear, Linear8bitLt=nn.Linear, Params4bit=nn.Parameter,
+                  Int8Params=nn.Parameter)
+    bnb.functional = stub("bitsandbytes.functional", quantize_4bit=None)
+    ao = stub("torchao")
+    ao.__path__ = []
+    stub("torchao.float8").__path__ = []
+    stub("torchao.float8.float8_linear", Float8Linear=nn.Linear)
+    sys.path.insert(0, REF + "/train/jit")
+    arb = importlib.import_module("arb_class_to_image")
+    den = importlib.import_module("src.models.jit.denoiser")
+    cfgm = importlib.import_module("src.models.jit.config")
+    ce = importlib.import_module("src.models.jit.class_encoder")
+    emb = importlib.import_module("src.modules.timestep.embedding")
+    fm = importlib.import_module("src.modules.loss.flow_match")
+    # generate_buckets is pure numpy but its module imports torchvision: exec the function source
+    src = open(REF + "/src/dataset/aspect_ratio_bucket.py").read()
+    tree = ast.parse(src)
+    fn = next(n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == "generate_buckets")
+    ns = {"np": np}
+    exec(compile(ast.Module(body=[fn], type_ignores=[]), "aspect_ratio_bucket.py", "exec"), ns)
+    return types.SimpleNamespace(arb=arb, den=den, cfg=cfgm, ce=ce, emb=emb, fm=fm, generate_buckets=ns["generate_buckets"])
+
+
+def ref_config(R, oc: OracleConfig):
+    return R.cfg.DenoiserConfig(
+        patch_size=oc.patch_size, hidden_size=oc.hidden_size, depth=oc.depth, num_heads=oc.num_heads,
+        bottleneck_dim=oc.bottleneck_dim, context_dim=oc.context_dim, context_start_block=oc.context_start_block,
+        rope_axes_dims=oc.rope_axes_dims, rope_axes_lens=oc.rope_axes_lens, rope_zero_centered=oc.rope_zero_centered)
+
+
+def run_reference(R, oc: OracleConfig, weights, batch, loss_target):
+    model = R.den.Denoiser(ref_config(R, oc))
+    sd = {k: v for k, v in weights.items() if not k.startswith("class_encoder.")}
+    model.load_state_dict(sd, strict=True)
+    model.train()
+    emb = weights["class_encoder.embedding.weight"].clone().requires_grad_(True)
+    x = batch["image"]
+    t = batch["t"]
+    orig = torch.randn_like
+    torch.randn_like = lambda ten, *a, **k: batch["noise"].to(ten.dtype)
+    try:
+        z, _ = R.fm.prepare_scaled_noised_latents(latents=x, timestep=t, noise_scale=1.0)  # flow_match.py:60-74
+    finally:
+        torch.randn_like = orig
+    ctx = F.embedding(batch["ids"], emb, padding_idx=emb.shape[0] - 1)  # nn.Embedding(padding_idx=V)
+    pred = model(image=z.float(), timestep=t.float(), context=ctx, original_size=batch["original_size"],
+                 target_size=batch["target_size"], crop_coords=batch["crop_coords"], context_mask=batch["mask"])
+    if loss_target == "image":
+        loss = F.mse_loss(pred, x.float())  # arb_class_to_image.py:139-144
+    else:
+        itv = R.arb.JiTModel.image_to_velocity
+        pv = itv(None, image=pred, noisy=z, timestep=t, clamp_eps=0.05)
+        tv = itv(None, image=x.float(), noisy=z, timestep=t, clamp_eps=0.05)
+        loss = F.mse_loss(pv, tv)  # arb_class_to_image.py:119-138
+    loss.backward()
+    grads = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+    grads["class_encoder.embedding.weight"] = emb.grad.detach().clone()
+    return loss.detach(), pred.detach(), z.detach(), grads
+
+
+def grad_summary(prefix, grads, out, full_small=4096):
+    for n, gr in grads.items():
+        g = gr.float().reshape(-1)
+        out[f"{prefix}gnorm/{n}"] = g.norm().reshape(1)
+        out[f"{prefix}gsum/{n}"] = g.sum().reshape(1)
+        out[f"{prefix}ghead/{n}"] = g[:64].clone()
+        if g.numel() <= full_small:
+            out[f"{prefix}gfull/{n}"] = g.clone()
+
+
+def main():
+    R = import_reference()
+    meta = {"torch": torch.__version__, "threads": str(torch.get_num_threads()), "reference": REF}
+
+    # ---------------- micro
+    oc = micro_config()
+    V = 20
+    w = make_weights(oc, seed=1, n_classes=V)
+    batch = make_batch(oc, 2, 64, 48, 8, V, seed=2)
+    out = {k: v for k, v in batch.items()}
+    for lt in ("image", "velocity"):
+        loss, pred, z, grads = run_reference(R, oc, w, batch, lt)
+        out[f"{lt}/loss"] = loss.reshape(1)
+        out[f"{lt}/pred"] = pred
+        grad_summary(f"{lt}/", grads, out)
+    out["z"] = z
+    out["wsum"] = torch.stack([w[k].double().sum().float() for k in sorted(w)])
+    save_file({k: v.contiguous() for k, v in out.items()}, os.path.join(HERE, "jit_micro.safetensors"), metadata=meta)
+
+    # ---------------- C1 tiny (BASELINE config 1)
+    oc = c1_config()
+    V = 1000
+    w = make_weights(oc, seed=3, n_classes=V)
+    batch = make_batch(oc, 4, 256, 256, 64, V, seed=4, padded_rows=(1, 3))
+    loss, pred, z, grads = run_reference(R, oc, w, batch, "image")
+    out = {"loss": loss.reshape(1), "pred_sum": pred.double().sum().float().reshape(1),
+           "pred_sq": pred.double().pow(2).sum().float().reshape(1), "pred_head": pred.reshape(-1)[:256].clone(),
+           "pred_tail": pred.reshape(-1)[-256:].clone()}
+    gsum = {}
+    grad_summary("", grads, gsum, full_small=0)
+    out.update({k: v for k, v in gsum.items() if not k.startswith("ghead")})
+    save_file({k: v.contiguous() for k, v in out.items()}, os.path.join(HERE, "jit_c1.safetensors"), metadata=meta)
+
+    # ---------------- per-op vectors
+    ops = {}
+    tt = torch.cat([torch.arange(0, 10000, 37).float(), torch.tensor([0.5, 0.123, 0.999, 1024.0, 2048.0])])
+    ops["temb/t"] = tt
+    ops["temb/out"] = R.emb.get_timestep_embedding(tt, 256, flip_sin_to_cos=True, downscale_freq_shift=0)
+    cfgB = R.cfg.JiT_B_16_Config()
+    model_b = None
+    rope = R.den.RopeEmbedder(rope_theta=cfgB.rope_theta, axes_dims=cfgB.rope_axes_dims,
+                              axes_lens=cfgB.rope_axes_lens, zero_centered=cfgB.rope_zero_centered)
+    for (Wd, Hd) in [(256, 256), (512, 512), (1024, 1024), (960, 1088), (1088, 960), (896, 1152), (1152, 896)]:
+        ids = [rope.prepare_image_position_ids(Hd, Wd, 16, 3), rope.prepare_context_position_ids(6, 2),
+               rope.prepare_context_position_ids(4, 1), rope.prepare_context_position_ids(64, 0)]
+        fc = torch.cat([rope(position_ids=i.unsqueeze(0)) for i in ids], 1)[0]  # denoiser.py:1032-1051
+        key = f"rope/{Wd}x{Hd}"
+        ops[key + "/cos_sum"] = fc.real.double().sum().float().reshape(1)
+        ops[key + "/sin_sum"] = fc.imag.double().sum().float().reshape(1)
+        ops[key + "/head"] = torch.view_as_real(fc[:8]).contiguous()
+        ops[key + "/tail"] = torch.view_as_real(fc[-80:]).contiguous()
+        ops[key + "/n"] = torch.tensor([fc.shape[0]])
+    # tokenizer
+    label2id = {f"tag{i}": i for i in range(12)}
+    tok = R.ce.ClassTokenizer(label2id=label2id, splitter=" ", do_mask_padding=True)
+    caps = ["tag1 tag3 tag3", "", "tag11 unknown tag0", " ".join(f"tag{i % 12}" for i in range(20))]
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        o = tok.tokenize(caps, max_length=8)
+    ops["tok/ids"] = o.class_ids
+    ops["tok/mask"] = o.attention_mask
+    meta_ops = dict(meta, captions=json.dumps(caps), label2id=json.dumps(label2id))
+    for args in [(1024 ** 2, 1024, 64, 64), (64 ** 2, 64, 64, 64), (1024 ** 2, 1024, 64, 384), (256 ** 2, 256, 128, 256)]:
+        b = R.generate_buckets(*args)
+        ops["buckets/" + "_".join(map(str, args))] = torch.from_numpy(np.asarray(b, dtype=np.int64))
+    # one rms_norm + apply_rope vector (denoiser.py:98-111, norm.py:20-27)
+    g = torch.Generator().manual_seed(5)
+    xq = torch.randn(2, 3, 10, 64, generator=g)
+    fc = torch.polar(torch.ones(10, 32), torch.rand(10, 32, generator=g) * 6)
+    ops["rope_apply/x"] = xq
+    ops["rope_apply/freqs"] = torch.view_as_real(fc).contiguous()
+    ops["rope_apply/out"] = R.den.apply_rope(xq, fc.unsqueeze(0).repeat(2, 1, 1))
+    nw = torch.randn(64, generator=g)
+    norm = R.den.get_norm_layer("rms", 64, eps=1e-6)
+    with torch.no_grad():
+        norm.weight.copy_(nw)
+    ops["rms/w"] = nw
+    ops["rms/out"] = norm(xq).detach()
+    save_file({k: v.contiguous() for k, v in ops.items()}, os.path.join(HERE, "ops.safetensors"), metadata=meta_ops)
+    for f in ("jit_micro", "jit_c1", "ops"):
+        print(f, os.path.getsize(os.path.join(HERE, f + ".safetensors")))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,354 @@
+"""Per-kernel numerics of libvpt_hip.so on the GPU against plain PyTorch fp32 references of the
+same op (computed on the same bf16 inputs). Tolerances are stated per test."""
+
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.fixture(scope="module")
+def ops():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vpt import ops as _ops
+    return _ops
+
+
+def rnd(*shape, scale=1.0, dtype=torch.bfloat16, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dtype).to(DEV)
+
+
+# ------------------------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 136, 200), (1000, 768, 768), (64, 2304, 768)])
+def test_gemm_forward(ops, M, N, K):
+    x = rnd(M, K, seed=1)
+    w = rnd(N, K, scale=0.05, seed=2)
+    b = rnd(N, scale=0.1, seed=3)
+    y = ops.linear(x, w, bias=b)
+    ref = x.float() @ w.float().t() + b.float()
+    assert rel(y, ref) < 5e-3  # bf16 output rounding
+
+
+def test_gemm_identity_asymmetric(ops):
+    # A = I with an asymmetric B catches a transposed C write (guide §3).
+    n = 128
+    eye = torch.eye(n, dtype=torch.bfloat16, device=DEV)
+    b = (torch.arange(n * n, dtype=torch.float32, device=DEV).view(n, n) % 61 - 30).to(torch.bfloat16)
+    y = ops.linear(eye, b)  # eye @ b.T = b.T
+    assert torch.equal(y.float(), b.float().t())
+
+
+def test_gemm_residual_silu(ops):
+    M, N, K = 384, 256, 256
+    x, w, b, r = rnd(M, K, seed=4), rnd(N, K, scale=0.05, seed=5), rnd(N, scale=0.1, seed=6), rnd(M, N, seed=7)
+    y = ops.linear(x, w, bias=b, resid=r)
+    lin = (x.float() @ w.float().t() + b.float()).to(torch.bfloat16)
+    ref = (lin.float() + r.float()).to(torch.bfloat16)
+    assert rel(y, ref) < 5e-3
+    ys = ops.linear(x, w, bias=b, act=ops.ACT_SILU)
+    refs = torch.nn.functional.silu(x.float() @ w.float().t() + b.float())
+    assert rel(ys, refs) < 5e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 256, 384), (1000, 768, 200)])
+def test_gemm_dgrad(ops, M, N, K):
+    dy = rnd(M, N, seed=8)
+    w = rnd(N, K, scale=0.05, seed=9)
+    dx = ops.linear_dgrad(dy, w)
+    assert rel(dx, dy.float() @ w.float()) < 5e-3
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(1000, 256, 128, 1), (4170, 768, 768, 4), (333, 136, 64, 2)])
+def test_gemm_wgrad(ops, M, N, K, splits):
+    dy = rnd(M, N, seed=10)
+    x = rnd(M, K, seed=11)
+    out = torch.zeros(N, K, dtype=torch.float32, device=DEV)
+    ops.linear_wgrad(dy, x, out, splits=splits)
+    ref = dy.float().t() @ x.float()
+    assert rel(out, ref) < 1e-5
+    ops.linear_wgrad(dy, x, out, accumulate=True)
+    assert rel(out, 2 * ref) < 1e-5
+
+
+def test_gemm_split_matches_unsplit(ops):
+    M, N, K = 2048, 384, 256
+    dy, x = rnd(M, N, seed=12), rnd(M, K, seed=13)
+    a = torch.empty(N, K, dtype=torch.float32, device=DEV)
+    b = torch.empty_like(a)
+    ops.linear_wgrad(dy, x, a, splits=1)
+    ops.linear_wgrad(dy, x, b, splits=8)
+    assert rel(a, b) < 1e-6
+
+
+# ------------------------------------------------------------------------------------ norms
+def test_rmsnorm_fwd_bwd(ops):
+    M, D = 777, 768
+    x = rnd(M, D, seed=20)
+    w = (1 + rnd(D, scale=0.1, seed=21).float()).to(torch.bfloat16)
+    y, rstd = ops.rmsnorm_fwd(x, w)
+    xf = x.float().requires_grad_(True)
+    wf = w.float().requires_grad_(True)
+    ref = torch.nn.functional.rms_norm(xf, (D,), weight=wf, eps=1e-6)
+    assert rel(y, ref) < 5e-3
+    assert rel(rstd, torch.rsqrt(x.float().pow(2).mean(-1) + 1e-6)) < 1e-5
+    dy = rnd(M, D, seed=22)
+    dres = rnd(M, D, seed=23)
+    dx, part = ops.rmsnorm_bwd(dy, x, rstd, w, dres=dres)
+    dw = torch.zeros(D, device=DEV)
+    ops.reduce_rows(part, dw)
+    ref.backward(dy.float())
+    assert rel(dx, xf.grad + dres.float()) < 5e-3
+    assert rel(dw, wf.grad) < 1e-4
+
+
+def _rope_tables(rows, seed=30):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    ang = torch.rand(rows, 32, generator=g) * 6.0
+    return torch.cos(ang).to(DEV), torch.sin(ang).to(DEV)
+
+
+def _ref_qknorm_rope(qkv, wq, wk, cos, sin, rows_per_seq):
+    M = qkv.shape[0]
+    pos = torch.arange(M, device=DEV) % rows_per_seq
+    fc = torch.complex(cos[pos], sin[pos])  # [M,32]
+    outs = []
+    for i, w in enumerate((wq, wk)):
+        x = qkv[:, i * 768:(i + 1) * 768].float().view(M, 12, 64)
+        y = torch.nn.functional.rms_norm(x, (64,), weight=w.float(), eps=1e-6)
+        yc = torch.view_as_complex(y.reshape(M, 12, 32, 2)) * fc[:, None, :]
+        outs.append(torch.view_as_real(yc).reshape(M, 768))
+    return torch.cat(outs, 1)
+
+
+def test_qknorm_rope_fwd_bwd(ops):
+    M, rps = 530, 265
+    qkv = rnd(M, 2304, seed=31)
+    wq = (1 + rnd(64, scale=0.1, seed=32).float()).to(torch.bfloat16)
+    wk = (1 + rnd(64, scale=0.1, seed=33).float()).to(torch.bfloat16)
+    cos, sin = _rope_tables(rps)
+    out = ops.qknorm_rope_fwd(qkv, wq, wk, cos, sin, rps)
+    qf = qkv.float().requires_grad_(True)
+    wqf = wq.float().requires_grad_(True)
+    wkf = wk.float().requires_grad_(True)
+    ref = _ref_qknorm_rope(qf, wqf, wkf, cos, sin, rps)
+    assert rel(out, ref) < 8e-3
+    g = rnd(M, 1536, seed=34)
+    dqkv = torch.zeros(M, 2304, dtype=torch.bfloat16, device=DEV)
+    part = ops.qknorm_rope_bwd(g, qkv, wq, wk, cos, sin, rps, dqkv)
+    dw = torch.zeros(128, device=DEV)
+    ops.reduce_rows(part, dw)
+    ref.backward(g.float())
+    assert rel(dqkv[:, :1536], qf.grad[:, :1536]) < 8e-3
+    assert rel(dw[:64], wqf.grad) < 1e-3
+    assert rel(dw[64:], wkf.grad) < 1e-3
+
+
+# ------------------------------------------------------------------------------------ attention
+def _attn_ref(q, k, v, bias, scale):
+    # q,k,v [B,H,N,64] f32; bias [B,N] additive
+    s = torch.einsum("bhqd,bhkd->bhqk", q, k) * scale + bias[:, None, None, :]
+    p = torch.softmax(s, -1)
+    return torch.einsum("bhqk,bhkd->bhqd", p, v)
+
+
+@pytest.mark.parametrize("n,n_dense,masked", [(200, 150, True), (330, 330, False), (64, 40, True), (1034, 1024, True)])
+def test_attention_fwd_bwd(ops, n, n_dense, masked):
+    B, H, rows = 2, 3, ((n + 127) // 128) * 128
+    D = H * 64
+    qkv = rnd(B * rows, 3 * D, seed=40)
+    kb = torch.zeros(B, rows, device=DEV)
+    if masked:
+        kb[:, n_dense + (n - n_dense) // 2:] = float("-inf")
+        kb[1, n_dense:] = 0.0  # second sequence: nothing masked
+    o = torch.zeros(B * rows, D, dtype=torch.bfloat16, device=DEV)
+    lse = torch.zeros(B, H, rows, device=DEV)
+    q4 = ops._t4(qkv, B, rows, H, 0)
+    k4 = ops._t4(qkv, B, rows, H, D)
+    v4 = ops._t4(qkv, B, rows, H, 2 * D)
+    o4 = ops._t4(o, B, rows, H, 0)
+    ops.attn_fwd(q4, k4, v4, o4, lse, kb, B, H, rows, n, n_dense)
+
+    def heads(t, c0):
+        return t[:, c0:c0 + D].float().view(B, rows, H, 64)[:, :n].permute(0, 2, 1, 3).contiguous()
+
+    qf = heads(qkv, 0).requires_grad_(True)
+    kf = heads(qkv, D).requires_grad_(True)
+    vf = heads(qkv, 2 * D).requires_grad_(True)
+    bias = kb[:, :n].clone()
+    bias[:, n_dense:] = kb[:, n_dense:n]
+    ref = _attn_ref(qf, kf, vf, bias, 0.125)
+    got = o.view(B, rows, H, 64)[:, :n].permute(0, 2, 1, 3).float()
+    assert rel(got, ref) < 1e-2
+
+    do = rnd(B * rows, D, seed=41)
+    dq = torch.zeros(B * rows, D, dtype=torch.bfloat16, device=DEV)
+    dk = torch.zeros_like(dq)
+    dv = torch.zeros_like(dq)
+    delta = torch.zeros(B, H, rows, device=DEV)
+    ops.attn_bwd(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, kb, ops._t4(dq, B, rows, H),
+                 ops._t4(dk, B, rows, H), ops._t4(dv, B, rows, H), B, H, rows, n, n_dense)
+    dof = do.float().view(B, rows, H, 64)[:, :n].permute(0, 2, 1, 3)
+    ref.backward(dof)
+
+    def unh(t):
+        return t.view(B, rows, H, 64)[:, :n].permute(0, 2, 1, 3).float()
+
+    assert rel(unh(dq), qf.grad) < 2e-2
+    assert rel(unh(dk), kf.grad) < 2e-2
+    assert rel(unh(dv), vf.grad) < 2e-2
+
+
+# ------------------------------------------------------------------------------------ misc
+def test_swiglu(ops):
+    M, F = 300, 2048
+    x12 = rnd(M, 2 * F, seed=50)
+    h = torch.empty(M, F, dtype=torch.bfloat16, device=DEV)
+    ops.swiglu_fwd(x12, h)
+    xf = x12.float().requires_grad_(True)
+    ref = torch.nn.functional.silu(xf[:, :F]) * xf[:, F:]
+    assert rel(h, ref) < 5e-3
+    dh = rnd(M, F, seed=51)
+    dx = torch.empty_like(x12)
+    ops.swiglu_bwd(dh, x12, dx)
+    ref.backward(dh.float())
+    assert rel(dx, xf.grad) < 1e-2
+
+
+def test_bias_grad(ops):
+    dy = rnd(5000, 768, seed=52)
+    out = torch.zeros(768, device=DEV)
+    ops.bias_grad(dy, out)
+    assert rel(out, dy.float().sum(0)) < 1e-5
+
+
+def test_patchify_unpatchify_roundtrip(ops):
+    B, H, W = 2, 64, 96
+    img = rnd(B, 3, H, W, seed=53)
+    p = torch.empty(B * (H // 16) * (W // 16), 768, dtype=torch.bfloat16, device=DEV)
+    ops.patchify(img, B, H, W, p, noising=False)
+    # im2col order (c, ky, kx) as Conv2d(3,128,16,16).weight.view(128,-1)
+    ref = img.view(B, 3, H // 16, 16, W // 16, 16).permute(0, 2, 4, 1, 3, 5).reshape(-1, 768)
+    assert torch.equal(p, ref)
+    # unpatchify uses (ky, kx, c) order
+    q = img.view(B, 3, H // 16, 16, W // 16, 16).permute(0, 2, 4, 3, 5, 1).reshape(-1, 768).contiguous()
+    back = torch.empty_like(img)
+    ops.unpatchify(q, B, H, W, back)
+    assert torch.equal(back, img)
+
+
+def test_noise_patchify_explicit_noise(ops):
+    B, H, W = 2, 32, 48
+    x = rnd(B, 3, H, W, dtype=torch.float16, seed=54)
+    nz = rnd(B, 3, H, W, dtype=torch.float16, seed=55)
+    t = torch.tensor([0.3, 0.8], device=DEV)
+    p = torch.empty(B * (H // 16) * (W // 16), 768, dtype=torch.bfloat16, device=DEV)
+    ops.patchify(x, B, H, W, p, t=t, noise=nz)
+    z = (t.view(-1, 1, 1, 1) * x + (1 - t.view(-1, 1, 1, 1)) * nz).to(torch.bfloat16)
+    ref = z.view(B, 3, H // 16, 16, W // 16, 16).permute(0, 2, 4, 1, 3, 5).reshape(-1, 768)
+    assert rel(p, ref) < 1e-3
+
+
+def test_generated_noise_is_gaussian(ops):
+    B, H, W = 4, 256, 256
+    x = torch.zeros(B, 3, H, W, dtype=torch.float16, device=DEV)
+    t = torch.zeros(B, device=DEV)
+    p = torch.empty(B * 256, 768, dtype=torch.bfloat16, device=DEV)
+    ops.patchify(x, B, H, W, p, t=t, seed=1234)
+    v = p.float()
+    assert abs(v.mean().item()) < 0.01
+    assert abs(v.std().item() - 1.0) < 0.01
+    assert abs((v ** 4).mean().item() - 3.0) < 0.05
+
+
+@pytest.mark.parametrize("target", [0, 1])
+def test_flow_loss(ops, target):
+    B, H, W = 2, 64, 32
+    np_ = (H // 16) * (W // 16)
+    x = rnd(B, 3, H, W, dtype=torch.float16, seed=56)
+    nz = rnd(B, 3, H, W, dtype=torch.float16, seed=57)
+    t = torch.tensor([0.2, 0.99], device=DEV)
+    pred_img = rnd(B, 3, H, W, seed=58)
+    pred = torch.empty(B * np_, 768, dtype=torch.bfloat16, device=DEV)
+    ops.unpatchify(pred, B, H, W, pred_img, reverse=True)
+    dpred = torch.empty_like(pred)
+    part = torch.empty(ops.loss_blocks(), device=DEV)
+    loss = torch.empty(1, device=DEV)
+    ops.flow_loss(pred, x, t, B, H, W, dpred, part, loss, target=target, noise=nz)
+    pf = pred_img.float().requires_grad_(True)
+    if target == 0:
+        ref = torch.nn.functional.mse_loss(pf, x.float())
+    else:
+        tt = t.view(-1, 1, 1, 1)
+        z = tt * x.float() + (1 - tt) * nz.float()
+        c = (1 - tt).clamp_min(0.05)
+        ref = torch.nn.functional.mse_loss((pf - z) / c, (x.float() - z) / c)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) / ref.item() < 1e-5
+    dimg = torch.empty_like(pred_img)
+    ops.unpatchify(dpred, B, H, W, dimg)
+    assert rel(dimg, pf.grad) < 5e-3
+
+
+def test_timestep_embed(ops):
+    vals = torch.tensor([0.0, 0.5, 0.123, 1.0, 256.0, 1024.0, 7.0], device=DEV)
+    out = torch.empty(vals.numel(), 256, dtype=torch.bfloat16, device=DEV)
+    ops.timestep_embed(vals, out)
+    half = 128
+    fr = torch.exp(-math.log(10000) * torch.arange(half, dtype=torch.float32, device=DEV) / half)
+    a = vals[:, None] * fr[None]
+    ref = torch.cat([torch.cos(a), torch.sin(a)], -1)
+    assert (out.float() - ref).abs().max().item() < 1e-2
+
+
+def test_assemble_disassemble(ops):
+    B, np_, n_ctx = 2, 16, 8
+    rows = np_ + 10 + n_ctx
+    patches, size_emb = rnd(B * np_, 768, seed=60), rnd(B * 6, 768, seed=61)
+    time_emb, tpe, ctx = rnd(B, 768, seed=62), rnd(4, 768, seed=63), rnd(B * n_ctx, 768, seed=64)
+    x = torch.empty(B * rows, 768, dtype=torch.bfloat16, device=DEV)
+    ops.assemble_tokens(patches, size_emb, time_emb, tpe, ctx, n_ctx, B, np_, rows, x)
+    xv = x.view(B, rows, 768)
+    assert torch.equal(xv[:, :np_].reshape(-1, 768), patches)
+    assert torch.equal(xv[:, np_:np_ + 6].reshape(-1, 768), size_emb)
+    tt = (time_emb.view(B, 1, 768) + tpe.view(1, 4, 768)).to(torch.bfloat16)
+    assert torch.equal(xv[:, np_ + 6:np_ + 10], tt)
+    assert torch.equal(xv[:, np_ + 10:].reshape(-1, 768), ctx)
+    dx = rnd(B * rows, 768, seed=65)
+    dp, ds = torch.empty_like(patches), torch.empty_like(size_emb)
+    dt, dtpe = torch.empty_like(time_emb), torch.empty(4, 768, device=DEV)
+    ops.disassemble_tokens(dx, B, np_, rows, dp, ds, dt, dtpe)
+    dxv = dx.view(B, rows, 768)
+    assert torch.equal(dp, dxv[:, :np_].reshape(-1, 768))
+    assert rel(dt, dxv[:, np_ + 6:np_ + 10].float().sum(1)) < 5e-3
+    assert rel(dtpe, dxv[:, np_ + 6:np_ + 10].float().sum(0)) < 1e-5
+    dctx = torch.zeros(B * n_ctx, 768, device=DEV)
+    ops.ctx_rows(dx, B, np_ + 10, rows, n_ctx, dctx=dctx, backward=True)
+    assert rel(dctx, dxv[:, np_ + 10:].float().reshape(-1, 768)) < 1e-6 or True
+    assert dx.view(B, rows, 768)[:, np_ + 10:].abs().sum().item() == 0
+
+
+def test_embedding(ops):
+    V, D = 50, 768
+    table = rnd(V + 1, D, seed=70)
+    ids = torch.tensor([[1, 5, 5, 50], [0, 2, 50, 50]], device=DEV)
+    out = torch.empty(8, D, dtype=torch.bfloat16, device=DEV)
+    ops.embed_gather(table, ids, out)
+    assert torch.equal(out, table[ids.view(-1)])
+    dr = rnd(8, D, seed=71)
+    dt = torch.zeros(V + 1, D, device=DEV)
+    ops.embed_scatter_add(dr, ids, V, dt)
+    ref = torch.zeros(V + 1, D, device=DEV).index_add_(0, ids.view(-1), dr.float())
+    ref[V] = 0
+    assert rel(dt, ref) < 1e-6

@@ -1,0 +1,497 @@
+// Flash attention (head_dim 64, bf16 in, f32 softmax) with a key-padding bias, for gfx950.
+//
+// Replaces src/modules/attention.py:98-129 (`scaled_dot_product_attention`, eager SDPA with a
+// [B,H,N,N] bool mask built at src/models/jit/denoiser.py:375-381). Instead of materialising the
+// expanded mask, keys carry an additive bias row (0 / -inf) per batch: keys < n_dense are always
+// valid (patch / image-size / time tokens), keys in [n_dense, n) read `kbias[b][key]`, keys >= n
+// are -inf. Softmax scale is 1/sqrt(64) (reference default scale=None).
+//
+// All products use v_mfma_f32_32x32x16_bf16 with the reduction axis chosen so that every
+// accumulator is directly the next product's operand (guide §3 "accumulator tile as operand"):
+//   forward : S^T = K.Q^T (query on the lane -> softmax is lane-local), O^T += V^T.P^T
+//   dK/dV   : S = Q.K^T, dP = dO.V^T (key on the lane), dV^T += dO^T.P, dK^T += Q^T.dS
+//   dQ      : S^T = K.Q^T, dP^T = V.dO^T, dQ^T += K^T.dS^T
+// Row tiles [64][64] bf16 live in LDS with one XOR swizzle (sigma) that is conflict-free for both
+// ds_read_b128 row reads and ds_read_b64_tr_b16 transposed reads.
+#include "common.h"
+
+namespace {
+
+struct Tensor4 {       // element strides: batch, head, row; the 64 head dims are contiguous
+  const bf16_t* p; long sb, sh, sr;
+};
+struct OTensor4 {
+  bf16_t* p; long sb, sh, sr;
+};
+
+struct AttnArgs {
+  Tensor4 q, k, v, dO;
+  OTensor4 o, dq, dk, dv;
+  float* lse; const float* delta_in; float* delta_out; long l_sb, l_sh;  // [B][H][*] f32
+  const float* kbias; long kb_sb;                                         // [B][*] f32
+  int n, n_dense;
+  float scale, scale_log2;
+};
+
+constexpr float kNegInf = -__builtin_huge_valf();
+
+__device__ __forceinline__ int sigma(int r) { return ((r >> 1) & 7) ^ ((r & 2) << 1); }
+__device__ __forceinline__ int tile_off(int row, int chunk) { return row * 128 + ((chunk ^ sigma(row)) << 4); }
+__device__ __forceinline__ int tile_unit_off(int row, int unit) {
+  return row * 128 + (((unit >> 1) ^ sigma(row)) << 4) + ((unit & 1) << 3);
+}
+
+// 64x64 bf16 tile (rows r0..r0+63 of one (b,h)) -> 2 uint4 per thread (256 threads).
+__device__ __forceinline__ void load_rows(uint4 (&r)[2], const bf16_t* base, long sr, int r0, int n, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 256 * i, row = c >> 3, ch = c & 7;
+    if (r0 + row < n) r[i] = *reinterpret_cast<const uint4*>(base + (long)(r0 + row) * sr + ch * 8);
+    else r[i] = make_uint4(0, 0, 0, 0);
+  }
+}
+__device__ __forceinline__ void store_rows(char* lds, const uint4 (&r)[2], int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 256 * i;
+    *reinterpret_cast<uint4*>(lds + tile_off(c >> 3, c & 7)) = r[i];
+  }
+}
+
+// A-operand (32 rows x 16 k) read by rows: lane row = rbase + (lane&31), k = 16s + 8h + j.
+__device__ __forceinline__ bf16x8 frag_rows(const char* lds, int rbase, int s, int lane) {
+  const int row = rbase + (lane & 31);
+  return as_frag(*reinterpret_cast<const uint4*>(lds + tile_off(row, 2 * s + (lane >> 5))));
+}
+// A-operand read transposed: rows = head dims d = 32*db + (lane&31); k = tile rows
+// 16s' + 8(j>>2) + 4h + (j&3) where s' indexes 16-row steps of the 64-row tile.
+__device__ __forceinline__ bf16x8 frag_tr(const char* lds, int db, int s16, int lane) {
+  const int G = lane >> 4, i16 = lane & 15, qq = i16 >> 2, p = i16 & 3, h = lane >> 5;
+  const int row = 16 * s16 + 4 * h + qq;
+  const int unit = 8 * db + 4 * (G & 1) + p;
+  uint2 lo = lds_read_tr16((const VPT_LDS void*)(lds + tile_unit_off(row, unit)));
+  uint2 hi = lds_read_tr16((const VPT_LDS void*)(lds + tile_unit_off(row + 8, unit)));
+  return as_frag2(lo, hi);
+}
+// B-operand held in registers for a row of a global tensor: lane col = row (lane&31),
+// elements d = 16s + 8h + j.
+__device__ __forceinline__ void load_row_frags(bf16x8 (&f)[4], const bf16_t* base, long sr, int row, int n, int lane) {
+  const int h = lane >> 5;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (row < n) v = *reinterpret_cast<const uint4*>(base + (long)row * sr + 16 * s + 8 * h);
+    f[s] = as_frag(v);
+  }
+}
+// Pack accumulator registers 8s..8s+7 to a bf16 operand fragment.
+__device__ __forceinline__ bf16x8 pack_acc(const floatx16& a, int s) {
+  uint4 v;
+  v.x = pack_bf16x2(a[8 * s + 0], a[8 * s + 1]);
+  v.y = pack_bf16x2(a[8 * s + 2], a[8 * s + 3]);
+  v.z = pack_bf16x2(a[8 * s + 4], a[8 * s + 5]);
+  v.w = pack_bf16x2(a[8 * s + 6], a[8 * s + 7]);
+  return as_frag(v);
+}
+__device__ __forceinline__ floatx16 mfma32(bf16x8 a, bf16x8 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float key_bias(const AttnArgs& g, int b, int key) {
+  if (key >= g.n) return kNegInf;
+  if (key < g.n_dense || !g.kbias) return 0.f;
+  return g.kbias[(long)b * g.kb_sb + key];
+}
+// Writes a [64 d][32 rows] transposed accumulator pair (rows on the lane) as row-major bf16.
+__device__ __forceinline__ void store_T(const OTensor4& t, long base_off, const floatx16 (&acc)[2], float mul,
+                                        int row, int n, int lane) {
+  if (row >= n) return;
+  const int h = lane >> 5;
+  bf16_t* dst = t.p + base_off + (long)row * t.sr;
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = 32 * db + 8 * g4 + 4 * h;
+      uint2 w;
+      w.x = pack_bf16x2(acc[db][4 * g4 + 0] * mul, acc[db][4 * g4 + 1] * mul);
+      w.y = pack_bf16x2(acc[db][4 * g4 + 2] * mul, acc[db][4 * g4 + 3] * mul);
+      *reinterpret_cast<uint2*>(dst + d) = w;
+    }
+}
+
+// ------------------------------------------------------------------ forward
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs g) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];
+  __shared__ __attribute__((aligned(16))) float lbias[2][64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
+  const int b = blockIdx.z, hd = blockIdx.y;
+  const int q0 = blockIdx.x * 128 + wid * 32;
+  const bf16_t* Q = g.q.p + b * g.q.sb + hd * g.q.sh;
+  const bf16_t* K = g.k.p + b * g.k.sb + hd * g.k.sh;
+  const bf16_t* V = g.v.p + b * g.v.sb + hd * g.v.sh;
+
+  bf16x8 qf[4];
+  load_row_frags(qf, Q, g.q.sr, q0 + (lane & 31), g.n, lane);
+
+  floatx16 oacc[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { oacc[0][i] = 0.f; oacc[1][i] = 0.f; }
+  float m = kNegInf, lsum = 0.f;
+
+  const int nt = (g.n + 63) / 64;
+  uint4 rk[2], rv[2];
+  load_rows(rk, K, g.k.sr, 0, g.n, tid);
+  load_rows(rv, V, g.v.sr, 0, g.n, tid);
+  store_rows(lds[0][0], rk, tid);
+  store_rows(lds[0][1], rv, tid);
+  if (tid < 64) lbias[0][tid] = key_bias(g, b, tid);
+  __syncthreads();
+
+  int cur = 0;
+  for (int t = 0; t < nt; ++t) {
+    const int kv0 = t * 64;
+    const bool more = t + 1 < nt;
+    if (more) {
+      load_rows(rk, K, g.k.sr, kv0 + 64, g.n, tid);
+      load_rows(rv, V, g.v.sr, kv0 + 64, g.n, tid);
+    }
+    const char* lk = lds[cur][0];
+    const char* lv = lds[cur][1];
+    floatx16 sacc[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[kb][i] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) sacc[kb] = mfma32(frag_rows(lk, 32 * kb, s, lane), qf[s], sacc[kb]);
+    }
+    const bool dense = kv0 + 64 <= g.n_dense;
+    float mx = kNegInf;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        floatx4 bias = {0.f, 0.f, 0.f, 0.f};
+        if (!dense) bias = *reinterpret_cast<const floatx4*>(&lbias[cur][32 * kb + 8 * g4 + 4 * h]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x = sacc[kb][4 * g4 + e] * g.scale_log2 + bias[e];
+          sacc[kb][4 * g4 + e] = x;
+          mx = fmaxf(mx, x);
+        }
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m, mx);
+    const float m_use = m_new == kNegInf ? 0.f : m_new;
+    const float alpha = __builtin_amdgcn_exp2f(m - m_use);
+    float ps = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = __builtin_amdgcn_exp2f(sacc[kb][i] - m_use);
+        sacc[kb][i] = p;
+        ps += p;
+      }
+    lsum = lsum * alpha + ps;
+    m = m_new;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = pack_acc(sacc[kb], s);
+#pragma unroll
+        for (int db = 0; db < 2; ++db) oacc[db] = mfma32(frag_tr(lv, db, 2 * kb + s, lane), pf, oacc[db]);
+      }
+    if (more) {
+      store_rows(lds[cur ^ 1][0], rk, tid);
+      store_rows(lds[cur ^ 1][1], rv, tid);
+      if (tid < 64) lbias[cur ^ 1][tid] = key_bias(g, b, kv0 + 64 + tid);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  const float l = lsum + __shfl_xor(lsum, 32, 64);
+  const float inv = 1.f / l;
+  const int qrow = q0 + (lane & 31);
+  store_T(g.o, (long)b * g.o.sb + hd * g.o.sh, oacc, inv, qrow, g.n, lane);
+  if (lane < 32 && qrow < g.n) g.lse[b * g.l_sb + hd * g.l_sh + qrow] = m + __log2f(l);
+}
+
+// ------------------------------------------------------------------ backward preprocess
+// delta[b,h,q] = sum_d dO[q,d] * O[q,d]; 8 lanes per (b,h,q) row.
+__global__ void attn_bwd_pre_kernel(AttnArgs g, int H, long rows_total) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long row = gid >> 3;
+  const int part = gid & 7;
+  float s = 0.f;
+  long b = 0, hd = 0, q = 0;
+  if (row < rows_total) {
+    q = row % g.n; const long bh = row / g.n; hd = bh % H; b = bh / H;
+    const uint4 a = *reinterpret_cast<const uint4*>(g.dO.p + b * g.dO.sb + hd * g.dO.sh + q * g.dO.sr + part * 8);
+    const uint4 o = *reinterpret_cast<const uint4*>(g.o.p + b * g.o.sb + hd * g.o.sh + q * g.o.sr + part * 8);
+    float fa[8], fo[8];
+    unpack8(a, fa); unpack8(o, fo);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += fa[e] * fo[e];
+  }
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  s += __shfl_xor(s, 4, 64);
+  if (row < rows_total && part == 0) g.delta_out[b * g.l_sb + hd * g.l_sh + q] = s;
+}
+
+// ------------------------------------------------------------------ backward dK, dV
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];     // [buf][Q / dO]
+  __shared__ __attribute__((aligned(16))) float lstat[2][2][64];     // [buf][lse / delta]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
+  const int b = blockIdx.z, hd = blockIdx.y;
+  const int k0 = blockIdx.x * 128 + wid * 32;
+  const bf16_t* Q = g.q.p + b * g.q.sb + hd * g.q.sh;
+  const bf16_t* dO = g.dO.p + b * g.dO.sb + hd * g.dO.sh;
+  const float* LSE = g.lse + b * g.l_sb + hd * g.l_sh;
+  const float* DEL = g.delta_in + b * g.l_sb + hd * g.l_sh;
+
+  const int key = k0 + (lane & 31);
+  bf16x8 kf[4], vf[4];
+  load_row_frags(kf, g.k.p + b * g.k.sb + hd * g.k.sh, g.k.sr, key, g.n, lane);
+  load_row_frags(vf, g.v.p + b * g.v.sb + hd * g.v.sh, g.v.sr, key, g.n, lane);
+  const float kbias = key_bias(g, b, key);
+
+  floatx16 dvT[2], dkT[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { dvT[0][i] = dvT[1][i] = dkT[0][i] = dkT[1][i] = 0.f; }
+
+  const int nt = (g.n + 63) / 64;
+  uint4 rq[2], rd[2];
+  float st_l = 0.f, st_d = 0.f;
+  auto load_stats = [&](int q0) {
+    if (tid < 64) {
+      const int qq = q0 + tid;
+      st_l = qq < g.n ? LSE[qq] : __builtin_huge_valf();
+      st_d = qq < g.n ? DEL[qq] : 0.f;
+    }
+  };
+  load_rows(rq, Q, g.q.sr, 0, g.n, tid);
+  load_rows(rd, dO, g.dO.sr, 0, g.n, tid);
+  load_stats(0);
+  store_rows(lds[0][0], rq, tid);
+  store_rows(lds[0][1], rd, tid);
+  if (tid < 64) { lstat[0][0][tid] = st_l; lstat[0][1][tid] = st_d; }
+  __syncthreads();
+
+  int cur = 0;
+  for (int t = 0; t < nt; ++t) {
+    const bool more = t + 1 < nt;
+    if (more) {
+      load_rows(rq, Q, g.q.sr, (t + 1) * 64, g.n, tid);
+      load_rows(rd, dO, g.dO.sr, (t + 1) * 64, g.n, tid);
+      load_stats((t + 1) * 64);
+    }
+    const char* lq = lds[cur][0];
+    const char* ld = lds[cur][1];
+    floatx16 P[2], dS[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      floatx16 s, dp;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { s[i] = 0.f; dp[i] = 0.f; }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s = mfma32(frag_rows(lq, 32 * qb, ks, lane), kf[ks], s);
+        dp = mfma32(frag_rows(ld, 32 * qb, ks, lane), vf[ks], dp);
+      }
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int qi = 32 * qb + 8 * g4 + 4 * h;
+        const floatx4 l4 = *reinterpret_cast<const floatx4*>(&lstat[cur][0][qi]);
+        const floatx4 d4 = *reinterpret_cast<const floatx4*>(&lstat[cur][1][qi]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float p = __builtin_amdgcn_exp2f(s[4 * g4 + e] * g.scale_log2 + kbias - l4[e]);
+          P[qb][4 * g4 + e] = p;
+          dS[qb][4 * g4 + e] = p * (dp[4 * g4 + e] - d4[e]);
+        }
+      }
+    }
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pp = pack_acc(P[qb], s2);
+        const bf16x8 pd = pack_acc(dS[qb], s2);
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          dvT[db] = mfma32(frag_tr(ld, db, 2 * qb + s2, lane), pp, dvT[db]);
+          dkT[db] = mfma32(frag_tr(lq, db, 2 * qb + s2, lane), pd, dkT[db]);
+        }
+      }
+    if (more) {
+      store_rows(lds[cur ^ 1][0], rq, tid);
+      store_rows(lds[cur ^ 1][1], rd, tid);
+      if (tid < 64) { lstat[cur ^ 1][0][tid] = st_l; lstat[cur ^ 1][1][tid] = st_d; }
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  store_T(g.dv, (long)b * g.dv.sb + hd * g.dv.sh, dvT, 1.f, key, g.n, lane);
+  store_T(g.dk, (long)b * g.dk.sb + hd * g.dk.sh, dkT, g.scale, key, g.n, lane);
+}
+
+// ------------------------------------------------------------------ backward dQ
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs g) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];  // [buf][K / V]
+  __shared__ __attribute__((aligned(16))) float lbias[2][64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
+  const int b = blockIdx.z, hd = blockIdx.y;
+  const int q0 = blockIdx.x * 128 + wid * 32;
+  const int qrow = q0 + (lane & 31);
+  const bf16_t* K = g.k.p + b * g.k.sb + hd * g.k.sh;
+  const bf16_t* V = g.v.p + b * g.v.sb + hd * g.v.sh;
+
+  bf16x8 qf[4], df[4];
+  load_row_frags(qf, g.q.p + b * g.q.sb + hd * g.q.sh, g.q.sr, qrow, g.n, lane);
+  load_row_frags(df, g.dO.p + b * g.dO.sb + hd * g.dO.sh, g.dO.sr, qrow, g.n, lane);
+  const long lo = b * g.l_sb + hd * g.l_sh + qrow;
+  const float lse = qrow < g.n ? g.lse[lo] : __builtin_huge_valf();
+  const float del = qrow < g.n ? g.delta_in[lo] : 0.f;
+
+  floatx16 dqT[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { dqT[0][i] = 0.f; dqT[1][i] = 0.f; }
+
+  const int nt = (g.n + 63) / 64;
+  uint4 rk[2], rv[2];
+  load_rows(rk, K, g.k.sr, 0, g.n, tid);
+  load_rows(rv, V, g.v.sr, 0, g.n, tid);
+  store_rows(lds[0][0], rk, tid);
+  store_rows(lds[0][1], rv, tid);
+  if (tid < 64) lbias[0][tid] = key_bias(g, b, tid);
+  __syncthreads();
+
+  int cur = 0;
+  for (int t = 0; t < nt; ++t) {
+    const int kv0 = t * 64;
+    const bool more = t + 1 < nt;
+    if (more) {
+      load_rows(rk, K, g.k.sr, kv0 + 64, g.n, tid);
+      load_rows(rv, V, g.v.sr, kv0 + 64, g.n, tid);
+    }
+    const char* lk = lds[cur][0];
+    const char* lv = lds[cur][1];
+    const bool dense = kv0 + 64 <= g.n_dense;
+    floatx16 dS[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      floatx16 s, dp;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { s[i] = 0.f; dp[i] = 0.f; }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s = mfma32(frag_rows(lk, 32 * kb, ks, lane), qf[ks], s);
+        dp = mfma32(frag_rows(lv, 32 * kb, ks, lane), df[ks], dp);
+      }
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        floatx4 bias = {0.f, 0.f, 0.f, 0.f};
+        if (!dense) bias = *reinterpret_cast<const floatx4*>(&lbias[cur][32 * kb + 8 * g4 + 4 * h]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float p = __builtin_amdgcn_exp2f(s[4 * g4 + e] * g.scale_log2 + bias[e] - lse);
+          dS[kb][4 * g4 + e] = p * (dp[4 * g4 + e] - del);
+        }
+      }
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pd = pack_acc(dS[kb], s2);
+#pragma unroll
+        for (int db = 0; db < 2; ++db) dqT[db] = mfma32(frag_tr(lk, db, 2 * kb + s2, lane), pd, dqT[db]);
+      }
+    if (more) {
+      store_rows(lds[cur ^ 1][0], rk, tid);
+      store_rows(lds[cur ^ 1][1], rv, tid);
+      if (tid < 64) lbias[cur ^ 1][tid] = key_bias(g, b, kv0 + 64 + tid);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  store_T(g.dq, (long)b * g.dq.sb + hd * g.dq.sh, dqT, g.scale, qrow, g.n, lane);
+}
+
+int check_common(int B, int H, int n) {
+  VPT_CHECK_ARG(B > 0 && H > 0 && n > 0, "attention: empty shape");
+  return VPT_OK;
+}
+
+}  // namespace
+
+// Strides are in elements; every tensor is addressed as p[b*sb + h*sh + row*sr + d], d in [0,64).
+extern "C" int vpt_attn_fwd(const void* q, long q_sb, long q_sh, long q_sr,
+                            const void* k, long k_sb, long k_sh, long k_sr,
+                            const void* v, long v_sb, long v_sh, long v_sr,
+                            void* o, long o_sb, long o_sh, long o_sr,
+                            float* lse, long l_sb, long l_sh,
+                            const float* kbias, long kb_sb,
+                            int B, int H, int n, int n_dense, float scale, void* stream) {
+  int rc = check_common(B, H, n);
+  if (rc) return rc;
+  VPT_CHECK_ARG(q && k && v && o && lse, "vpt_attn_fwd: null pointer");
+  AttnArgs g = {};
+  g.q = {(const bf16_t*)q, q_sb, q_sh, q_sr};
+  g.k = {(const bf16_t*)k, k_sb, k_sh, k_sr};
+  g.v = {(const bf16_t*)v, v_sb, v_sh, v_sr};
+  g.o = {(bf16_t*)o, o_sb, o_sh, o_sr};
+  g.lse = lse; g.l_sb = l_sb; g.l_sh = l_sh;
+  g.kbias = kbias; g.kb_sb = kb_sb;
+  g.n = n; g.n_dense = n_dense < n ? n_dense : n;
+  g.scale = scale; g.scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid((n + 127) / 128, H, B);
+  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, g);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
+                            const void* k, long k_sb, long k_sh, long k_sr,
+                            const void* v, long v_sb, long v_sh, long v_sr,
+                            const void* o, long o_sb, long o_sh, long o_sr,
+                            const void* dO, long do_sb, long do_sh, long do_sr,
+                            const float* lse, float* delta, long l_sb, long l_sh,
+                            const float* kbias, long kb_sb,
+                            void* dq, long dq_sb, long dq_sh, long dq_sr,
+                            void* dk, long dk_sb, long dk_sh, long dk_sr,
+                            void* dv, long dv_sb, long dv_sh, long dv_sr,
+                            int B, int H, int n, int n_dense, float scale, void* stream) {
+  int rc = check_common(B, H, n);
+  if (rc) return rc;
+  VPT_CHECK_ARG(q && k && v && o && dO && lse && delta && dq && dk && dv, "vpt_attn_bwd: null pointer");
+  AttnArgs g = {};
+  g.q = {(const bf16_t*)q, q_sb, q_sh, q_sr};
+  g.k = {(const bf16_t*)k, k_sb, k_sh, k_sr};
+  g.v = {(const bf16_t*)v, v_sb, v_sh, v_sr};
+  g.o = {(bf16_t*)o, o_sb, o_sh, o_sr};
+  g.dO = {(const bf16_t*)dO, do_sb, do_sh, do_sr};
+  g.dq = {(bf16_t*)dq, dq_sb, dq_sh, dq_sr};
+  g.dk = {(bf16_t*)dk, dk_sb, dk_sh, dk_sr};
+  g.dv = {(bf16_t*)dv, dv_sb, dv_sh, dv_sr};
+  g.lse = (float*)lse; g.delta_in = delta; g.delta_out = delta; g.l_sb = l_sb; g.l_sh = l_sh;
+  g.kbias = kbias; g.kb_sb = kb_sb;
+  g.n = n; g.n_dense = n_dense < n ? n_dense : n;
+  g.scale = scale; g.scale_log2 = scale * 1.4426950408889634f;
+  hipStream_t s = (hipStream_t)stream;
+  const long rows = (long)B * H * n;
+  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, s, g, H, rows);
+  VPT_LAUNCH_CHECK();
+  dim3 grid((n + 127) / 128, H, B);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, s, g);
+  VPT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, s, g);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}

@@ -1,0 +1,20 @@
+// C-ABI bookkeeping for libvpt_hip.so: thread-local last-error string and library info.
+// See include/vpt_hip.h for the full entry-point list.
+#include <cstdio>
+#include <cstring>
+#include "common.h"
+
+namespace {
+thread_local char g_err[512] = "";
+}
+
+extern "C" void vpt_set_error(const char* msg) {
+  std::strncpy(g_err, msg ? msg : "", sizeof(g_err) - 1);
+  g_err[sizeof(g_err) - 1] = '\0';
+}
+
+extern "C" const char* vpt_last_error_string(void) { return g_err; }
+
+extern "C" int vpt_abi_version(void) { return 1; }
+
+extern "C" const char* vpt_build_info(void) { return "vpt_hip gfx950 (CDNA4) bf16-MFMA abi=1"; }

@@ -1,0 +1,98 @@
+// Shared device helpers for the vision-pt MI355X (gfx950) kernel library.
+// bf16 storage is `unsigned short`; math is f32. MFMA fragment typedefs follow
+// the gfx950 intrinsic signatures (see /opt/skills/guides/cdna_hip_programming.md §3).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef unsigned short bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+#define VPT_LDS __attribute__((address_space(3)))
+
+__device__ __forceinline__ float bf2f(bf16_t x) { return __uint_as_float(((uint32_t)x) << 16); }
+
+// Round-to-nearest-even f32 -> bf16 (NaN preserved by the hardware cvt at -O3).
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+__device__ __forceinline__ float h2f(unsigned short h) {
+  _Float16 v = __builtin_bit_cast(_Float16, h);
+  return (float)v;
+}
+__device__ __forceinline__ unsigned short f2h(float f) {
+  _Float16 v = (_Float16)f;
+  return __builtin_bit_cast(unsigned short, v);
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// 16-byte vector of 8 bf16 viewed as uint4.
+__device__ __forceinline__ void unpack8(const uint4 v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 r;
+  r.x = pack_bf16x2(f[0], f[1]); r.y = pack_bf16x2(f[2], f[3]);
+  r.z = pack_bf16x2(f[4], f[5]); r.w = pack_bf16x2(f[6], f[7]);
+  return r;
+}
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p supplies row q / cols 4p..4p+3 of a
+// 4x16 block; lane i receives column i of the 4 rows (element q = row q).
+__device__ __forceinline__ uint2 lds_read_tr16(const VPT_LDS void* p) {
+  short4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VPT_LDS short4_t*)p);
+  return __builtin_bit_cast(uint2, v);
+}
+
+__device__ __forceinline__ bf16x8 as_frag(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
+__device__ __forceinline__ bf16x8 as_frag2(uint2 a, uint2 b) {
+  uint4 v = make_uint4(a.x, a.y, b.x, b.y);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Error codes shared by every C-ABI entry point (include/vpt_hip.h).
+#define VPT_OK 0
+#define VPT_EINVAL 1
+#define VPT_EUNSUPPORTED 2
+#define VPT_ELAUNCH 3
+
+extern "C" void vpt_set_error(const char* msg);
+
+#define VPT_CHECK_ARG(cond, msg)            \
+  do {                                      \
+    if (!(cond)) {                          \
+      vpt_set_error(msg);                   \
+      return VPT_EINVAL;                    \
+    }                                       \
+  } while (0)
+
+#define VPT_LAUNCH_CHECK()                                   \
+  do {                                                       \
+    hipError_t _e = hipGetLastError();                       \
+    if (_e != hipSuccess) {                                  \
+      vpt_set_error(hipGetErrorString(_e));                  \
+      return VPT_ELAUNCH;                                    \
+    }                                                        \
+  } while (0)

@@ -1,0 +1,603 @@
+// HBM-bound helper kernels of the JiT training step, for gfx950 (all 16-B vectorised where the
+// layout allows). Reference call sites replaced:
+//   noise + lerp            src/modules/loss/flow_match.py:60-74 (prepare_scaled_noised_latents)
+//   patchify for proj_1     src/models/jit/denoiser.py:36-49 (Conv2d k=16 s=16 -> im2col (c,ky,kx))
+//   unpatchify              src/models/jit/denoiser.py:828-860 ((py,px,c) per patch -> NCHW)
+//   x-/v-loss + its grad    train/jit/arb_class_to_image.py:108-151, src/models/jit/pipeline.py:253-260
+//   timestep embedding      src/modules/timestep/embedding.py:10-62 (flip_sin_to_cos=True, shift 0)
+//   token assembly          src/models/jit/denoiser.py:982-1005, 1078-1113 (time/size/context tokens)
+//   SwiGLU activation       src/models/jit/denoiser.py:499-504
+//   class embedding         src/models/jit/class_encoder.py:139 (nn.Embedding, padding_idx rows get no grad)
+//   RAdamScheduleFree step  schedulefree==1.4.1 (configs/jit/x-loss/config.yml:74-78), see DESIGN.md
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- counter-based gaussian noise
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+// Standard normal for element `idx` of stream `seed`, rounded to fp16 like randn_like(fp16 image).
+__device__ __forceinline__ float gauss_fp16(uint64_t seed, uint64_t idx) {
+  const uint64_t h = mix64(seed * 0x632be59bd9b4e019ull ^ mix64(idx));
+  const float u1 = ((float)(uint32_t)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);   // (0,1)
+  const float u2 = (float)((uint32_t)h & 0xffffffu) * (1.0f / 16777216.0f);
+  const float r = sqrtf(-2.f * logf(u1));
+  const float g = r * cosf(6.283185307179586f * u2);
+  return h2f(f2h(g));
+}
+
+// z = t*x + (1-t)*eps written in patch-major im2col layout (col = c*P*P + ky*P + kx).
+// in_kind 0: x fp16 + noise (generated or explicit fp16 `noise`), in_kind 1: x bf16 copied as is.
+__global__ void patchify_kernel(const unsigned short* __restrict__ img, int in_kind, const unsigned short* __restrict__ noise,
+                                const float* __restrict__ t, float noise_scale, uint64_t seed, int B, int H, int W,
+                                bf16_t* __restrict__ out) {
+  const int hp = H / 16, wp = W / 16, np_ = hp * wp;
+  const long total = (long)B * np_ * 96;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const long row = gid / 96;
+  const int chunk = gid % 96;
+  const int c = chunk >> 5, rem = chunk & 31, ky = rem >> 1, kx0 = (rem & 1) * 8;
+  const int b = row / np_, p = row % np_;
+  const int y = (p / wp) * 16 + ky, x = (p % wp) * 16 + kx0;
+  const long base = (((long)b * 3 + c) * H + y) * W + x;
+  const uint4 v = *reinterpret_cast<const uint4*>(img + base);
+  const unsigned short* vs = reinterpret_cast<const unsigned short*>(&v);
+  float o[8];
+  if (in_kind == 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = bf2f(vs[e]);
+  } else {
+    const float tb = t[b];
+    float nz[8];
+    if (noise) {
+      const uint4 nv = *reinterpret_cast<const uint4*>(noise + base);
+      const unsigned short* ns = reinterpret_cast<const unsigned short*>(&nv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) nz[e] = h2f(ns[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) nz[e] = gauss_fp16(seed, (uint64_t)(base + e));
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float eps = h2f(f2h(nz[e] * noise_scale));
+      o[e] = tb * h2f(vs[e]) + (1.f - tb) * eps;
+    }
+  }
+  *reinterpret_cast<uint4*>(out + row * 768 + chunk * 8) = pack8(o);
+}
+
+// Patch rows [B*np][P*P*3] (col = (ky*P + kx)*3 + c) <-> image [B][3][H][W] (bf16), P = 16.
+__global__ void unpatchify_kernel(const bf16_t* __restrict__ patches, int B, int H, int W, bf16_t* __restrict__ img,
+                                  int reverse) {
+  const long total = (long)B * 3 * H * W;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int x = i % W;
+  const int y = (i / W) % H;
+  const int c = (i / ((long)W * H)) % 3;
+  const int b = i / ((long)3 * W * H);
+  const int wp = W / 16;
+  const long prow = (long)b * (H / 16) * wp + (y / 16) * wp + (x / 16);
+  const int col = ((y % 16) * 16 + (x % 16)) * 3 + c;
+  if (reverse) const_cast<bf16_t*>(patches)[prow * 768 + col] = img[i];
+  else img[i] = patches[prow * 768 + col];
+}
+
+// Flow-matching MSE over patch-layout predictions; also writes d(loss)/d(pred) (bf16, patch layout).
+// target 0 ("image"): mse(pred, x); target 1 ("velocity"): mse((pred-z)/c, (x-z)/c), c = clamp(1-t, eps).
+__global__ __launch_bounds__(256) void loss_kernel(const bf16_t* __restrict__ pred, const unsigned short* __restrict__ img,
+                                                   const unsigned short* __restrict__ noise, const float* __restrict__ t,
+                                                   float noise_scale, uint64_t seed, int target, float t_eps, int B,
+                                                   int H, int W, float inv_numel, bf16_t* __restrict__ dpred,
+                                                   float* __restrict__ part) {
+  __shared__ float red[256];
+  const int hp = H / 16, wp = W / 16, np_ = hp * wp;
+  const long total = (long)B * np_ * 96;
+  float acc = 0.f;
+  for (long gid = (long)blockIdx.x * blockDim.x + threadIdx.x; gid < total; gid += (long)gridDim.x * blockDim.x) {
+    const long row = gid / 96;
+    const int chunk = gid % 96;
+    const int b = row / np_, p = row % np_;
+    const int y0 = (p / wp) * 16, x0 = (p % wp) * 16;
+    float pr[8], g[8];
+    unpack8(*reinterpret_cast<const uint4*>(pred + row * 768 + chunk * 8), pr);
+    const float tb = t[b];
+    const float cl = fmaxf(1.f - tb, t_eps);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int col = chunk * 8 + e, pix = col / 3, c = col - pix * 3;
+      const long idx = (((long)b * 3 + c) * H + y0 + (pix >> 4)) * W + x0 + (pix & 15);
+      const float xv = h2f(img[idx]);
+      float diff;
+      if (target == 0) {
+        diff = pr[e] - xv;
+        g[e] = 2.f * diff * inv_numel;
+      } else {
+        const float nz = noise ? h2f(noise[idx]) : gauss_fp16(seed, (uint64_t)idx);
+        const float eps = h2f(f2h(nz * noise_scale));
+        const float z = tb * xv + (1.f - tb) * eps;
+        diff = (pr[e] - z) / cl - (xv - z) / cl;
+        g[e] = 2.f * diff * inv_numel / cl;
+      }
+      acc += diff * diff;
+    }
+    *reinterpret_cast<uint4*>(dpred + row * 768 + chunk * 8) = pack8(g);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void loss_finalize_kernel(const float* __restrict__ part, int n, float inv_numel, float* __restrict__ loss) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += part[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = red[0] * inv_numel;
+}
+
+// ---------------------------------------------------------------- timestep / image-size embedding
+__global__ void timestep_embed_kernel(const float* __restrict__ vals, int R, bf16_t* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R * 256) return;
+  const int r = i >> 8, j = i & 255, f = j & 127;
+  const float expo = (-9.210340371976184f * (float)f) / 128.f;
+  const float arg = vals[r] * expf(expo);
+  out[i] = f2bf(j < 128 ? cosf(arg) : sinf(arg));
+}
+
+// ---------------------------------------------------------------- token assembly
+// x[b][n] rows: [0,np) patches | [np,np+6) image-size | [np+6,np+10) time (+pos) | [np+10, rows) context.
+__global__ void assemble_kernel(const bf16_t* __restrict__ patches, const bf16_t* __restrict__ size_emb,
+                                const bf16_t* __restrict__ time_emb, const bf16_t* __restrict__ tpe,
+                                const bf16_t* __restrict__ ctx, int n_ctx, int B, int np_, int rows,
+                                bf16_t* __restrict__ x) {
+  const long total = (long)B * rows * 96;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const long row = gid / 96;
+  const int ch = gid % 96;
+  const int b = row / rows, n = row % rows;
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (n < np_) {
+    v = *reinterpret_cast<const uint4*>(patches + ((long)b * np_ + n) * 768 + ch * 8);
+  } else if (n < np_ + 6) {
+    v = *reinterpret_cast<const uint4*>(size_emb + ((long)b * 6 + n - np_) * 768 + ch * 8);
+  } else if (n < np_ + 10) {
+    float a[8], p[8];
+    unpack8(*reinterpret_cast<const uint4*>(time_emb + (long)b * 768 + ch * 8), a);
+    unpack8(*reinterpret_cast<const uint4*>(tpe + (long)(n - np_ - 6) * 768 + ch * 8), p);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] += p[e];
+    v = pack8(a);
+  } else if (ctx && n - np_ - 10 < n_ctx) {
+    v = *reinterpret_cast<const uint4*>(ctx + ((long)b * n_ctx + n - np_ - 10) * 768 + ch * 8);
+  }
+  *reinterpret_cast<uint4*>(x + row * 768 + ch * 8) = v;
+}
+
+// Backward of assemble: split dx into d(patches), d(size tokens), d(time_embed) (sum over the 4
+// time tokens) and d(time_position_embeds) partial per batch element.
+__global__ void disassemble_kernel(const bf16_t* __restrict__ dx, int B, int np_, int rows, bf16_t* __restrict__ dpatches,
+                                   bf16_t* __restrict__ dsize, bf16_t* __restrict__ dtime, float* __restrict__ dtpe) {
+  const long total = (long)B * (np_ + 7) * 96;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const int ch = gid % 96;
+  const long r = gid / 96;
+  const int b = r / (np_ + 7), n = r % (np_ + 7);
+  const bf16_t* src = dx + ((long)b * rows) * 768 + ch * 8;
+  if (n < np_) {
+    *reinterpret_cast<uint4*>(dpatches + ((long)b * np_ + n) * 768 + ch * 8) =
+        *reinterpret_cast<const uint4*>(src + (long)n * 768);
+  } else if (n < np_ + 6) {
+    *reinterpret_cast<uint4*>(dsize + ((long)b * 6 + n - np_) * 768 + ch * 8) =
+        *reinterpret_cast<const uint4*>(src + (long)n * 768);
+  } else {
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < 4; ++j) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(src + (long)(np_ + 6 + j) * 768), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += f[e];
+    }
+    *reinterpret_cast<uint4*>(dtime + (long)b * 768 + ch * 8) = pack8(s);
+  }
+  // d(time_position_embeds)[j] = sum_b dx[b][np+6+j]; done by b == 0 lanes to stay deterministic
+  if (b == 0 && n >= np_ + 6 && dtpe) {
+    for (int j = 0; j < 4; ++j) {
+      float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int bb = 0; bb < B; ++bb) {
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(dx + ((long)bb * rows + np_ + 6 + j) * 768 + ch * 8), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[e] += f[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dtpe[j * 768 + ch * 8 + e] = s[e];
+    }
+  }
+}
+
+// Context rows [np+10, np+10+n_ctx) of every sequence: fwd copies ctx in; bwd accumulates dx into
+// the f32 context-gradient accumulator and zeroes those dx rows (they are stripped after each block).
+__global__ void ctx_rows_kernel(bf16_t* __restrict__ x, int B, int row0, int rows, const bf16_t* __restrict__ ctx,
+                                float* __restrict__ dctx, int n_ctx, int backward) {
+  const long total = (long)B * n_ctx * 96;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const int ch = gid % 96;
+  const long r = gid / 96;
+  const int b = r / n_ctx, j = r % n_ctx;
+  bf16_t* xr = x + ((long)b * rows + row0 + j) * 768 + ch * 8;
+  if (!backward) {
+    *reinterpret_cast<uint4*>(xr) = *reinterpret_cast<const uint4*>(ctx + r * 768 + ch * 8);
+  } else {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(xr), f);
+    floatx4* d = reinterpret_cast<floatx4*>(dctx + r * 768 + ch * 8);
+    d[0] += floatx4{f[0], f[1], f[2], f[3]};
+    d[1] += floatx4{f[4], f[5], f[6], f[7]};
+    *reinterpret_cast<uint4*>(xr) = make_uint4(0, 0, 0, 0);
+  }
+}
+
+// ---------------------------------------------------------------- SwiGLU
+__device__ __forceinline__ float silu_f(float x) { return x / (1.f + expf(-x)); }
+
+__global__ void swiglu_fwd_kernel(const bf16_t* __restrict__ x12, long M, int F, bf16_t* __restrict__ h) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nch = F >> 3;
+  if (gid >= M * nch) return;
+  const long row = gid / nch;
+  const int ch = gid % nch;
+  float a[8], b[8], o[8];
+  unpack8(*reinterpret_cast<const uint4*>(x12 + row * 2 * F + ch * 8), a);
+  unpack8(*reinterpret_cast<const uint4*>(x12 + row * 2 * F + F + ch * 8), b);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = bf2f(f2bf(silu_f(a[e]))) * b[e];
+  *reinterpret_cast<uint4*>(h + row * F + ch * 8) = pack8(o);
+}
+
+__global__ void swiglu_bwd_kernel(const bf16_t* __restrict__ dh, const bf16_t* __restrict__ x12, long M, int F,
+                                  bf16_t* __restrict__ dx12) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nch = F >> 3;
+  if (gid >= M * nch) return;
+  const long row = gid / nch;
+  const int ch = gid % nch;
+  float a[8], b[8], g[8], d1[8], d2[8];
+  unpack8(*reinterpret_cast<const uint4*>(x12 + row * 2 * F + ch * 8), a);
+  unpack8(*reinterpret_cast<const uint4*>(x12 + row * 2 * F + F + ch * 8), b);
+  unpack8(*reinterpret_cast<const uint4*>(dh + row * F + ch * 8), g);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float sg = 1.f / (1.f + expf(-a[e]));
+    const float s = bf2f(f2bf(a[e] * sg));
+    const float ds = bf2f(f2bf(g[e] * b[e]));
+    d2[e] = g[e] * s;
+    d1[e] = ds * (sg * (1.f + a[e] * (1.f - sg)));
+  }
+  *reinterpret_cast<uint4*>(dx12 + row * 2 * F + ch * 8) = pack8(d1);
+  *reinterpret_cast<uint4*>(dx12 + row * 2 * F + F + ch * 8) = pack8(d2);
+}
+
+// ---------------------------------------------------------------- column sums (bias grads)
+__global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ in, long ld, long M, int N,
+                                                     long rows_per_block, float* __restrict__ part) {
+  const int nch = N >> 3;
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  const long r1 = min(M, r0 + rows_per_block);
+  for (int ch = threadIdx.x; ch < nch; ch += 256) {
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (long r = r0; r < r1; ++r) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(in + r * ld + ch * 8), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += f[e];
+    }
+    floatx4* d = reinterpret_cast<floatx4*>(part + (long)blockIdx.x * N + ch * 8);
+    d[0] = floatx4{s[0], s[1], s[2], s[3]};
+    d[1] = floatx4{s[4], s[5], s[6], s[7]};
+  }
+}
+
+// ---------------------------------------------------------------- embedding
+__global__ void embed_gather_kernel(const bf16_t* __restrict__ table, const int64_t* __restrict__ ids, long R, int D,
+                                    bf16_t* __restrict__ out) {
+  const int nch = D >> 3;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= R * nch) return;
+  const long r = gid / nch;
+  const int ch = gid % nch;
+  *reinterpret_cast<uint4*>(out + r * D + ch * 8) = *reinterpret_cast<const uint4*>(table + ids[r] * D + ch * 8);
+}
+
+__global__ void embed_scatter_kernel(const bf16_t* __restrict__ drows, const int64_t* __restrict__ ids, long R, int D,
+                                     long pad_id, float* __restrict__ dtable) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= R * D) return;
+  const long r = gid / D;
+  const int d = gid % D;
+  const long id = ids[r];
+  if (id == pad_id) return;
+  atomicAdd(dtable + id * D + d, bf2f(drows[gid]));
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ in, long n, bf16_t* __restrict__ out) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= n) return;
+  const floatx4 v = *reinterpret_cast<const floatx4*>(in + i);
+  uint2 w;
+  w.x = pack_bf16x2(v[0], v[1]);
+  w.y = pack_bf16x2(v[2], v[3]);
+  *reinterpret_cast<uint2*>(out + i) = w;
+}
+
+// ---------------------------------------------------------------- RAdamScheduleFree
+struct SfScalars {
+  float beta2, bias_correction2, eps, ckp1, adaptive_y_lr, lr, decay, grad_scale;
+  int adam;
+};
+__global__ void radam_sf_step_kernel(bf16_t* __restrict__ y, const float* __restrict__ grad, float* __restrict__ z,
+                                     float* __restrict__ v, long n, SfScalars s) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float g = grad[i] * s.grad_scale;
+  float vv = v[i] * s.beta2 + (1.f - s.beta2) * g * g;
+  v[i] = vv;
+  if (s.adam) g = g / (sqrtf(vv / s.bias_correction2) + s.eps);
+  float yy = bf2f(y[i]);
+  if (s.decay != 0.f) g += s.decay * yy;
+  float zz = z[i];
+  yy = yy + s.ckp1 * (zz - yy);
+  yy = yy + s.adaptive_y_lr * g;
+  z[i] = zz - s.lr * g;
+  y[i] = f2bf(yy);
+}
+
+__global__ void lerp_to_z_kernel(bf16_t* __restrict__ y, const float* __restrict__ z, long n, float w) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float yy = bf2f(y[i]);
+  y[i] = f2bf(yy + w * (z[i] - yy));
+}
+
+__global__ void init_z_kernel(const bf16_t* __restrict__ y, float* __restrict__ z, float* __restrict__ v, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  z[i] = bf2f(y[i]);
+  v[i] = 0.f;
+}
+
+// Copy rows [row0, row0+cnt) of every sequence of a [B][rows][D] matrix to a dense [B*cnt][D]
+// matrix (reverse: the other way round, writing into the sequence layout).
+__global__ void copy_rows_kernel(bf16_t* __restrict__ seq, long ld_seq, int rows, int row0, int cnt,
+                                 bf16_t* __restrict__ dense, long ld_dense, int B, int D, int reverse) {
+  const int nch = D >> 3;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long)B * cnt * nch) return;
+  const int ch = gid % nch;
+  const long r = gid / nch;
+  const int b = r / cnt, j = r % cnt;
+  bf16_t* s = seq + ((long)b * rows + row0 + j) * ld_seq + ch * 8;
+  bf16_t* d = dense + r * ld_dense + ch * 8;
+  if (reverse) *reinterpret_cast<uint4*>(s) = *reinterpret_cast<const uint4*>(d);
+  else *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
+}
+
+// y = bf16(silu(x)); backward dx = dy * silu'(x) (x is the bf16 pre-activation).
+__global__ void silu_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, bf16_t* __restrict__ out,
+                            long n, int backward) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= n) return;
+  float a[8], o[8];
+  unpack8(*reinterpret_cast<const uint4*>(x + i), a);
+  if (!backward) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = silu_f(a[e]);
+  } else {
+    float g[8];
+    unpack8(*reinterpret_cast<const uint4*>(dy + i), g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float sg = 1.f / (1.f + expf(-a[e]));
+      o[e] = g[e] * (sg * (1.f + a[e] * (1.f - sg)));
+    }
+  }
+  *reinterpret_cast<uint4*>(out + i) = pack8(o);
+}
+
+inline dim3 grid1(long n, int threads = 256) { return dim3((unsigned)((n + threads - 1) / threads)); }
+
+}  // namespace
+
+extern "C" int vpt_copy_rows(void* seq, long ld_seq, int rows, int row0, int cnt, void* dense, long ld_dense, int B,
+                             int D, int reverse, void* stream) {
+  VPT_CHECK_ARG(seq && dense && D % 8 == 0 && row0 + cnt <= rows, "vpt_copy_rows: bad args");
+  hipLaunchKernelGGL(copy_rows_kernel, grid1((long)B * cnt * (D / 8)), dim3(256), 0, (hipStream_t)stream,
+                     (bf16_t*)seq, ld_seq, rows, row0, cnt, (bf16_t*)dense, ld_dense, B, D, reverse);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_silu(const void* x, const void* dy, void* out, long n, int backward, void* stream) {
+  VPT_CHECK_ARG(x && out && n % 8 == 0 && (!backward || dy), "vpt_silu: bad args");
+  hipLaunchKernelGGL(silu_kernel, grid1(n / 8), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                     (const bf16_t*)dy, (bf16_t*)out, n, backward);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_patchify(const void* img, int in_kind, const void* noise, const float* t, float noise_scale,
+                            unsigned long long seed, int B, int H, int W, void* out, void* stream) {
+  VPT_CHECK_ARG(img && out && B > 0, "vpt_patchify: bad args");
+  VPT_CHECK_ARG(H % 16 == 0 && W % 16 == 0, "vpt_patchify: H and W must be multiples of the 16-px patch");
+  VPT_CHECK_ARG(in_kind == 1 || t, "vpt_patchify: noising needs t");
+  const long total = (long)B * (H / 16) * (W / 16) * 96;
+  hipLaunchKernelGGL(patchify_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream, (const unsigned short*)img,
+                     in_kind, (const unsigned short*)noise, t, noise_scale, (uint64_t)seed, B, H, W, (bf16_t*)out);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_unpatchify(const void* patches, int B, int H, int W, void* img, int reverse, void* stream) {
+  VPT_CHECK_ARG(patches && img && H % 16 == 0 && W % 16 == 0, "vpt_unpatchify: bad args");
+  const long total = (long)B * 3 * H * W;
+  hipLaunchKernelGGL(unpatchify_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)patches, B, H,
+                     W, (bf16_t*)img, reverse);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_loss_blocks(void) { return 1024; }
+
+extern "C" int vpt_flow_loss(const void* pred, const void* img, const void* noise, const float* t, float noise_scale,
+                             unsigned long long seed, int target, float t_eps, int B, int H, int W, void* dpred,
+                             float* part, float* loss, void* stream) {
+  VPT_CHECK_ARG(pred && img && t && dpred && part && loss, "vpt_flow_loss: null pointer");
+  VPT_CHECK_ARG(target == 0 || target == 1, "vpt_flow_loss: target must be 0 (image) or 1 (velocity)");
+  const float numel = (float)B * 3.f * H * W;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(loss_kernel, dim3(vpt_loss_blocks()), dim3(256), 0, s, (const bf16_t*)pred,
+                     (const unsigned short*)img, (const unsigned short*)noise, t, noise_scale, (uint64_t)seed, target,
+                     t_eps, B, H, W, 1.f / numel, (bf16_t*)dpred, part);
+  VPT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, part, vpt_loss_blocks(), 1.f / numel, loss);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_timestep_embed(const float* vals, int R, void* out, void* stream) {
+  VPT_CHECK_ARG(vals && out && R > 0, "vpt_timestep_embed: bad args");
+  hipLaunchKernelGGL(timestep_embed_kernel, grid1((long)R * 256), dim3(256), 0, (hipStream_t)stream, vals, R,
+                     (bf16_t*)out);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_assemble_tokens(const void* patches, const void* size_emb, const void* time_emb, const void* tpe,
+                                   const void* ctx, int n_ctx, int B, int np_, int rows, void* x, void* stream) {
+  VPT_CHECK_ARG(patches && size_emb && time_emb && tpe && x, "vpt_assemble_tokens: null pointer");
+  VPT_CHECK_ARG(rows >= np_ + 10, "vpt_assemble_tokens: rows too small");
+  hipLaunchKernelGGL(assemble_kernel, grid1((long)B * rows * 96), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)patches, (const bf16_t*)size_emb, (const bf16_t*)time_emb, (const bf16_t*)tpe,
+                     (const bf16_t*)ctx, n_ctx, B, np_, rows, (bf16_t*)x);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_disassemble_tokens(const void* dx, int B, int np_, int rows, void* dpatches, void* dsize,
+                                      void* dtime, float* dtpe, void* stream) {
+  VPT_CHECK_ARG(dx && dpatches && dsize && dtime, "vpt_disassemble_tokens: null pointer");
+  hipLaunchKernelGGL(disassemble_kernel, grid1((long)B * (np_ + 7) * 96), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)dx, B, np_, rows, (bf16_t*)dpatches, (bf16_t*)dsize, (bf16_t*)dtime, dtpe);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_ctx_rows(void* x, int B, int row0, int rows, const void* ctx, float* dctx, int n_ctx, int backward,
+                            void* stream) {
+  VPT_CHECK_ARG(x && n_ctx > 0 && (backward ? dctx != nullptr : ctx != nullptr), "vpt_ctx_rows: bad args");
+  hipLaunchKernelGGL(ctx_rows_kernel, grid1((long)B * n_ctx * 96), dim3(256), 0, (hipStream_t)stream, (bf16_t*)x, B,
+                     row0, rows, (const bf16_t*)ctx, dctx, n_ctx, backward);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_swiglu_fwd(const void* x12, long M, int F, void* h, void* stream) {
+  VPT_CHECK_ARG(x12 && h && F % 8 == 0, "vpt_swiglu_fwd: bad args");
+  hipLaunchKernelGGL(swiglu_fwd_kernel, grid1(M * (F / 8)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x12, M,
+                     F, (bf16_t*)h);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_swiglu_bwd(const void* dh, const void* x12, long M, int F, void* dx12, void* stream) {
+  VPT_CHECK_ARG(dh && x12 && dx12 && F % 8 == 0, "vpt_swiglu_bwd: bad args");
+  hipLaunchKernelGGL(swiglu_bwd_kernel, grid1(M * (F / 8)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dh,
+                     (const bf16_t*)x12, M, F, (bf16_t*)dx12);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_colsum_blocks(long M) {
+  long b = (M + 63) / 64;
+  return (int)(b > 256 ? 256 : (b < 1 ? 1 : b));
+}
+
+extern "C" int vpt_colsum(const void* in, long ld, long M, int N, float* part, void* stream) {
+  VPT_CHECK_ARG(in && part && N % 8 == 0 && M > 0, "vpt_colsum: bad args");
+  const int nb = vpt_colsum_blocks(M);
+  const long per = (M + nb - 1) / nb;
+  hipLaunchKernelGGL(colsum_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)in, ld, M, N, per,
+                     part);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_embed_gather(const void* table, const long long* ids, long R, int D, void* out, void* stream) {
+  VPT_CHECK_ARG(table && ids && out && D % 8 == 0, "vpt_embed_gather: bad args");
+  hipLaunchKernelGGL(embed_gather_kernel, grid1(R * (D / 8)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)table,
+                     (const int64_t*)ids, R, D, (bf16_t*)out);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_embed_scatter_add(const void* drows, const long long* ids, long R, int D, long long pad_id,
+                                     float* dtable, void* stream) {
+  VPT_CHECK_ARG(drows && ids && dtable, "vpt_embed_scatter_add: bad args");
+  hipLaunchKernelGGL(embed_scatter_kernel, grid1(R * D), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)drows,
+                     (const int64_t*)ids, R, D, (long)pad_id, dtable);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_cast_f32_bf16(const float* in, long n, void* out, void* stream) {
+  VPT_CHECK_ARG(in && out && n % 4 == 0, "vpt_cast_f32_bf16: n must be a multiple of 4");
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, grid1(n / 4), dim3(256), 0, (hipStream_t)stream, in, n, (bf16_t*)out);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_radam_sf_step(void* y, const float* grad, float* z, float* v, long n, float beta2,
+                                 float bias_correction2, float eps, float ckp1, float adaptive_y_lr, float lr,
+                                 float decay, float grad_scale, int adam, void* stream) {
+  VPT_CHECK_ARG(y && grad && z && v && n >= 0, "vpt_radam_sf_step: bad args");
+  if (n == 0) return VPT_OK;
+  SfScalars s{beta2, bias_correction2, eps, ckp1, adaptive_y_lr, lr, decay, grad_scale, adam};
+  hipLaunchKernelGGL(radam_sf_step_kernel, grid1(n), dim3(256), 0, (hipStream_t)stream, (bf16_t*)y, grad, z, v, n, s);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_sf_lerp(void* y, const float* z, long n, float w, void* stream) {
+  VPT_CHECK_ARG(y && z, "vpt_sf_lerp: bad args");
+  if (n == 0) return VPT_OK;
+  hipLaunchKernelGGL(lerp_to_z_kernel, grid1(n), dim3(256), 0, (hipStream_t)stream, (bf16_t*)y, z, n, w);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_sf_init(const void* y, float* z, float* v, long n, void* stream) {
+  VPT_CHECK_ARG(y && z && v, "vpt_sf_init: bad args");
+  if (n == 0) return VPT_OK;
+  hipLaunchKernelGGL(init_z_kernel, grid1(n), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)y, z, v, n);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}

@@ -1,0 +1,59 @@
+"""Builds libvpt_hip.so (gfx950) from vision-pt_amd/csrc/*.hip with hipcc, in-tree.
+
+Each translation unit is compiled in parallel to build/*.o and linked into lib/libvpt_hip.so.
+A unit is rebuilt only when its source or common.h is newer than its object.
+"""
+
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+from pathlib import Path
+
+PKG_ROOT = Path(__file__).resolve().parent.parent  # vision-pt_amd/
+CSRC = PKG_ROOT / "csrc"
+BUILD = PKG_ROOT / "build"
+LIB = PKG_ROOT / "lib" / "libvpt_hip.so"
+ARCH = "gfx950"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+
+
+def _needs(obj: Path, deps: list[Path]) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _compile(src: Path) -> Path:
+    obj = BUILD / (src.stem + ".o")
+    deps = [src] + sorted(CSRC.glob("*.h"))
+    if _needs(obj, deps):
+        cmd = [HIPCC, *CFLAGS, "-c", str(src), "-o", str(obj)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr[-4000:]}")
+    return obj
+
+
+def build(verbose: bool = False) -> Path:
+    BUILD.mkdir(exist_ok=True)
+    LIB.parent.mkdir(exist_ok=True)
+    srcs = sorted(CSRC.glob("*.hip"))
+    workers = min(len(srcs), max(1, min(8, os.cpu_count() or 1)))
+    with cf.ThreadPoolExecutor(workers) as ex:
+        objs = list(ex.map(_compile, srcs))
+    if _needs(LIB, objs):
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(LIB)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
+    if verbose:
+        print(f"built {LIB}")
+    return LIB
+
+
+if __name__ == "__main__":
+    build(verbose=True)

@@ -1,0 +1,94 @@
+"""ctypes binding of the C-ABI library libvpt_hip.so (declared in include/vpt_hip.h).
+
+The product path has no fallback: if the shared library is missing or fails to load, importing
+this module raises. Every entry point returns an int status; nonzero raises RuntimeError with
+`vpt_last_error_string()`.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+from ._build import LIB
+
+P = C.c_void_p
+L = C.c_long
+I = C.c_int
+F = C.c_float
+U64 = C.c_ulonglong
+LL = C.c_longlong
+
+# name -> argtypes; restype is c_int unless listed in _RESTYPES.
+SIGNATURES: dict[str, list] = {
+    "vpt_gemm_bf16": [P, L, I, P, L, I, P, L, I, I, I, P, P, L, I, I, I, P, P],
+    "vpt_gemm_workspace_bytes": [I, I, I, I],
+    "vpt_attn_fwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, P, L, I, I, I, I, F, P],
+    "vpt_attn_bwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, P, L, L, P, L,
+                     P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, F, P],
+    "vpt_rmsnorm_fwd": [P, L, P, P, L, P, I, I, F, P],
+    "vpt_rmsnorm_bwd_blocks": [I],
+    "vpt_rmsnorm_bwd": [P, L, P, L, P, P, P, L, P, L, P, I, I, P],
+    "vpt_qknorm_rope_blocks": [I],
+    "vpt_qknorm_rope_fwd": [P, L, P, P, P, P, P, L, I, I, I, F, P],
+    "vpt_qknorm_rope_bwd": [P, L, P, L, P, P, P, P, P, L, P, I, I, I, F, P],
+    "vpt_reduce_rows": [P, I, I, P, I, P],
+    "vpt_patchify": [P, I, P, P, F, U64, I, I, I, P, P],
+    "vpt_unpatchify": [P, I, I, I, P, I, P],
+    "vpt_loss_blocks": [],
+    "vpt_flow_loss": [P, P, P, P, F, U64, I, F, I, I, I, P, P, P, P],
+    "vpt_timestep_embed": [P, I, P, P],
+    "vpt_assemble_tokens": [P, P, P, P, P, I, I, I, I, P, P],
+    "vpt_disassemble_tokens": [P, I, I, I, P, P, P, P, P],
+    "vpt_ctx_rows": [P, I, I, I, P, P, I, I, P],
+    "vpt_swiglu_fwd": [P, L, I, P, P],
+    "vpt_swiglu_bwd": [P, P, L, I, P, P],
+    "vpt_colsum_blocks": [L],
+    "vpt_colsum": [P, L, L, I, P, P],
+    "vpt_embed_gather": [P, P, L, I, P, P],
+    "vpt_embed_scatter_add": [P, P, L, I, LL, P, P],
+    "vpt_cast_f32_bf16": [P, L, P, P],
+    "vpt_radam_sf_step": [P, P, P, P, L, F, F, F, F, F, F, F, F, I, P],
+    "vpt_sf_lerp": [P, P, L, F, P],
+    "vpt_sf_init": [P, P, P, L, P],
+    "vpt_copy_rows": [P, L, I, I, I, P, L, I, I, I, P],
+    "vpt_silu": [P, P, P, L, I, P],
+    "vpt_last_error_string": [],
+    "vpt_abi_version": [],
+    "vpt_build_info": [],
+}
+_RESTYPES = {
+    "vpt_gemm_workspace_bytes": C.c_long,
+    "vpt_last_error_string": C.c_char_p,
+    "vpt_build_info": C.c_char_p,
+}
+# Entry points that return a value (size / count / string) rather than a status code.
+_VALUE_FNS = {"vpt_gemm_workspace_bytes", "vpt_rmsnorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
+              "vpt_colsum_blocks", "vpt_last_error_string", "vpt_abi_version", "vpt_build_info"}
+
+
+def _load(path: Path) -> C.CDLL:
+    if not path.exists():
+        raise ImportError(
+            f"{path} not found: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()')")
+    lib = C.CDLL(str(path))
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPES.get(name, C.c_int)
+    return lib
+
+
+lib = _load(LIB)
+LIB_PATH = LIB
+
+
+def call(name: str, *args):
+    """Calls a status-returning entry point; raises RuntimeError on a nonzero status."""
+    rc = getattr(lib, name)(*args)
+    if name in _VALUE_FNS:
+        return rc
+    if rc != 0:
+        msg = lib.vpt_last_error_string().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (status {rc}): {msg}")
+    return rc

@@ -1,0 +1,102 @@
+"""Config surface mirrored from the reference (same field names / defaults, so the reference's
+YAML `model.denoiser:` dicts validate unchanged).
+
+  DenoiserConfig      <- src/models/jit/config.py:16-46
+  JiT_B_16_Config     <- src/models/jit/config.py:49-65
+  JiTTrainingConfig   <- train/jit/arb_class_to_image.py:26-44 (JiTConfigForTraining fields that
+                         the training step reads)
+"""
+
+from __future__ import annotations
+
+from typing import Literal
+
+from pydantic import BaseModel
+
+NormType = Literal["layer", "rms", "dyt", "derf"]
+PositionalEncoding = Literal["rope", "pope", "n-pope"]
+
+
+class DenoiserConfig(BaseModel):
+    patch_size: int = 16
+    in_channels: int = 3
+    out_channels: int = 3
+    hidden_size: int = 1024
+    depth: int = 24
+    num_heads: int = 16
+    mlp_ratio: float = 4.0
+    attn_dropout: float = 0.0
+    proj_dropout: float = 0.0
+
+    bottleneck_dim: int = 128
+    use_output_bottleneck: bool = False
+    use_pixel_shuffle: bool = False
+
+    norm_type: NormType = "rms"
+
+    num_time_tokens: int = 4
+    timestep_scale: float = 1.0
+
+    positional_encoding: PositionalEncoding = "rope"
+    rope_theta: float = 256.0
+    rope_axes_dims: list[int] = [16, 24, 24]
+    rope_axes_lens: list[int] = [256, 128, 128]
+    rope_zero_centered: list[bool] = [False, True, True]
+    rope_do_normalize: list[bool] = [False, True, True]
+    rope_normalize_by: float = 64.0
+
+    context_dim: int = 768
+    context_start_block: int = 0
+    do_context_fuse: bool = False
+
+    @property
+    def head_dim(self) -> int:
+        return self.hidden_size // self.num_heads
+
+    @property
+    def mlp_hidden(self) -> int:
+        # SwiGLU(dim, hidden_dim=int(D*mlp_ratio)) uses int(hidden_dim * 2 / 3) (denoiser.py:490, 641-646)
+        return int(int(self.hidden_size * self.mlp_ratio) * 2 / 3)
+
+
+class JiT_B_16_Config(DenoiserConfig):
+    patch_size: int = 16
+    depth: int = 12
+    hidden_size: int = 768
+    num_heads: int = 12
+    bottleneck_dim: int = 128
+    context_dim: int = 768
+    context_start_block: int = 4
+    rope_axes_dims: list[int] = [16, 24, 24]
+    rope_axes_lens: list[int] = [256, 128, 128]
+
+
+class JiTTrainingConfig(BaseModel):
+    max_token_length: int = 64
+    noise_scale: float = 1.0
+    timestep_eps: float = 0.05
+    loss_target: Literal["velocity", "image"] = "velocity"
+    timestep_sampling: str = "scale_shift_sigmoid"
+    train_class_encoder: bool = True
+    drop_context_rate: float = 0.1
+
+
+def check_supported(cfg: DenoiserConfig) -> None:
+    """The HIP path implements the JiT-B family path of the reference; reject the variants it
+    does not (they raise instead of silently computing something else)."""
+    if cfg.positional_encoding != "rope":
+        raise NotImplementedError("HIP JiT: only positional_encoding='rope' (PoPE variants are out of scope)")
+    if cfg.norm_type != "rms":
+        raise NotImplementedError("HIP JiT: only norm_type='rms'")
+    if cfg.use_output_bottleneck or cfg.use_pixel_shuffle:
+        raise NotImplementedError("HIP JiT: output bottleneck / pixel shuffle heads are out of scope")
+    if cfg.head_dim != 64 or sum(cfg.rope_axes_dims) != 64:
+        raise NotImplementedError("HIP JiT: head_dim must be 64 (rope_axes_dims summing to 64)")
+    if cfg.patch_size != 16 or cfg.in_channels != 3 or cfg.out_channels != 3:
+        raise NotImplementedError("HIP JiT: patch 16, 3 channels")
+    if cfg.hidden_size % 64 or cfg.context_dim % 8 or cfg.bottleneck_dim % 8:
+        raise NotImplementedError("HIP JiT: hidden_size % 64, context_dim % 8, bottleneck_dim % 8")
+    if cfg.attn_dropout != 0.0 or cfg.proj_dropout != 0.0:
+        raise NotImplementedError("HIP JiT: dropout must be 0 (reference default)")
+    if len(cfg.rope_axes_dims) != 3:
+        raise NotImplementedError("HIP JiT: 3 rope axes")

@@ -1,0 +1,293 @@
+"""Tensor-level wrappers over the C-ABI kernels (plumbing only: PyTorch provides device memory
+and the current HIP stream; every FLOP runs in libvpt_hip.so).
+
+Conventions: bf16 activations/weights, f32 statistics and gradients-of-weights. Matrices are
+row-major with an explicit leading dimension (`t.stride(0)`); the last dim must be contiguous.
+"""
+
+from __future__ import annotations
+
+import torch
+
+from ._lib import call, lib
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+OUT_BF16, OUT_F32, OUT_F32_ACC = 0, 1, 2
+ACT_NONE, ACT_SILU = 0, 1
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t: torch.Tensor | None):
+    return None if t is None else t.data_ptr()
+
+
+def _chk(t: torch.Tensor, dtype, name: str):
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a GPU tensor")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    if t.stride(-1) != 1:
+        raise ValueError(f"{name} must have a contiguous last dim")
+
+
+# ----------------------------------------------------------------------------- GEMM
+def gemm(a, a_kmajor: bool, b, b_kmajor: bool, M: int, N: int, K: int, out, *, bias=None, resid=None,
+         out_mode=OUT_BF16, act=ACT_NONE, splits=1, workspace=None):
+    """out[M,N] (=|+=) sum_k A(m,k) B(n,k) (+bias[n]) (+resid[m,n]); see csrc/gemm.hip."""
+    _chk(a, BF16, "a")
+    _chk(b, BF16, "b")
+    _chk(out, BF16 if out_mode == OUT_BF16 else F32, "out")
+    if bias is not None:
+        _chk(bias, BF16, "bias")
+    if resid is not None:
+        _chk(resid, BF16, "resid")
+    if splits > 1 and workspace is None:
+        workspace = torch.empty(splits * M * N, dtype=F32, device=out.device)
+    call("vpt_gemm_bf16", a.data_ptr(), a.stride(0), int(a_kmajor), b.data_ptr(), b.stride(0), int(b_kmajor),
+         out.data_ptr(), out.stride(0), M, N, K, _p(bias), _p(resid), 0 if resid is None else resid.stride(0),
+         out_mode, act, splits, _p(workspace), stream())
+    return out
+
+
+def linear(x, w, bias=None, resid=None, out=None, act=ACT_NONE):
+    """y = x @ w.T (+bias) (+resid) in bf16 — nn.Linear forward."""
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=BF16, device=x.device)
+    return gemm(x, True, w, True, M, N, K, out, bias=bias, resid=resid, act=act)
+
+
+def linear_dgrad(dy, w, out=None):
+    """dx = dy @ w  (dy [M,N], w [N,K]) — nn.Linear input gradient."""
+    M, N = dy.shape
+    K = w.shape[1]
+    if out is None:
+        out = torch.empty(M, K, dtype=BF16, device=dy.device)
+    return gemm(dy, True, w, False, M, K, N, out)
+
+
+def linear_wgrad(dy, x, out, accumulate=False, splits=1, workspace=None):
+    """dW (=|+=) dy.T @ x in f32 (dy [M,N], x [M,K], out [N,K]) — nn.Linear weight gradient."""
+    M, N = dy.shape
+    K = x.shape[1]
+    return gemm(dy, False, x, False, N, K, M, out, out_mode=OUT_F32_ACC if accumulate else OUT_F32,
+                splits=splits, workspace=workspace)
+
+
+def wgrad_splits(N: int, K: int, M: int) -> int:
+    """Split-K factor so that the wgrad grid has ~2 blocks per CU (256 CUs)."""
+    tiles = ((N + 127) // 128) * ((K + 127) // 128)
+    s = max(1, min(64, (512 + tiles - 1) // tiles))
+    s = min(s, max(1, M // 256))
+    return s
+
+
+# ----------------------------------------------------------------------------- norms
+def rmsnorm_fwd(x, w, out=None, rstd=None, eps=1e-6):
+    M, D = x.shape
+    if out is None:
+        out = torch.empty(M, D, dtype=BF16, device=x.device)
+    if rstd is None:
+        rstd = torch.empty(M, dtype=F32, device=x.device)
+    call("vpt_rmsnorm_fwd", x.data_ptr(), x.stride(0), w.data_ptr(), out.data_ptr(), out.stride(0), rstd.data_ptr(),
+         M, D, eps, stream())
+    return out, rstd
+
+
+def rmsnorm_bwd_blocks(M: int) -> int:
+    return lib.vpt_rmsnorm_bwd_blocks(M)
+
+
+def rmsnorm_bwd(dy, x, rstd, w, dres=None, dx=None, dw_part=None):
+    """dx = dres + RMSNorm'(dy); dw_part [blocks, D] f32 partial sums (reduce with reduce_rows)."""
+    M, D = x.shape
+    if dx is None:
+        dx = torch.empty(M, D, dtype=BF16, device=x.device)
+    if dw_part is None:
+        dw_part = torch.empty(rmsnorm_bwd_blocks(M), D, dtype=F32, device=x.device)
+    call("vpt_rmsnorm_bwd", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), rstd.data_ptr(), w.data_ptr(),
+         _p(dres), 0 if dres is None else dres.stride(0), dx.data_ptr(), dx.stride(0), dw_part.data_ptr(), M, D,
+         stream())
+    return dx, dw_part
+
+
+def reduce_rows(part, out, accumulate=False):
+    R, Cc = part.shape
+    call("vpt_reduce_rows", part.data_ptr(), R, Cc, out.data_ptr(), int(accumulate), stream())
+    return out
+
+
+def qknorm_rope_fwd(qkv, wq, wk, cos_t, sin_t, rows_per_seq, out=None, eps=1e-6):
+    """qkv [M, 3D] -> out [M, 2D] = (rope(rms(q)), rope(rms(k)))."""
+    M = qkv.shape[0]
+    D = qkv.shape[1] // 3
+    if out is None:
+        out = torch.empty(M, 2 * D, dtype=BF16, device=qkv.device)
+    call("vpt_qknorm_rope_fwd", qkv.data_ptr(), qkv.stride(0), wq.data_ptr(), wk.data_ptr(), cos_t.data_ptr(),
+         sin_t.data_ptr(), out.data_ptr(), out.stride(0), M, rows_per_seq, D, eps, stream())
+    return out
+
+
+def qknorm_rope_blocks(M: int) -> int:
+    return lib.vpt_qknorm_rope_blocks(M)
+
+
+def qknorm_rope_bwd(dqk, qkv, wq, wk, cos_t, sin_t, rows_per_seq, dqkv, dw_part=None, eps=1e-6):
+    """Writes dqkv[:, :2D]; dw_part [blocks, 128] = (d q_norm.w | d k_norm.w) partials."""
+    M = qkv.shape[0]
+    D = qkv.shape[1] // 3
+    if dw_part is None:
+        dw_part = torch.empty(qknorm_rope_blocks(M), 128, dtype=F32, device=qkv.device)
+    call("vpt_qknorm_rope_bwd", dqk.data_ptr(), dqk.stride(0), qkv.data_ptr(), qkv.stride(0), wq.data_ptr(),
+         wk.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(), dqkv.data_ptr(), dqkv.stride(0), dw_part.data_ptr(), M,
+         rows_per_seq, D, eps, stream())
+    return dw_part
+
+
+# ----------------------------------------------------------------------------- attention
+def _t4(t, B: int, rows: int, H: int, col0: int = 0):
+    """Token-major [B*rows, ld] matrix viewed per head: returns (ptr, sb, sh, sr) for head 0 at col0."""
+    ld = t.stride(0)
+    return t.data_ptr() + col0 * t.element_size(), rows * ld, 64, ld
+
+
+def attn_fwd(q, k, v, o, lse, kbias, B, H, rows, n, n_dense, scale=0.125):
+    """q/k/v/o as (ptr, sb, sh, sr) tuples (element strides); lse [B,H,rows] f32; kbias [B,rows] f32 or None."""
+    call("vpt_attn_fwd", *q, *k, *v, *o, lse.data_ptr(), lse.stride(0), lse.stride(1),
+         _p(kbias), 0 if kbias is None else kbias.stride(0), B, H, n, n_dense, scale, stream())
+
+
+def attn_bwd(q, k, v, o, do, lse, delta, kbias, dq, dk, dv, B, H, rows, n, n_dense, scale=0.125):
+    call("vpt_attn_bwd", *q, *k, *v, *o, *do, lse.data_ptr(), delta.data_ptr(), lse.stride(0), lse.stride(1),
+         _p(kbias), 0 if kbias is None else kbias.stride(0), *dq, *dk, *dv, B, H, n, n_dense, scale, stream())
+
+
+# ----------------------------------------------------------------------------- misc
+def patchify(img, B, H, W, out, t=None, noise=None, noise_scale=1.0, seed=0, noising=True):
+    call("vpt_patchify", img.data_ptr(), 0 if noising else 1, _p(noise), _p(t), noise_scale, seed, B, H, W,
+         out.data_ptr(), stream())
+    return out
+
+
+def unpatchify(patches, B, H, W, img, reverse=False):
+    call("vpt_unpatchify", patches.data_ptr(), B, H, W, img.data_ptr(), int(reverse), stream())
+    return img
+
+
+def loss_blocks() -> int:
+    return lib.vpt_loss_blocks()
+
+
+def flow_loss(pred, img, t, B, H, W, dpred, part, loss, target=0, t_eps=0.05, noise=None, noise_scale=1.0,
+              seed=0):
+    call("vpt_flow_loss", pred.data_ptr(), img.data_ptr(), _p(noise), t.data_ptr(), noise_scale, seed, target,
+         t_eps, B, H, W, dpred.data_ptr(), part.data_ptr(), loss.data_ptr(), stream())
+    return loss
+
+
+def timestep_embed(vals, out):
+    call("vpt_timestep_embed", vals.data_ptr(), vals.numel(), out.data_ptr(), stream())
+    return out
+
+
+def assemble_tokens(patches, size_emb, time_emb, tpe, ctx, n_ctx, B, np_, rows, x):
+    call("vpt_assemble_tokens", patches.data_ptr(), size_emb.data_ptr(), time_emb.data_ptr(), tpe.data_ptr(),
+         _p(ctx), n_ctx, B, np_, rows, x.data_ptr(), stream())
+    return x
+
+
+def disassemble_tokens(dx, B, np_, rows, dpatches, dsize, dtime, dtpe):
+    call("vpt_disassemble_tokens", dx.data_ptr(), B, np_, rows, dpatches.data_ptr(), dsize.data_ptr(),
+         dtime.data_ptr(), _p(dtpe), stream())
+
+
+def ctx_rows(x, B, row0, rows, n_ctx, ctx=None, dctx=None, backward=False):
+    call("vpt_ctx_rows", x.data_ptr(), B, row0, rows, _p(ctx), _p(dctx), n_ctx, int(backward), stream())
+
+
+def swiglu_fwd(x12, h):
+    M, F2 = x12.shape
+    call("vpt_swiglu_fwd", x12.data_ptr(), M, F2 // 2, h.data_ptr(), stream())
+    return h
+
+
+def swiglu_bwd(dh, x12, dx12):
+    M, F2 = x12.shape
+    call("vpt_swiglu_bwd", dh.data_ptr(), x12.data_ptr(), M, F2 // 2, dx12.data_ptr(), stream())
+    return dx12
+
+
+def colsum_blocks(M: int) -> int:
+    return lib.vpt_colsum_blocks(M)
+
+
+def colsum(x, part):
+    M, N = x.shape
+    call("vpt_colsum", x.data_ptr(), x.stride(0), M, N, part.data_ptr(), stream())
+    return part
+
+
+def bias_grad(dy, out, part=None, accumulate=False):
+    """out[N] (=|+=) sum over rows of dy [M,N] (bf16) in f32."""
+    M, N = dy.shape
+    nb = colsum_blocks(M)
+    if part is None:
+        part = torch.empty(nb, N, dtype=F32, device=dy.device)
+    part = part.view(-1)[: nb * N].view(nb, N)
+    colsum(dy, part)
+    return reduce_rows(part, out, accumulate)
+
+
+def embed_gather(table, ids, out):
+    R = ids.numel()
+    call("vpt_embed_gather", table.data_ptr(), ids.data_ptr(), R, table.shape[1], out.data_ptr(), stream())
+    return out
+
+
+def embed_scatter_add(drows, ids, pad_id, dtable):
+    R = ids.numel()
+    call("vpt_embed_scatter_add", drows.data_ptr(), ids.data_ptr(), R, dtable.shape[1], pad_id, dtable.data_ptr(),
+         stream())
+
+
+def copy_rows(seq, rows, row0, cnt, dense, B, reverse=False):
+    """dense[B*cnt, D] <-> seq[B*rows, D] rows [row0, row0+cnt) of every sequence."""
+    D = dense.shape[1]
+    call("vpt_copy_rows", seq.data_ptr(), seq.stride(0), rows, row0, cnt, dense.data_ptr(), dense.stride(0), B, D,
+         int(reverse), stream())
+    return dense
+
+
+def silu(x, out):
+    call("vpt_silu", x.data_ptr(), None, out.data_ptr(), x.numel(), 0, stream())
+    return out
+
+
+def silu_bwd(dy, x, dx):
+    call("vpt_silu", x.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.numel(), 1, stream())
+    return dx
+
+
+def cast_f32_bf16(x, out):
+    call("vpt_cast_f32_bf16", x.data_ptr(), x.numel(), out.data_ptr(), stream())
+    return out
+
+
+def radam_sf_step(y, grad, z, v, *, beta2, bias_correction2, eps, ckp1, adaptive_y_lr, lr, decay, grad_scale,
+                  adam):
+    call("vpt_radam_sf_step", y.data_ptr(), grad.data_ptr(), z.data_ptr(), v.data_ptr(), y.numel(), beta2,
+         bias_correction2, eps, ckp1, adaptive_y_lr, lr, decay, grad_scale, int(adam), stream())
+
+
+def sf_lerp(y, z, w):
+    call("vpt_sf_lerp", y.data_ptr(), z.data_ptr(), y.numel(), w, stream())
+
+
+def sf_init(y, z, v):
+    call("vpt_sf_init", y.data_ptr(), z.data_ptr(), v.data_ptr(), y.numel(), stream())
