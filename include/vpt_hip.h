@@ -1,0 +1,143 @@
+/*
+ * vpt_hip.h — C ABI of libvpt_hip.so, the MI355X (gfx950 / CDNA4) kernel library behind the
+ * JiT rectified-flow training step of p1atdev/vision-pt.
+ *
+ * Conventions
+ *  - Plain pointers to device memory, element strides / leading dimensions in ELEMENTS, sizes as
+ *    int/long. bf16 tensors are 16-bit words, f32 tensors are float, fp16 images are 16-bit words.
+ *  - Every call is enqueued on `stream` (a hipStream_t passed as void*), never synchronises the
+ *    host, never allocates or frees device memory (callers own outputs and workspaces), and keeps
+ *    no reference to its arguments after returning. Safe to capture in a hipGraph.
+ *  - Status: 0 = OK, 1 = invalid argument, 2 = unsupported shape, 3 = HIP launch error; the
+ *    message of the calling thread's last failure is vpt_last_error_string(). No C++ exception
+ *    crosses the boundary.
+ *  - Functions named *_blocks / *_bytes return sizes (partial-sum rows, workspace bytes).
+ *
+ * Reference interfaces replaced (paths relative to p1atdev/vision-pt):
+ *  see the comment above each function.
+ */
+#ifndef VPT_HIP_H
+#define VPT_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- library ---------------------------------------------------------------------------- */
+const char* vpt_last_error_string(void);
+int vpt_abi_version(void);
+const char* vpt_build_info(void);
+
+/* ---- GEMM (MFMA bf16, f32 accumulate) -----------------------------------------------------
+ * C[M,N] (=|+=) sum_k A(m,k) B(n,k) (+bias[n]) (+resid[m,n]) (SiLU).
+ * A(m,k) = A[m*lda + k] if a_kmajor else A[k*lda + m]; same for B with n.
+ * out_mode 0 = bf16 store, 1 = f32 store, 2 = f32 accumulate; act 0 = none, 1 = SiLU.
+ * splits > 1: split-K into f32 slabs in `workspace` (vpt_gemm_workspace_bytes), deterministic sum.
+ * Replaces nn.Linear / 1x1 & patch Conv2d forward and their autograd backward:
+ *   src/models/jit/denoiser.py:36-49,59-65 (BottleneckPatchEmbed), :80-84 (TimestepEmbedder MLP),
+ *   :318-323,360-366,391-395 (Attention to_q/k/v/o), :492-504 (SwiGLU), :535-543 (FinalLayer),
+ *   :715-719,997 (context_embedder). */
+int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* B, long ldb, int b_kmajor, void* C,
+                  long ldc, int M, int N, int K, const void* bias, const void* resid, long ldr, int out_mode,
+                  int act, int splits, void* workspace, void* stream);
+long vpt_gemm_workspace_bytes(int M, int N, int K, int splits);
+
+/* ---- flash attention, head_dim 64 ---------------------------------------------------------
+ * Tensors addressed p[b*sb + h*sh + row*sr + d]. Keys < n_dense always valid; keys in
+ * [n_dense, n) get kbias[b*kb_sb + key] (0 or -inf); keys >= n masked. lse/delta [b*l_sb+h*l_sh+q].
+ * Replaces src/modules/attention.py:98-159 scaled_dot_product_attention (eager SDPA with the
+ * [B,H,N,N] bool mask of src/models/jit/denoiser.py:375-390) and its autograd backward. */
+int vpt_attn_fwd(const void* q, long q_sb, long q_sh, long q_sr, const void* k, long k_sb, long k_sh, long k_sr,
+                 const void* v, long v_sb, long v_sh, long v_sr, void* o, long o_sb, long o_sh, long o_sr,
+                 float* lse, long l_sb, long l_sh, const float* kbias, long kb_sb, int B, int H, int n,
+                 int n_dense, float scale, void* stream);
+int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr, const void* k, long k_sb, long k_sh, long k_sr,
+                 const void* v, long v_sb, long v_sh, long v_sr, const void* o, long o_sb, long o_sh, long o_sr,
+                 const void* dO, long do_sb, long do_sh, long do_sr, const float* lse, float* delta, long l_sb,
+                 long l_sh, const float* kbias, long kb_sb, void* dq, long dq_sb, long dq_sh, long dq_sr,
+                 void* dk, long dk_sb, long dk_sh, long dk_sr, void* dv, long dv_sb, long dv_sh, long dv_sr,
+                 int B, int H, int n, int n_dense, float scale, void* stream);
+
+/* ---- RMSNorm over the hidden dim -----------------------------------------------------------
+ * Replaces FP32RMSNorm.forward src/modules/norm.py:20-27 (norm1/norm2/norm_final,
+ * src/models/jit/denoiser.py:521,600,625) and its backward (dx = dres + RMSNorm'(dy);
+ * dw_part[blocks][D] partial sums, reduce with vpt_reduce_rows). */
+int vpt_rmsnorm_fwd(const void* x, long ldx, const void* w, void* y, long ldy, float* rstd, int M, int D, float eps,
+                    void* stream);
+int vpt_rmsnorm_bwd_blocks(int M);
+int vpt_rmsnorm_bwd(const void* dy, long lddy, const void* x, long ldx, const float* rstd, const void* w,
+                    const void* dres, long ldr, void* dx, long lddx, float* dw_part, int M, int D, void* stream);
+
+/* ---- fused per-head QK-RMSNorm + RoPE --------------------------------------------------------
+ * qkv [M][ldin] (q|k|v, D each) -> out [M][ldout] (rope(rms(q)) | rope(rms(k))).
+ * Replaces Attention.q_norm/k_norm + apply_rope, src/models/jit/denoiser.py:307-316,369-373,98-111
+ * (cos/sin tables [rows_per_seq][32] f32 replace the per-forward host RoPE gather 1013-1051). */
+int vpt_qknorm_rope_blocks(int M);
+int vpt_qknorm_rope_fwd(const void* qkv, long ldin, const void* wq, const void* wk, const float* cos_t,
+                        const float* sin_t, void* out, long ldout, int M, int rows_per_seq, int D, float eps,
+                        void* stream);
+int vpt_qknorm_rope_bwd(const void* dqk, long lddqk, const void* qkv, long ldin, const void* wq, const void* wk,
+                        const float* cos_t, const float* sin_t, void* dqkv, long lddqkv, float* dw_part, int M,
+                        int rows_per_seq, int D, float eps, void* stream);
+int vpt_reduce_rows(const float* in, int R, int C, float* out, int accumulate, void* stream);
+
+/* ---- flow matching input / loss ----------------------------------------------------------------
+ * patchify: z = t*x + (1-t)*eps (eps from `noise` fp16 or the counter RNG `seed`), written in the
+ * Conv2d(k=16,s=16) im2col order; in_kind 1 copies a bf16 image. Replaces
+ * prepare_scaled_noised_latents src/modules/loss/flow_match.py:60-74 + the proj_1 im2col.
+ * flow_loss: mse(pred, x) (target 0) or mse(v(pred), v(x)) (target 1) with v = (. - z)/max(1-t, eps),
+ * writes d loss/d pred. Replaces treat_loss train/jit/arb_class_to_image.py:108-151,
+ * JiTModel.image_to_velocity src/models/jit/pipeline.py:253-260, JiT._unpatchify denoiser.py:828-860. */
+int vpt_patchify(const void* img, int in_kind, const void* noise, const float* t, float noise_scale,
+                 unsigned long long seed, int B, int H, int W, void* out, void* stream);
+int vpt_unpatchify(const void* patches, int B, int H, int W, void* img, int reverse, void* stream);
+int vpt_loss_blocks(void);
+int vpt_flow_loss(const void* pred, const void* img, const void* noise, const float* t, float noise_scale,
+                  unsigned long long seed, int target, float t_eps, int B, int H, int W, void* dpred, float* part,
+                  float* loss, void* stream);
+
+/* ---- embeddings and token assembly ----------------------------------------------------------
+ * timestep_embed: get_timestep_embedding(flip_sin_to_cos=True, shift 0),
+ *   src/modules/timestep/embedding.py:10-62.
+ * assemble/disassemble/ctx_rows: token concatenation and per-block context append/strip,
+ *   src/models/jit/denoiser.py:982-993,1078-1113 (+ their backward).
+ * copy_rows: patch-token slice tokens[:, :N_p] (denoiser.py:1115).
+ * embed_gather/scatter_add: nn.Embedding(padding_idx) of ClassEncoder, class_encoder.py:107-144. */
+int vpt_timestep_embed(const float* vals, int R, void* out, void* stream);
+int vpt_assemble_tokens(const void* patches, const void* size_emb, const void* time_emb, const void* tpe,
+                        const void* ctx, int n_ctx, int B, int np_, int rows, int D, void* x, void* stream);
+int vpt_disassemble_tokens(const void* dx, int B, int np_, int rows, int D, void* dpatches, void* dsize, void* dtime,
+                           float* dtpe, void* stream);
+int vpt_ctx_rows(void* x, int B, int row0, int rows, int D, const void* ctx, float* dctx, int n_ctx, int backward,
+                 void* stream);
+int vpt_copy_rows(void* seq, long ld_seq, int rows, int row0, int cnt, void* dense, long ld_dense, int B, int D,
+                  int reverse, void* stream);
+int vpt_embed_gather(const void* table, const long long* ids, long R, int D, void* out, void* stream);
+int vpt_embed_scatter_add(const void* drows, const long long* ids, long R, int D, long long pad_id, float* dtable,
+                          void* stream);
+
+/* ---- activations / reductions ---------------------------------------------------------------
+ * swiglu: silu(x1) * x2, SwiGLU.forward src/models/jit/denoiser.py:499-504 (+ backward).
+ * silu: the TimestepEmbedder SiLU (denoiser.py:80-84). colsum: Linear bias gradients. */
+int vpt_swiglu_fwd(const void* x12, long M, int F, void* h, void* stream);
+int vpt_swiglu_bwd(const void* dh, const void* x12, long M, int F, void* dx12, void* stream);
+int vpt_silu(const void* x, const void* dy, void* out, long n, int backward, void* stream);
+int vpt_colsum_blocks(long M);
+int vpt_colsum(const void* in, long ld, long M, int N, float* part, void* stream);
+int vpt_cast_f32_bf16(const float* in, long n, void* out, void* stream);
+
+/* ---- optimizer -------------------------------------------------------------------------------
+ * RAdamScheduleFree step over flat buffers (bf16 y, f32 grad / z / v); sf_lerp implements the
+ * train()/eval() y<->x swap; sf_init lazily creates z = y, v = 0. Replaces schedulefree 1.4.1
+ * RAdamScheduleFree (configs/jit/x-loss/config.yml:74-78, src/optimizer/util.py:5-31,
+ * src/trainer/common.py:276-285,382-388). */
+int vpt_radam_sf_step(void* y, const float* grad, float* z, float* v, long n, float beta2, float bias_correction2,
+                      float eps, float ckp1, float adaptive_y_lr, float lr, float decay, float grad_scale, int adam,
+                      void* stream);
+int vpt_sf_lerp(void* y, const float* z, long n, float w, void* stream);
+int vpt_sf_init(const void* y, float* z, float* v, long n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VPT_HIP_H */

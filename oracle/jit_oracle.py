@@ -357,7 +357,8 @@ def train_step_loss(model: OracleJiT, emb: torch.Tensor, batch: dict, loss_targe
     t = batch["t"]
     z = noised(x, t, batch["noise"].float())
     ids, mask = batch["ids"], batch["mask"]
-    if drop_context:
+    if drop_context:  # captions -> "" (all pad ids), mask -> ones (arb_class_to_image.py:162-189)
+        ids = torch.full_like(ids, emb.shape[0] - 1)
         mask = torch.ones_like(mask)
     ctx = F.embedding(ids, emb, padding_idx=emb.shape[0] - 1)
     pred = model(z, t, ctx, batch["original_size"], batch["target_size"], batch["crop_coords"], mask)

@@ -163,94 +163,98 @@ __global__ void timestep_embed_kernel(const float* __restrict__ vals, int R, bf1
 
 // ---------------------------------------------------------------- token assembly
 // x[b][n] rows: [0,np) patches | [np,np+6) image-size | [np+6,np+10) time (+pos) | [np+10, rows) context.
+// D = hidden size (multiple of 8); one thread per 16-byte chunk.
 __global__ void assemble_kernel(const bf16_t* __restrict__ patches, const bf16_t* __restrict__ size_emb,
                                 const bf16_t* __restrict__ time_emb, const bf16_t* __restrict__ tpe,
-                                const bf16_t* __restrict__ ctx, int n_ctx, int B, int np_, int rows,
+                                const bf16_t* __restrict__ ctx, int n_ctx, int B, int np_, int rows, int D,
                                 bf16_t* __restrict__ x) {
-  const long total = (long)B * rows * 96;
+  const int nch = D >> 3;
+  const long total = (long)B * rows * nch;
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= total) return;
-  const long row = gid / 96;
-  const int ch = gid % 96;
+  const long row = gid / nch;
+  const int ch = gid % nch;
   const int b = row / rows, n = row % rows;
   uint4 v = make_uint4(0, 0, 0, 0);
   if (n < np_) {
-    v = *reinterpret_cast<const uint4*>(patches + ((long)b * np_ + n) * 768 + ch * 8);
+    v = *reinterpret_cast<const uint4*>(patches + ((long)b * np_ + n) * D + ch * 8);
   } else if (n < np_ + 6) {
-    v = *reinterpret_cast<const uint4*>(size_emb + ((long)b * 6 + n - np_) * 768 + ch * 8);
+    v = *reinterpret_cast<const uint4*>(size_emb + ((long)b * 6 + n - np_) * D + ch * 8);
   } else if (n < np_ + 10) {
     float a[8], p[8];
-    unpack8(*reinterpret_cast<const uint4*>(time_emb + (long)b * 768 + ch * 8), a);
-    unpack8(*reinterpret_cast<const uint4*>(tpe + (long)(n - np_ - 6) * 768 + ch * 8), p);
+    unpack8(*reinterpret_cast<const uint4*>(time_emb + (long)b * D + ch * 8), a);
+    unpack8(*reinterpret_cast<const uint4*>(tpe + (long)(n - np_ - 6) * D + ch * 8), p);
 #pragma unroll
     for (int e = 0; e < 8; ++e) a[e] += p[e];
     v = pack8(a);
   } else if (ctx && n - np_ - 10 < n_ctx) {
-    v = *reinterpret_cast<const uint4*>(ctx + ((long)b * n_ctx + n - np_ - 10) * 768 + ch * 8);
+    v = *reinterpret_cast<const uint4*>(ctx + ((long)b * n_ctx + n - np_ - 10) * D + ch * 8);
   }
-  *reinterpret_cast<uint4*>(x + row * 768 + ch * 8) = v;
+  *reinterpret_cast<uint4*>(x + row * D + ch * 8) = v;
 }
 
 // Backward of assemble: split dx into d(patches), d(size tokens), d(time_embed) (sum over the 4
-// time tokens) and d(time_position_embeds) partial per batch element.
-__global__ void disassemble_kernel(const bf16_t* __restrict__ dx, int B, int np_, int rows, bf16_t* __restrict__ dpatches,
-                                   bf16_t* __restrict__ dsize, bf16_t* __restrict__ dtime, float* __restrict__ dtpe) {
-  const long total = (long)B * (np_ + 7) * 96;
+// time tokens) and d(time_position_embeds) (sum over the batch, written by the b == 0 threads).
+__global__ void disassemble_kernel(const bf16_t* __restrict__ dx, int B, int np_, int rows, int D,
+                                   bf16_t* __restrict__ dpatches, bf16_t* __restrict__ dsize,
+                                   bf16_t* __restrict__ dtime, float* __restrict__ dtpe) {
+  const int nch = D >> 3;
+  const long total = (long)B * (np_ + 7) * nch;
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= total) return;
-  const int ch = gid % 96;
-  const long r = gid / 96;
+  const int ch = gid % nch;
+  const long r = gid / nch;
   const int b = r / (np_ + 7), n = r % (np_ + 7);
-  const bf16_t* src = dx + ((long)b * rows) * 768 + ch * 8;
+  const bf16_t* src = dx + ((long)b * rows) * D + ch * 8;
   if (n < np_) {
-    *reinterpret_cast<uint4*>(dpatches + ((long)b * np_ + n) * 768 + ch * 8) =
-        *reinterpret_cast<const uint4*>(src + (long)n * 768);
+    *reinterpret_cast<uint4*>(dpatches + ((long)b * np_ + n) * D + ch * 8) =
+        *reinterpret_cast<const uint4*>(src + (long)n * D);
   } else if (n < np_ + 6) {
-    *reinterpret_cast<uint4*>(dsize + ((long)b * 6 + n - np_) * 768 + ch * 8) =
-        *reinterpret_cast<const uint4*>(src + (long)n * 768);
+    *reinterpret_cast<uint4*>(dsize + ((long)b * 6 + n - np_) * D + ch * 8) =
+        *reinterpret_cast<const uint4*>(src + (long)n * D);
   } else {
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int j = 0; j < 4; ++j) {
       float f[8];
-      unpack8(*reinterpret_cast<const uint4*>(src + (long)(np_ + 6 + j) * 768), f);
+      unpack8(*reinterpret_cast<const uint4*>(src + (long)(np_ + 6 + j) * D), f);
 #pragma unroll
       for (int e = 0; e < 8; ++e) s[e] += f[e];
     }
-    *reinterpret_cast<uint4*>(dtime + (long)b * 768 + ch * 8) = pack8(s);
-  }
-  // d(time_position_embeds)[j] = sum_b dx[b][np+6+j]; done by b == 0 lanes to stay deterministic
-  if (b == 0 && n >= np_ + 6 && dtpe) {
-    for (int j = 0; j < 4; ++j) {
-      float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (int bb = 0; bb < B; ++bb) {
-        float f[8];
-        unpack8(*reinterpret_cast<const uint4*>(dx + ((long)bb * rows + np_ + 6 + j) * 768 + ch * 8), f);
+    *reinterpret_cast<uint4*>(dtime + (long)b * D + ch * 8) = pack8(s);
+    if (b == 0 && dtpe) {
+      for (int j = 0; j < 4; ++j) {
+        float t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int bb = 0; bb < B; ++bb) {
+          float f[8];
+          unpack8(*reinterpret_cast<const uint4*>(dx + ((long)bb * rows + np_ + 6 + j) * D + ch * 8), f);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) s[e] += f[e];
+          for (int e = 0; e < 8; ++e) t[e] += f[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dtpe[j * D + ch * 8 + e] = t[e];
       }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dtpe[j * 768 + ch * 8 + e] = s[e];
     }
   }
 }
 
-// Context rows [np+10, np+10+n_ctx) of every sequence: fwd copies ctx in; bwd accumulates dx into
+// Context rows [row0, row0+n_ctx) of every sequence: fwd copies ctx in; bwd accumulates dx into
 // the f32 context-gradient accumulator and zeroes those dx rows (they are stripped after each block).
-__global__ void ctx_rows_kernel(bf16_t* __restrict__ x, int B, int row0, int rows, const bf16_t* __restrict__ ctx,
-                                float* __restrict__ dctx, int n_ctx, int backward) {
-  const long total = (long)B * n_ctx * 96;
+__global__ void ctx_rows_kernel(bf16_t* __restrict__ x, int B, int row0, int rows, int D,
+                                const bf16_t* __restrict__ ctx, float* __restrict__ dctx, int n_ctx, int backward) {
+  const int nch = D >> 3;
+  const long total = (long)B * n_ctx * nch;
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= total) return;
-  const int ch = gid % 96;
-  const long r = gid / 96;
+  const int ch = gid % nch;
+  const long r = gid / nch;
   const int b = r / n_ctx, j = r % n_ctx;
-  bf16_t* xr = x + ((long)b * rows + row0 + j) * 768 + ch * 8;
+  bf16_t* xr = x + ((long)b * rows + row0 + j) * D + ch * 8;
   if (!backward) {
-    *reinterpret_cast<uint4*>(xr) = *reinterpret_cast<const uint4*>(ctx + r * 768 + ch * 8);
+    *reinterpret_cast<uint4*>(xr) = *reinterpret_cast<const uint4*>(ctx + r * D + ch * 8);
   } else {
     float f[8];
     unpack8(*reinterpret_cast<const uint4*>(xr), f);
-    floatx4* d = reinterpret_cast<floatx4*>(dctx + r * 768 + ch * 8);
+    floatx4* d = reinterpret_cast<floatx4*>(dctx + r * D + ch * 8);
     d[0] += floatx4{f[0], f[1], f[2], f[3]};
     d[1] += floatx4{f[4], f[5], f[6], f[7]};
     *reinterpret_cast<uint4*>(xr) = make_uint4(0, 0, 0, 0);
@@ -492,30 +496,32 @@ extern "C" int vpt_timestep_embed(const float* vals, int R, void* out, void* str
 }
 
 extern "C" int vpt_assemble_tokens(const void* patches, const void* size_emb, const void* time_emb, const void* tpe,
-                                   const void* ctx, int n_ctx, int B, int np_, int rows, void* x, void* stream) {
+                                   const void* ctx, int n_ctx, int B, int np_, int rows, int D, void* x,
+                                   void* stream) {
   VPT_CHECK_ARG(patches && size_emb && time_emb && tpe && x, "vpt_assemble_tokens: null pointer");
-  VPT_CHECK_ARG(rows >= np_ + 10, "vpt_assemble_tokens: rows too small");
-  hipLaunchKernelGGL(assemble_kernel, grid1((long)B * rows * 96), dim3(256), 0, (hipStream_t)stream,
+  VPT_CHECK_ARG(rows >= np_ + 10 && D % 8 == 0 && D > 0, "vpt_assemble_tokens: rows too small or D % 8 != 0");
+  hipLaunchKernelGGL(assemble_kernel, grid1((long)B * rows * (D / 8)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)patches, (const bf16_t*)size_emb, (const bf16_t*)time_emb, (const bf16_t*)tpe,
-                     (const bf16_t*)ctx, n_ctx, B, np_, rows, (bf16_t*)x);
+                     (const bf16_t*)ctx, n_ctx, B, np_, rows, D, (bf16_t*)x);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
 
-extern "C" int vpt_disassemble_tokens(const void* dx, int B, int np_, int rows, void* dpatches, void* dsize,
+extern "C" int vpt_disassemble_tokens(const void* dx, int B, int np_, int rows, int D, void* dpatches, void* dsize,
                                       void* dtime, float* dtpe, void* stream) {
-  VPT_CHECK_ARG(dx && dpatches && dsize && dtime, "vpt_disassemble_tokens: null pointer");
-  hipLaunchKernelGGL(disassemble_kernel, grid1((long)B * (np_ + 7) * 96), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)dx, B, np_, rows, (bf16_t*)dpatches, (bf16_t*)dsize, (bf16_t*)dtime, dtpe);
+  VPT_CHECK_ARG(dx && dpatches && dsize && dtime && D % 8 == 0 && D > 0, "vpt_disassemble_tokens: bad args");
+  hipLaunchKernelGGL(disassemble_kernel, grid1((long)B * (np_ + 7) * (D / 8)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)dx, B, np_, rows, D, (bf16_t*)dpatches, (bf16_t*)dsize, (bf16_t*)dtime, dtpe);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
 
-extern "C" int vpt_ctx_rows(void* x, int B, int row0, int rows, const void* ctx, float* dctx, int n_ctx, int backward,
-                            void* stream) {
-  VPT_CHECK_ARG(x && n_ctx > 0 && (backward ? dctx != nullptr : ctx != nullptr), "vpt_ctx_rows: bad args");
-  hipLaunchKernelGGL(ctx_rows_kernel, grid1((long)B * n_ctx * 96), dim3(256), 0, (hipStream_t)stream, (bf16_t*)x, B,
-                     row0, rows, (const bf16_t*)ctx, dctx, n_ctx, backward);
+extern "C" int vpt_ctx_rows(void* x, int B, int row0, int rows, int D, const void* ctx, float* dctx, int n_ctx,
+                            int backward, void* stream) {
+  VPT_CHECK_ARG(x && n_ctx > 0 && D % 8 == 0 && row0 + n_ctx <= rows && (backward ? dctx != nullptr : ctx != nullptr),
+                "vpt_ctx_rows: bad args");
+  hipLaunchKernelGGL(ctx_rows_kernel, grid1((long)B * n_ctx * (D / 8)), dim3(256), 0, (hipStream_t)stream, (bf16_t*)x,
+                     B, row0, rows, D, (const bf16_t*)ctx, dctx, n_ctx, backward);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

@@ -38,9 +38,9 @@ SIGNATURES: dict[str, list] = {
     "vpt_loss_blocks": [],
     "vpt_flow_loss": [P, P, P, P, F, U64, I, F, I, I, I, P, P, P, P],
     "vpt_timestep_embed": [P, I, P, P],
-    "vpt_assemble_tokens": [P, P, P, P, P, I, I, I, I, P, P],
-    "vpt_disassemble_tokens": [P, I, I, I, P, P, P, P, P],
-    "vpt_ctx_rows": [P, I, I, I, P, P, I, I, P],
+    "vpt_assemble_tokens": [P, P, P, P, P, I, I, I, I, I, P, P],
+    "vpt_disassemble_tokens": [P, I, I, I, I, P, P, P, P, P],
+    "vpt_ctx_rows": [P, I, I, I, I, P, P, I, I, P],
     "vpt_swiglu_fwd": [P, L, I, P, P],
     "vpt_swiglu_bwd": [P, P, L, I, P, P],
     "vpt_colsum_blocks": [L],

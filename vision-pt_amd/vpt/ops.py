@@ -198,17 +198,17 @@ def timestep_embed(vals, out):
 
 def assemble_tokens(patches, size_emb, time_emb, tpe, ctx, n_ctx, B, np_, rows, x):
     call("vpt_assemble_tokens", patches.data_ptr(), size_emb.data_ptr(), time_emb.data_ptr(), tpe.data_ptr(),
-         _p(ctx), n_ctx, B, np_, rows, x.data_ptr(), stream())
+         _p(ctx), n_ctx, B, np_, rows, x.shape[1], x.data_ptr(), stream())
     return x
 
 
 def disassemble_tokens(dx, B, np_, rows, dpatches, dsize, dtime, dtpe):
-    call("vpt_disassemble_tokens", dx.data_ptr(), B, np_, rows, dpatches.data_ptr(), dsize.data_ptr(),
+    call("vpt_disassemble_tokens", dx.data_ptr(), B, np_, rows, dx.shape[1], dpatches.data_ptr(), dsize.data_ptr(),
          dtime.data_ptr(), _p(dtpe), stream())
 
 
 def ctx_rows(x, B, row0, rows, n_ctx, ctx=None, dctx=None, backward=False):
-    call("vpt_ctx_rows", x.data_ptr(), B, row0, rows, _p(ctx), _p(dctx), n_ctx, int(backward), stream())
+    call("vpt_ctx_rows", x.data_ptr(), B, row0, rows, x.shape[1], _p(ctx), _p(dctx), n_ctx, int(backward), stream())
 
 
 def swiglu_fwd(x12, h):

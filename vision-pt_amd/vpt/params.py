@@ -67,7 +67,9 @@ def param_shapes(cfg: DenoiserConfig, n_classes: int | None) -> list[tuple[str, 
            "w_3.weight": (D, F), "w_3.bias": (D,)}
     for i in range(cfg.depth):
         for n in block_param_names(i):
-            out.append((n, blk[n.split(".", 2)[2].split(".", 1)[1]]))
+            suffix = n.split(".", 2)[2]                       # e.g. "attn.to_q.weight", "norm1.weight"
+            key = suffix.split(".", 1)[1] if suffix.startswith(("attn.", "mlp.")) else suffix
+            out.append((n, blk[key]))
     out += [
         ("final_layer.norm_final.weight", (D,)),
         ("final_layer.mlp.w_1.weight", (F, D)), ("final_layer.mlp.w_2.weight", (F, D)),
