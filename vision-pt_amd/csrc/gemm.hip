@@ -88,6 +88,48 @@ __device__ __forceinline__ void store_tile(char* lds, const uint4 (&r)[4], int t
   }
 }
 
+// LDS-DMA staging of one full 64-deep operand tile (16 KB = 16 wave-instructions of 1 KB; wave `wid`
+// issues 4). The LDS image is written lane-linearly (dst = base + 16*lane), so the XOR swizzle of
+// kmaj_off / mnmaj_off is applied to each lane's GLOBAL source address instead (guide rule 21).
+// Rows past the matrix edge are clamped to a valid row: they only feed output rows/cols that are
+// never stored. K must be a full tile here (partial K tiles go through load_tile/store_tile).
+// One 16-B-per-lane LDS-DMA (1 KB per wave) in inline asm, so that hipcc's waitcnt pass does not
+// serialise it against the ds_reads of the other buffer (it cannot prove the two do not alias);
+// completion is waited for explicitly with `s_waitcnt vmcnt(0)` before the K-step barrier.
+// M0 holds the wave-uniform LDS destination and is restored (guide §5.7 LDS-DMA recipe).
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_addr)
+               : "memory");
+}
+
+template <bool KMAJ>
+__device__ __forceinline__ void glds_tile(char* lds, const bf16_t* __restrict__ base, long ld, int row0, int nrows,
+                                          int k0, int wid, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = wid * 4 + i;
+    const bf16_t* src;
+    if (KMAJ) {
+      const int row = q * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      int gr = row0 + row;
+      gr = gr < nrows ? gr : nrows - 1;
+      src = base + (long)gr * ld + k0 + c * 8;
+    } else {
+      const int krow = q * 4 + (lane >> 4);
+      const int c = (lane & 15) ^ (mnmaj_f(krow) << 1);
+      int gm = row0 + c * 8;
+      gm = gm < nrows ? gm : 0;
+      src = base + (long)(k0 + krow) * ld + gm;
+    }
+    const uint32_t dst = (uint32_t)(uintptr_t)(VPT_LDS char*)(lds + q * 1024);
+    glds16((const void*)src, __builtin_amdgcn_readfirstlane(dst));
+  }
+}
+
 // Fragment for a 16(row) x 32(k) MFMA operand: lane holds row (lane&15), k = 8*(lane>>4)+0..7.
 template <bool KMAJ>
 __device__ __forceinline__ bf16x8 read_frag(const char* lds, int row_base, int kk, int lane) {
@@ -102,6 +144,26 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int row_base, int k
     uint2 lo = lds_read_tr16((const VPT_LDS void*)(lds + mnmaj_off(k0, unit)));
     uint2 hi = lds_read_tr16((const VPT_LDS void*)(lds + mnmaj_off(k0 + 4, unit)));
     return as_frag2(lo, hi);
+  }
+}
+
+// One 64-deep K step of the block tile: each wave reads its 4 A and 4 B fragments per 32-k half
+// and issues 16 MFMA 16x16x32 into its 64x64 accumulator.
+template <bool AK, bool BK_>
+__device__ __forceinline__ void mma_tile(const char* la, floatx4 (&acc)[4][4], int wm, int wn, int lane) {
+  const char* lb = la + 16384;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    bf16x8 af[4], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = read_frag<AK>(la, wm * 64 + i * 16, kk, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = read_frag<BK_>(lb, wn * 64 + j * 16, kk, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
   }
 }
 
@@ -121,7 +183,9 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
 
   const int kbeg = blockIdx.y * g.k_split;
   const int kend = min(g.K, kbeg + g.k_split);
-  const int nk = (kend - kbeg + BK - 1) / BK;
+  const int nfull = (kend - kbeg) / BK;
+  const bool ktail = (kend - kbeg) % BK != 0;
+  const int nk = nfull + (ktail ? 1 : 0);
 
   floatx4 acc[4][4];
 #pragma unroll
@@ -129,42 +193,39 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[4], rb[4];
-  load_tile<AK>(ra, g.A, g.lda, m0, g.M, kbeg, kend, tid);
-  load_tile<BK_>(rb, g.B, g.ldb, n0, g.N, kbeg, kend, tid);
-  store_tile<AK>(smem, ra, tid);
-  store_tile<BK_>(smem + 16384, rb, tid);
-  __syncthreads();
-
+  // Main loop over the full K tiles: LDS-DMA only (no ordinary VGPR loads in the loop, so hipcc
+  // does not insert a vmcnt(0) ahead of the ds_reads); the next tile lands while this one computes.
   int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    const bool more = kt + 1 < nk;
-    if (more) {
-      load_tile<AK>(ra, g.A, g.lda, m0, g.M, kbeg + (kt + 1) * BK, kend, tid);
-      load_tile<BK_>(rb, g.B, g.ldb, n0, g.N, kbeg + (kt + 1) * BK, kend, tid);
-    }
-    const char* la = smem + cur * 32768;
-    const char* lb = la + 16384;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[4], bfr[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = read_frag<AK>(la, wm * 64 + i * 16, kk, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = read_frag<BK_>(lb, wn * 64 + j * 16, kk, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    if (more) {
-      char* nb = smem + (cur ^ 1) * 32768;
-      store_tile<AK>(nb, ra, tid);
-      store_tile<BK_>(nb + 16384, rb, tid);
-    }
+  if (nfull > 0) {
+    glds_tile<AK>(smem, g.A, g.lda, m0, g.M, kbeg, wid, lane);
+    glds_tile<BK_>(smem + 16384, g.B, g.ldb, n0, g.N, kbeg, wid, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  }
+  for (int kt = 0; kt < nfull; ++kt) {
+    if (kt + 1 < nfull) {
+      char* nb = smem + (cur ^ 1) * 32768;
+      const int kn = kbeg + (kt + 1) * BK;
+      glds_tile<AK>(nb, g.A, g.lda, m0, g.M, kn, wid, lane);
+      glds_tile<BK_>(nb + 16384, g.B, g.ldb, n0, g.N, kn, wid, lane);
+    }
+    mma_tile<AK, BK_>(smem + cur * 32768, acc, wm, wn, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA for tile kt+1 has landed
+    __syncthreads();                                   // ... and every other wave's too
     cur ^= 1;
+  }
+  // Partial last K tile (wgrad over a token count that is not a multiple of 64): zero-filled
+  // register loads into the free buffer.
+  if (ktail) {
+    uint4 ra[4], rb[4];
+    const int kn = kbeg + nfull * BK;
+    load_tile<AK>(ra, g.A, g.lda, m0, g.M, kn, kend, tid);
+    load_tile<BK_>(rb, g.B, g.ldb, n0, g.N, kn, kend, tid);
+    store_tile<AK>(smem + cur * 32768, ra, tid);
+    store_tile<BK_>(smem + cur * 32768 + 16384, rb, tid);
+    __syncthreads();
+    mma_tile<AK, BK_>(smem + cur * 32768, acc, wm, wn, lane);
+    __syncthreads();
   }
 
   // ---- epilogue: stage the wave's 64x64 f32 tile in LDS, then vectorised row pass ----

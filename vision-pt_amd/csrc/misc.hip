@@ -302,22 +302,33 @@ __global__ void swiglu_bwd_kernel(const bf16_t* __restrict__ dh, const bf16_t* _
 }
 
 // ---------------------------------------------------------------- column sums (bias grads)
+// Column sums of a bf16 [M][N] matrix into f32 partial rows part[slice][N]. Grid (N/256, slices);
+// block = 32 lanes x 16-B chunks (256 columns, 512 B per row segment) x 8 row groups.
 __global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ in, long ld, long M, int N,
-                                                     long rows_per_block, float* __restrict__ part) {
-  const int nch = N >> 3;
-  const long r0 = (long)blockIdx.x * rows_per_block;
-  const long r1 = min(M, r0 + rows_per_block);
-  for (int ch = threadIdx.x; ch < nch; ch += 256) {
-    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (long r = r0; r < r1; ++r) {
+                                                     long rows_per_slice, float* __restrict__ part) {
+  __shared__ float red[8][257];
+  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int col = blockIdx.x * 256 + cl * 8;
+  const long r0 = (long)blockIdx.y * rows_per_slice;
+  const long r1 = min(M, r0 + rows_per_slice);
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (col < N) {
+    for (long r = r0 + rg; r < r1; r += 8) {
       float f[8];
-      unpack8(*reinterpret_cast<const uint4*>(in + r * ld + ch * 8), f);
+      unpack8(*reinterpret_cast<const uint4*>(in + r * ld + col), f);
 #pragma unroll
       for (int e = 0; e < 8; ++e) s[e] += f[e];
     }
-    floatx4* d = reinterpret_cast<floatx4*>(part + (long)blockIdx.x * N + ch * 8);
-    d[0] = floatx4{s[0], s[1], s[2], s[3]};
-    d[1] = floatx4{s[4], s[5], s[6], s[7]};
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rg][cl * 8 + e] = s[e];
+  __syncthreads();
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c < N) {
+    float t = red[0][threadIdx.x];
+#pragma unroll
+    for (int g = 1; g < 8; ++g) t += red[g][threadIdx.x];
+    part[(long)blockIdx.y * N + c] = t;
   }
 }
 
@@ -542,17 +553,17 @@ extern "C" int vpt_swiglu_bwd(const void* dh, const void* x12, long M, int F, vo
   return VPT_OK;
 }
 
-extern "C" int vpt_colsum_blocks(long M) {
-  long b = (M + 63) / 64;
-  return (int)(b > 256 ? 256 : (b < 1 ? 1 : b));
+extern "C" int vpt_colsum_blocks(long M) {  // number of partial rows written by vpt_colsum
+  long b = (M + 255) / 256;
+  return (int)(b > 64 ? 64 : (b < 1 ? 1 : b));
 }
 
 extern "C" int vpt_colsum(const void* in, long ld, long M, int N, float* part, void* stream) {
   VPT_CHECK_ARG(in && part && N % 8 == 0 && M > 0, "vpt_colsum: bad args");
   const int nb = vpt_colsum_blocks(M);
   const long per = (M + nb - 1) / nb;
-  hipLaunchKernelGGL(colsum_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)in, ld, M, N, per,
-                     part);
+  hipLaunchKernelGGL(colsum_kernel, dim3((N + 255) / 256, nb), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)in,
+                     ld, M, N, per, part);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

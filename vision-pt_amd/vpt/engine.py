@@ -226,7 +226,7 @@ class JiTEngine:
         return i == cs or (not self.cfg.do_context_fuse and i > cs)
 
     # ------------------------------------------------------------------ backward
-    def backward(self, dout: torch.Tensor, zero_grads: bool = True) -> torch.Tensor | None:
+    def backward(self, dout: torch.Tensor, zero_grads: bool = True, on_ready=None) -> torch.Tensor | None:
         """dout [B*N_p, P*P*C] bf16 gradient of the patch-layout output. Fills self.grads (f32;
         accumulates when zero_grads=False) and returns d(ctx_raw) [B*n_ctx, context_dim] bf16."""
         st = self._state
@@ -269,6 +269,8 @@ class JiTEngine:
         dxf, part = ops.rmsnorm_bwd(dxnf, xf, rstdf, f["pn"], dx=pool.get("d_c", (M2, D)),
                                     dw_part=pool.get("rms_part", (ops.rmsnorm_bwd_blocks(max(M, M2)), D), F32))
         ops.reduce_rows(part[:ops.rmsnorm_bwd_blocks(M2)], f["gn"], acc)
+        if on_ready is not None:
+            on_ready("final")  # every final_layer.* gradient is enqueued
         dx = pool.get("dx_a", (M, D), zero=True)
         ops.copy_rows(dx, rows, 0, np_, dxf, B, reverse=True)
         # --- blocks in reverse
@@ -321,6 +323,8 @@ class JiTEngine:
             dx_new, part = ops.rmsnorm_bwd(dxn1, x_in, rstd1, w["pn1"], dres=dxm, dx=pool.get("dx_a", (M, D)),
                                            dw_part=pool.get("rms_part", (ops.rmsnorm_bwd_blocks(max(M, M2)), D), F32))
             ops.reduce_rows(part[:ops.rmsnorm_bwd_blocks(M)], w["gn1"], acc)
+            if on_ready is not None:
+                on_ready(f"block{i}")  # every blocks.{i}.* gradient is enqueued
             dx = dx_new
             if n_ctx and self._ctx_refresh(i):
                 ops.ctx_rows(dx, B, n_pre, rows, n_ctx, dctx=dctx, backward=True)

@@ -22,6 +22,39 @@ def stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
+class KernelProbe:
+    """Brackets every launch of one op with HIP events on the launching stream (used by bench.py
+    to time the dominant kernel inside the timed region). `flops_fn(**shape)` gives the
+    algorithmic FLOPs of one launch."""
+
+    def __init__(self, op: str):
+        self.op = op
+        self.records: list[tuple] = []
+        self.active = False
+
+    def record(self, flops: float, fn):
+        if not self.active:
+            return fn()
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        r = fn()
+        e.record()
+        self.records.append((s, e, flops))
+        return r
+
+    def summary(self):
+        """(launches, mean ms per launch, mean algorithmic FLOPs per launch)."""
+        if not self.records:
+            return 0, 0.0, 0.0
+        ms = [s.elapsed_time(e) for s, e, _ in self.records]
+        fl = [f for _, _, f in self.records]
+        return len(ms), sum(ms) / len(ms), sum(fl) / len(fl)
+
+
+PROBES: dict[str, KernelProbe] = {}
+
+
 def _p(t: torch.Tensor | None):
     return None if t is None else t.data_ptr()
 
@@ -48,9 +81,16 @@ def gemm(a, a_kmajor: bool, b, b_kmajor: bool, M: int, N: int, K: int, out, *, b
         _chk(resid, BF16, "resid")
     if splits > 1 and workspace is None:
         workspace = torch.empty(splits * M * N, dtype=F32, device=out.device)
-    call("vpt_gemm_bf16", a.data_ptr(), a.stride(0), int(a_kmajor), b.data_ptr(), b.stride(0), int(b_kmajor),
-         out.data_ptr(), out.stride(0), M, N, K, _p(bias), _p(resid), 0 if resid is None else resid.stride(0),
-         out_mode, act, splits, _p(workspace), stream())
+
+    def run():
+        call("vpt_gemm_bf16", a.data_ptr(), a.stride(0), int(a_kmajor), b.data_ptr(), b.stride(0), int(b_kmajor),
+             out.data_ptr(), out.stride(0), M, N, K, _p(bias), _p(resid), 0 if resid is None else resid.stride(0),
+             out_mode, act, splits, _p(workspace), stream())
+    pr = PROBES.get("gemm")
+    if pr is None:
+        run()
+    else:
+        pr.record(2.0 * M * N * K, run)
     return out
 
 
@@ -159,13 +199,23 @@ def _t4(t, B: int, rows: int, H: int, col0: int = 0):
 
 def attn_fwd(q, k, v, o, lse, kbias, B, H, rows, n, n_dense, scale=0.125):
     """q/k/v/o as (ptr, sb, sh, sr) tuples (element strides); lse [B,H,rows] f32; kbias [B,rows] f32 or None."""
-    call("vpt_attn_fwd", *q, *k, *v, *o, lse.data_ptr(), lse.stride(0), lse.stride(1),
-         _p(kbias), 0 if kbias is None else kbias.stride(0), B, H, n, n_dense, scale, stream())
+    def run():
+        call("vpt_attn_fwd", *q, *k, *v, *o, lse.data_ptr(), lse.stride(0), lse.stride(1),
+             _p(kbias), 0 if kbias is None else kbias.stride(0), B, H, n, n_dense, scale, stream())
+    pr = PROBES.get("attn_fwd")
+    if pr is None:
+        return run()
+    return pr.record(4.0 * B * H * n * n * 64, run)  # QK^T + PV over all (query, key) pairs
 
 
 def attn_bwd(q, k, v, o, do, lse, delta, kbias, dq, dk, dv, B, H, rows, n, n_dense, scale=0.125):
-    call("vpt_attn_bwd", *q, *k, *v, *o, *do, lse.data_ptr(), delta.data_ptr(), lse.stride(0), lse.stride(1),
-         _p(kbias), 0 if kbias is None else kbias.stride(0), *dq, *dk, *dv, B, H, n, n_dense, scale, stream())
+    def run():
+        call("vpt_attn_bwd", *q, *k, *v, *o, *do, lse.data_ptr(), delta.data_ptr(), lse.stride(0), lse.stride(1),
+             _p(kbias), 0 if kbias is None else kbias.stride(0), *dq, *dk, *dv, B, H, n, n_dense, scale, stream())
+    pr = PROBES.get("attn_bwd")
+    if pr is None:
+        return run()
+    return pr.record(8.0 * B * H * n * n * 64, run)  # dV, dP, dK, dQ products (algorithmic 2x forward)
 
 
 # ----------------------------------------------------------------------------- misc

@@ -82,7 +82,9 @@ class RAdamScheduleFreeFlat:
                     adaptive_y_lr=lr * (beta1 * (1 - ckp1) - 1), beta2=beta2)
 
     @torch.no_grad()
-    def step(self, grad_scale: float = 1.0):
+    def begin_step(self) -> dict:
+        """Computes this step's scalars; the update itself is applied range by range (so each
+        all-reduced gradient bucket can be stepped as soon as it lands) and closed by end_step."""
         g = self.param_groups[0]
         if not g["train_mode"]:
             raise RuntimeError("Optimizer was not in train mode when step is called. "
@@ -90,14 +92,29 @@ class RAdamScheduleFreeFlat:
         if not self._initialised:
             ops.sf_init(self.params, self.z, self.v)
             self._initialised = True
-        s = self.scalars()
-        ops.radam_sf_step(self.params, self.grads, self.z, self.v, beta2=s["beta2"], bias_correction2=s["bc2"],
-                          eps=g["eps"], ckp1=s["ckp1"], adaptive_y_lr=s["adaptive_y_lr"], lr=s["lr"],
-                          decay=g["weight_decay"], grad_scale=grad_scale, adam=s["adam"])
+        return self.scalars()
+
+    @torch.no_grad()
+    def apply_range(self, s: dict, lo: int, hi: int, grad_scale: float = 1.0):
+        g = self.param_groups[0]
+        if hi <= lo:
+            return
+        ops.radam_sf_step(self.params[lo:hi], self.grads[lo:hi], self.z[lo:hi], self.v[lo:hi], beta2=s["beta2"],
+                          bias_correction2=s["bc2"], eps=g["eps"], ckp1=s["ckp1"], adaptive_y_lr=s["adaptive_y_lr"],
+                          lr=s["lr"], decay=g["weight_decay"], grad_scale=grad_scale, adam=s["adam"])
+
+    def end_step(self, s: dict):
+        g = self.param_groups[0]
         g["scheduled_lr"] = s["lr"]
         g["lr_max"] = s["lr_max"]
         g["weight_sum"] = s["weight_sum"]
         g["k"] = g["k"] + 1
+
+    @torch.no_grad()
+    def step(self, grad_scale: float = 1.0):
+        s = self.begin_step()
+        self.apply_range(s, 0, self.params.numel(), grad_scale)
+        self.end_step(s)
 
     def zero_grad(self, set_to_none: bool = False):
         self.grads.zero_()
