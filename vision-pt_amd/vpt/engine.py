@@ -66,6 +66,7 @@ class JiTEngine:
         self.params = params if params is not None else torch.zeros(self.layout.total, dtype=BF16, device=self.device)
         self.grads = grads if grads is not None else torch.zeros(self.layout.total, dtype=F32, device=self.device)
         self.pool = _Pool(self.device)
+        self.pool_infer = _Pool(self.device)  # no-grad forwards never clobber saved activations
         self.rope = RopeCache(cfg, self.device)
         self.D = cfg.hidden_size
         self.F = cfg.mlp_hidden
@@ -155,7 +156,8 @@ class JiTEngine:
         bf16-rounded timestep times timestep_scale); size_vals [6B] f32; ctx_raw [B*n_ctx,
         context_dim] bf16; kbias [B, rows] f32 additive key bias (0 / -inf) or None.
         Returns the final-layer output in patch layout [B*N_p, P*P*C] (per patch (py, px, c))."""
-        cfg, pool, D, F, Hh = self.cfg, self.pool, self.D, self.F, self.H
+        cfg, D, F, Hh = self.cfg, self.D, self.F, self.H
+        pool = self.pool if save else self.pool_infer
         hp, wp, np_, rows = self.shape_info(B, H, W, n_ctx)
         M = B * rows
         n_pre = np_ + 6 + self.T           # tokens attended before context_start_block
