@@ -41,6 +41,8 @@ int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* B, long ldb
                   long ldc, int M, int N, int K, const void* bias, const void* resid, long ldr, int out_mode,
                   int act, int splits, void* workspace, void* stream);
 long vpt_gemm_workspace_bytes(int M, int N, int K, int splits);
+/* Tile geometry: 0 = automatic (default), 128 or 256 forces the 128x128 / 256x256 kernel (benchmarking). */
+int vpt_gemm_set_geometry(int geo);
 
 /* ---- flash attention, head_dim 64 ---------------------------------------------------------
  * Tensors addressed p[b*sb + h*sh + row*sr + d]. Keys < n_dense always valid; keys in

@@ -82,6 +82,27 @@ def test_gemm_wgrad(ops, M, N, K, splits):
     assert rel(out, 2 * ref) < 1e-5
 
 
+@pytest.mark.parametrize("geo", [128, 256])
+@pytest.mark.parametrize("M,N,K", [(700, 264, 200), (300, 512, 136), (2100, 768, 768)])
+def test_gemm_geometries_all_directions(ops, geo, M, N, K):
+    """Both tile geometries, all three GEMM directions, ragged M/N and partial K tiles
+    (K % 64 != 0 exercises the clamped-DMA + LDS zeroing path for k-major and mn-major tiles)."""
+    ops.lib.vpt_gemm_set_geometry(geo)
+    try:
+        x = rnd(M, K, seed=80)
+        w = rnd(N, K, scale=0.05, seed=81)
+        b = rnd(N, scale=0.1, seed=82)
+        dy = rnd(M, N, seed=83)
+        assert rel(ops.linear(x, w, bias=b), x.float() @ w.float().t() + b.float()) < 5e-3
+        assert rel(ops.linear_dgrad(dy, w), dy.float() @ w.float()) < 5e-3
+        out = torch.empty(N, K, dtype=torch.float32, device=DEV)
+        for splits in (1, 3):
+            ops.linear_wgrad(dy, x, out, splits=splits)
+            assert rel(out, dy.float().t() @ x.float()) < 1e-5
+    finally:
+        ops.lib.vpt_gemm_set_geometry(0)
+
+
 def test_gemm_split_matches_unsplit(ops):
     M, N, K = 2048, 384, 256
     dy, x = rnd(M, N, seed=12), rnd(M, K, seed=13)

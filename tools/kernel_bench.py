@@ -50,14 +50,19 @@ def main():
             dw = torch.empty(N, K, dtype=torch.float32, device=dev)
             fl = 2.0 * M * N * K
             sp = ops.wgrad_splits(N, K, M)
-            t = {
-                "fwd": timeit(lambda: ops.linear(x, w, out=y)),
-                "dgrad": timeit(lambda: ops.linear_dgrad(dy, w, out=dx)),
-                "wgrad": timeit(lambda: ops.linear_wgrad(dy, x, dw, splits=sp, workspace=ws)),
+            t = {}
+            for geo in (0, 128, 256):
+                ops.lib.vpt_gemm_set_geometry(geo)
+                sfx = {0: "", 128: "@128", 256: "@256"}[geo]
+                t["fwd" + sfx] = timeit(lambda: ops.linear(x, w, out=y))
+                t["dgrad" + sfx] = timeit(lambda: ops.linear_dgrad(dy, w, out=dx))
+                t["wgrad" + sfx] = timeit(lambda: ops.linear_wgrad(dy, x, dw, splits=sp, workspace=ws))
+            ops.lib.vpt_gemm_set_geometry(0)
+            t.update({
                 "torch_fwd": timeit(lambda: torch.matmul(x, w.t())),
                 "torch_dgrad": timeit(lambda: torch.matmul(dy, w)),
                 "torch_wgrad": timeit(lambda: torch.matmul(dy.t(), x)),
-            }
+            })
             for k, ms in t.items():
                 res.setdefault(f"{name}.{k}", []).append(fl / (ms * 1e-3) / 1e12)
         # attention at the 1024x1024 bucket

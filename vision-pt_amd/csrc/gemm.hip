@@ -8,22 +8,25 @@
 //   dgrad    dX = dY . W   : A = dY [M][N] (k-major),  B = W [N][K] stored [red][out] (mn-major)
 //   wgrad    dW = dY^T . X : A = dY stored [red][out], B = X stored [red][out] (both mn-major)
 //
-// Tile 128x128x64, 256 threads = 4 waves in 2x2, each wave 64x64 = 4x4 MFMA 16x16x32 bf16.
-// k-major tiles are staged [row][64k] (128 B rows, 16-B chunk XOR swizzle, read with
-// ds_read_b128); mn-major tiles are staged in their global [k][128mn] orientation (256 B rows,
-// 8-B unit XOR swizzle) and read with ds_read_b64_tr_b16, which delivers the transpose.
-// Register-staged double buffering, one barrier per K step, XCD-aware block remap,
-// epilogue staged through LDS so bias/residual/activation and stores are 8-16 B per lane.
-// Optional split-K writes f32 partial slabs (reduced by vpt_splitk_reduce).
+// Two geometries of one kernel template, BK = 64, MFMA 16x16x32 bf16:
+//   T128: 128x128 block tile, 4 waves (2x2) of 64x64, 2 blocks/CU   (small grids / N = 768)
+//   T256: 256x256 block tile, 8 waves (2x4) of 128x64, 1 block/CU   (large grids): 64 MFMA per wave
+//         per K step cover the LDS-DMA latency of the next tile, and 128x64 wave tiles cut LDS read
+//         traffic per FLOP by 25 % vs 64x64.
+// k-major tiles are staged [row][64k] (128 B rows, 16-B chunk XOR swizzle, read with ds_read_b128);
+// mn-major tiles keep their global [k][mn] orientation (8-B unit XOR swizzle) and are read with
+// ds_read_b64_tr_b16, which delivers the transpose. Full K tiles arrive by LDS-DMA
+// (global_load_lds_dwordx4, swizzle moved to the source address), issued one K step ahead into a
+// 2-stage ring; one barrier per K step; the partial last K tile (wgrad over a token count) is DMA'd
+// with clamped addresses and its out-of-range part zeroed in LDS. XCD-aware bijective block remap. Epilogue staged through
+// LDS (f32, 64 rows at a time) so bias / residual / SiLU and stores are 8-16 B per lane. Optional
+// split-K writes f32 partial slabs, summed in a fixed order by splitk_reduce_kernel.
 #include "common.h"
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int EPI_LD = 68;                         // f32 staging row stride (floats), conflict-free
-constexpr int LDS_MAIN = 2 * 2 * 16384;            // [buf][A/B] 16 KB tiles
-constexpr int LDS_EPI = 4 * 64 * EPI_LD * 4;       // 4 waves x 64x68 f32
-constexpr int LDS_BYTES = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
+constexpr int BK = 64;
+constexpr int EPI_LD = 68;  // f32 staging row stride (floats), conflict-free for the column writes
 
 enum { OUT_BF16 = 0, OUT_F32 = 1, OUT_F32_ACC = 2 };
 enum { ACT_NONE = 0, ACT_SILU = 1 };
@@ -40,98 +43,95 @@ struct GemmArgs {
   int out_mode, act;
 };
 
-__device__ __forceinline__ int kmaj_off(int row, int chunk) {  // bytes in a [128][64] bf16 tile
+// ---- LDS images -----------------------------------------------------------------------------
+__device__ __forceinline__ int kmaj_off(int row, int chunk) {  // [R][64] bf16, 128-B rows
   return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
 __device__ __forceinline__ int mnmaj_f(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
-__device__ __forceinline__ int mnmaj_off(int krow, int unit) {   // bytes in a [64][128] bf16 tile
-  return krow * 256 + ((unit ^ (mnmaj_f(krow) << 2)) << 3);
+template <int R>
+__device__ __forceinline__ int mnmaj_off(int krow, int unit) {  // [64][R] bf16, 2R-byte rows
+  return krow * (2 * R) + ((unit ^ (mnmaj_f(krow) << 2)) << 3);
 }
 
-// Loads one operand tile (rows = output dim, 128 of them; 64 along k) into 4 uint4 registers.
-template <bool KMAJ>
-__device__ __forceinline__ void load_tile(uint4 (&r)[4], const bf16_t* __restrict__ base, long ld,
-                                          int row0, int nrows, int k0, int kend, int tid) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = tid + 256 * i;
-    if (KMAJ) {
-      const int row = c >> 3, kc = c & 7;
-      const int gr = row0 + row, gk = k0 + kc * 8;
-      if (gr < nrows && gk < kend)
-        r[i] = *reinterpret_cast<const uint4*>(base + (long)gr * ld + gk);
-      else
-        r[i] = make_uint4(0, 0, 0, 0);
-    } else {
-      const int krow = c >> 4, mc = c & 15;
-      const int gk = k0 + krow, gm = row0 + mc * 8;
-      if (gk < kend && gm < nrows)
-        r[i] = *reinterpret_cast<const uint4*>(base + (long)gk * ld + gm);
-      else
-        r[i] = make_uint4(0, 0, 0, 0);
-    }
-  }
-}
-
-template <bool KMAJ>
-__device__ __forceinline__ void store_tile(char* lds, const uint4 (&r)[4], int tid) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = tid + 256 * i;
-    int off;
-    if (KMAJ) {
-      off = kmaj_off(c >> 3, c & 7);
-    } else {
-      off = mnmaj_off(c >> 4, (c & 15) * 2);
-    }
-    *reinterpret_cast<uint4*>(lds + off) = r[i];
-  }
-}
-
-// LDS-DMA staging of one full 64-deep operand tile (16 KB = 16 wave-instructions of 1 KB; wave `wid`
-// issues 4). The LDS image is written lane-linearly (dst = base + 16*lane), so the XOR swizzle of
-// kmaj_off / mnmaj_off is applied to each lane's GLOBAL source address instead (guide rule 21).
-// Rows past the matrix edge are clamped to a valid row: they only feed output rows/cols that are
-// never stored. K must be a full tile here (partial K tiles go through load_tile/store_tile).
 // One 16-B-per-lane LDS-DMA (1 KB per wave) in inline asm, so that hipcc's waitcnt pass does not
 // serialise it against the ds_reads of the other buffer (it cannot prove the two do not alias);
 // completion is waited for explicitly with `s_waitcnt vmcnt(0)` before the K-step barrier.
 // M0 holds the wave-uniform LDS destination and is restored (guide §5.7 LDS-DMA recipe).
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
+// saddr form: wave-uniform 64-bit base in SGPRs + 32-bit per-lane byte offset in one VGPR. The base
+// SGPRs come straight from v_readfirstlane: a VMEM read of a VALU-written SGPR needs wait states
+// that hipcc does not insert inside asm, hence the opening `s_nop 4` (guide §5.7 item 2).
+__device__ __forceinline__ void glds16(const void* sbase, uint32_t voff, uint32_t lds_addr) {
   unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_addr)
+               : "v"(voff), "s"(sbase), "s"(lds_addr)
                : "memory");
 }
 
-template <bool KMAJ>
-__device__ __forceinline__ void glds_tile(char* lds, const bf16_t* __restrict__ base, long ld, int row0, int nrows,
-                                          int k0, int wid, int lane) {
+// LDS-DMA of one full 64-deep operand tile of R rows (R*128 B = R/8 wave-instructions of 1 KB; each
+// of the NW waves issues R/(8*NW)). The image is written lane-linearly, so the XOR swizzle is
+// applied to each lane's GLOBAL source address (guide rule 21). Rows past the matrix edge are
+// clamped to a valid row: they only feed output rows/cols that are never stored.
+// `tile_base` is the wave-uniform address of element (row0, k0) [k-major] or (k0, row0) [mn-major].
+template <bool KMAJ, int R, int NW>
+__device__ __forceinline__ void glds_tile(char* lds, const bf16_t* tile_base, long ld, int row0, int nrows, int kvalid,
+                                          int wid, int lane) {
+  constexpr int PER_WAVE = R / (8 * NW);
+  const unsigned long long sb = (unsigned long long)tile_base;
+  // readfirstlane returns int: go through `unsigned` so the low word is zero-extended (a sign-extended
+  // low word with bit 31 set would OR 1s into the high word).
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)sb);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(sb >> 32));
+  const bf16_t* sbase = (const bf16_t*)(((unsigned long long)hi << 32) | lo);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int q = wid * 4 + i;
-    const bf16_t* src;
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int q = wid * PER_WAVE + i;
+    uint32_t off;
     if (KMAJ) {
       const int row = q * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ ((row >> 1) & 7);
-      int gr = row0 + row;
-      gr = gr < nrows ? gr : nrows - 1;
-      src = base + (long)gr * ld + k0 + c * 8;
+      int c = (lane & 7) ^ ((row >> 1) & 7);
+      c = c * 8 < kvalid ? c : 0;  // k past the end: any valid chunk, zeroed in LDS afterwards
+      int r = row0 + row < nrows ? row : nrows - 1 - row0;
+      off = (uint32_t)(((long)r * ld + c * 8) * 2);
     } else {
-      const int krow = q * 4 + (lane >> 4);
-      const int c = (lane & 15) ^ (mnmaj_f(krow) << 1);
-      int gm = row0 + c * 8;
-      gm = gm < nrows ? gm : 0;
-      src = base + (long)(k0 + krow) * ld + gm;
+      constexpr int CH = R / 8;  // 16-B chunks per k-row
+      const int krow = q * (64 / CH) + lane / CH;
+      const int c = (lane % CH) ^ (mnmaj_f(krow) << 1);
+      const int m = row0 + c * 8 < nrows ? c * 8 : nrows - 8 - row0;  // >= 0 (nrows % 8 == 0)
+      const int kr = krow < kvalid ? krow : kvalid - 1;               // zeroed in LDS afterwards
+      off = (uint32_t)(((long)kr * ld + m) * 2);
     }
     const uint32_t dst = (uint32_t)(uintptr_t)(VPT_LDS char*)(lds + q * 1024);
-    glds16((const void*)src, __builtin_amdgcn_readfirstlane(dst));
+    glds16((const void*)sbase, off, __builtin_amdgcn_readfirstlane(dst));
+  }
+}
+
+template <bool KMAJ>
+__device__ __forceinline__ const bf16_t* tile_ptr(const bf16_t* base, long ld, int row0, int k0) {
+  return KMAJ ? base + (long)row0 * ld + k0 : base + (long)k0 * ld + row0;
+}
+
+// Zeroes the k >= kvalid part of a staged tile (k-major: chunks kc*8 >= kvalid of every row;
+// mn-major: whole k-rows >= kvalid), so clamped DMA addresses never contribute to the product.
+template <bool KMAJ, int R, int T>
+__device__ __forceinline__ void zero_k_tail(char* lds, int kvalid, int tid) {
+  if (KMAJ) {
+    const int c0 = kvalid >> 3, nc = 8 - c0;
+    for (int idx = tid; idx < R * nc; idx += T) {
+      const int row = idx / nc, kc = c0 + idx % nc;
+      *reinterpret_cast<uint4*>(lds + kmaj_off(row, kc)) = make_uint4(0, 0, 0, 0);
+    }
+  } else {
+    constexpr int CH = R / 8;
+    for (int idx = tid; idx < (BK - kvalid) * CH; idx += T) {
+      const int krow = kvalid + idx / CH, ch = idx % CH;
+      *reinterpret_cast<uint4*>(lds + krow * (2 * R) + ch * 16) = make_uint4(0, 0, 0, 0);
+    }
   }
 }
 
 // Fragment for a 16(row) x 32(k) MFMA operand: lane holds row (lane&15), k = 8*(lane>>4)+0..7.
-template <bool KMAJ>
+template <bool KMAJ, int R>
 __device__ __forceinline__ bf16x8 read_frag(const char* lds, int row_base, int kk, int lane) {
   if (KMAJ) {
     const int row = row_base + (lane & 15);
@@ -141,154 +141,178 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int row_base, int k
     const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
     const int unit = (row_base >> 2) + p;
     const int k0 = kk * 32 + 8 * g + q;
-    uint2 lo = lds_read_tr16((const VPT_LDS void*)(lds + mnmaj_off(k0, unit)));
-    uint2 hi = lds_read_tr16((const VPT_LDS void*)(lds + mnmaj_off(k0 + 4, unit)));
+    uint2 lo = lds_read_tr16((const VPT_LDS void*)(lds + mnmaj_off<R>(k0, unit)));
+    uint2 hi = lds_read_tr16((const VPT_LDS void*)(lds + mnmaj_off<R>(k0 + 4, unit)));
     return as_frag2(lo, hi);
   }
 }
 
-// One 64-deep K step of the block tile: each wave reads its 4 A and 4 B fragments per 32-k half
-// and issues 16 MFMA 16x16x32 into its 64x64 accumulator.
-template <bool AK, bool BK_>
-__device__ __forceinline__ void mma_tile(const char* la, floatx4 (&acc)[4][4], int wm, int wn, int lane) {
-  const char* lb = la + 16384;
+template <int TM_, int TN_, int WGM, int WGN>
+struct Geo {
+  static constexpr int TM = TM_, TN = TN_;
+  static constexpr int NW = WGM * WGN, T = 64 * NW;
+  static constexpr int WR = TM / WGM, WC = TN / WGN;       // wave tile
+  static constexpr int MI = WR / 16, NI = WC / 16;         // MFMA fragments per wave
+  static constexpr int A_BYTES = TM * BK * 2, B_BYTES = TN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  static constexpr int EPI = NW * 64 * EPI_LD * 4;
+  static constexpr int LDS = 2 * STAGE > EPI ? 2 * STAGE : EPI;
+};
+
+// One 64-deep K step: per 32-k half each wave reads MI A and NI B fragments, issues MI*NI MFMAs.
+template <bool AK, bool BK_, typename G>
+__device__ __forceinline__ void mma_tile(const char* la, floatx4 (&acc)[G::MI][G::NI], int wm, int wn, int lane) {
+  const char* lb = la + G::A_BYTES;
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
-    bf16x8 af[4], bfr[4];
+    bf16x8 bfr[G::NI];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = read_frag<AK>(la, wm * 64 + i * 16, kk, lane);
+    for (int j = 0; j < G::NI; ++j) bfr[j] = read_frag<BK_, G::TN>(lb, wn * G::WC + j * 16, kk, lane);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bfr[j] = read_frag<BK_>(lb, wn * 64 + j * 16, kk, lane);
+    for (int i = 0; i < G::MI; ++i) {
+      const bf16x8 af = read_frag<AK, G::TM>(la, wm * G::WR + i * 16, kk, lane);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < G::NI; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+    }
   }
 }
 
-template <bool AK, bool BK_>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
+template <bool AK, bool BK_, int TM, int TN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_bf16_kernel(GemmArgs g) {
+  using G = Geo<TM, TN, WGM, WGN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WGN, wn = wid % WGN;
 
-  const int tiles_n = (g.N + BN - 1) / BN;
+  const int tiles_n = (g.N + TN - 1) / TN;
   const int nwg = gridDim.x;
   const int orig = blockIdx.x;
   const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   const int tm = wgid / tiles_n, tn = wgid % tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = tm * TM, n0 = tn * TN;
 
   const int kbeg = blockIdx.y * g.k_split;
   const int kend = min(g.K, kbeg + g.k_split);
   const int nfull = (kend - kbeg) / BK;
   const bool ktail = (kend - kbeg) % BK != 0;
+
+  floatx4 acc[G::MI][G::NI];
+#pragma unroll
+  for (int i = 0; i < G::MI; ++i)
+#pragma unroll
+    for (int j = 0; j < G::NI; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // Main loop: LDS-DMA only (no ordinary VGPR loads in the loop), next tile in flight while this one
+  // computes. A partial last K tile (wgrad over a token count) is DMA'd with clamped addresses and
+  // its out-of-range k rows / chunks are zeroed in LDS before it is consumed.
   const int nk = nfull + (ktail ? 1 : 0);
-
-  floatx4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  // Main loop over the full K tiles: LDS-DMA only (no ordinary VGPR loads in the loop, so hipcc
-  // does not insert a vmcnt(0) ahead of the ds_reads); the next tile lands while this one computes.
   int cur = 0;
-  if (nfull > 0) {
-    glds_tile<AK>(smem, g.A, g.lda, m0, g.M, kbeg, wid, lane);
-    glds_tile<BK_>(smem + 16384, g.B, g.ldb, n0, g.N, kbeg, wid, lane);
+  {
+    const int kv = min(BK, kend - kbeg);
+    glds_tile<AK, TM, G::NW>(smem, tile_ptr<AK>(g.A, g.lda, m0, kbeg), g.lda, m0, g.M, kv, wid, lane);
+    glds_tile<BK_, TN, G::NW>(smem + G::A_BYTES, tile_ptr<BK_>(g.B, g.ldb, n0, kbeg), g.ldb, n0, g.N, kv, wid, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-  }
-  for (int kt = 0; kt < nfull; ++kt) {
-    if (kt + 1 < nfull) {
-      char* nb = smem + (cur ^ 1) * 32768;
-      const int kn = kbeg + (kt + 1) * BK;
-      glds_tile<AK>(nb, g.A, g.lda, m0, g.M, kn, wid, lane);
-      glds_tile<BK_>(nb + 16384, g.B, g.ldb, n0, g.N, kn, wid, lane);
+    if (kv < BK) {
+      zero_k_tail<AK, TM, G::T>(smem, kv, tid);
+      zero_k_tail<BK_, TN, G::T>(smem + G::A_BYTES, kv, tid);
+      __syncthreads();
     }
-    mma_tile<AK, BK_>(smem + cur * 32768, acc, wm, wn, lane);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int kn = kbeg + (kt + 1) * BK;
+    const int kv = min(BK, kend - kn);  // valid k rows of the next tile (<= 0: no next tile)
+    char* nb = smem + (cur ^ 1) * G::STAGE;
+    if (kv > 0) {
+      glds_tile<AK, TM, G::NW>(nb, tile_ptr<AK>(g.A, g.lda, m0, kn), g.lda, m0, g.M, kv, wid, lane);
+      glds_tile<BK_, TN, G::NW>(nb + G::A_BYTES, tile_ptr<BK_>(g.B, g.ldb, n0, kn), g.ldb, n0, g.N, kv, wid, lane);
+    }
+    mma_tile<AK, BK_, G>(smem + cur * G::STAGE, acc, wm, wn, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA for tile kt+1 has landed
     __syncthreads();                                   // ... and every other wave's too
+    if (kv > 0 && kv < BK) {
+      zero_k_tail<AK, TM, G::T>(nb, kv, tid);
+      zero_k_tail<BK_, TN, G::T>(nb + G::A_BYTES, kv, tid);
+      __syncthreads();
+    }
     cur ^= 1;
   }
-  // Partial last K tile (wgrad over a token count that is not a multiple of 64): zero-filled
-  // register loads into the free buffer.
-  if (ktail) {
-    uint4 ra[4], rb[4];
-    const int kn = kbeg + nfull * BK;
-    load_tile<AK>(ra, g.A, g.lda, m0, g.M, kn, kend, tid);
-    load_tile<BK_>(rb, g.B, g.ldb, n0, g.N, kn, kend, tid);
-    store_tile<AK>(smem + cur * 32768, ra, tid);
-    store_tile<BK_>(smem + cur * 32768 + 16384, rb, tid);
-    __syncthreads();
-    mma_tile<AK, BK_>(smem + cur * 32768, acc, wm, wn, lane);
-    __syncthreads();
-  }
 
-  // ---- epilogue: stage the wave's 64x64 f32 tile in LDS, then vectorised row pass ----
+  // ---- epilogue: per 64-row slab of the wave tile, stage f32 in LDS, then a vectorised row pass
   float* st = reinterpret_cast<float*>(smem) + wid * 64 * EPI_LD;
+  const int colw = (lane & 15) * 4;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int h = 0; h < G::MI / 4; ++h) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        st[(i * 16 + (lane >> 4) * 4 + r) * EPI_LD + j * 16 + (lane & 15)] = acc[i][j][r];
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own-wave LDS writes retired
-  __builtin_amdgcn_wave_barrier();
-
-  const int col = n0 + wn * 64 + (lane & 15) * 4;
-  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
-  const bool col_ok = col < g.N;
-  if (g.bias && col_ok) {
-    const uint2 bv = *reinterpret_cast<const uint2*>(g.bias + col);
-    bias4[0] = __uint_as_float(bv.x << 16); bias4[1] = __uint_as_float(bv.x & 0xffff0000u);
-    bias4[2] = __uint_as_float(bv.y << 16); bias4[3] = __uint_as_float(bv.y & 0xffff0000u);
-  }
-  for (int pass = 0; pass < 16; ++pass) {
-    const int lr = pass * 4 + (lane >> 4);
-    const int row = m0 + wm * 64 + lr;
-    if (row >= g.M || !col_ok) continue;
-    floatx4 v = *reinterpret_cast<const floatx4*>(st + lr * EPI_LD + (lane & 15) * 4);
-    float o[4] = {v[0] + bias4[0], v[1] + bias4[1], v[2] + bias4[2], v[3] + bias4[3]};
-    if (g.act == ACT_SILU) {
+      for (int j = 0; j < G::NI; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = o[e] / (1.f + __expf(-o[e]));
-    }
-    if (g.out_mode == OUT_BF16) {
-      bf16_t* C = reinterpret_cast<bf16_t*>(g.C);
-      if (g.resid) {
-        const uint2 rv = *reinterpret_cast<const uint2*>(g.resid + (long)row * g.ldr + col);
-        // reference semantics: residual + bf16(linear output), rounded again to bf16
-        o[0] = bf2f(f2bf(o[0])) + __uint_as_float(rv.x << 16);
-        o[1] = bf2f(f2bf(o[1])) + __uint_as_float(rv.x & 0xffff0000u);
-        o[2] = bf2f(f2bf(o[2])) + __uint_as_float(rv.y << 16);
-        o[3] = bf2f(f2bf(o[3])) + __uint_as_float(rv.y & 0xffff0000u);
+        for (int r = 0; r < 4; ++r)
+          st[(i * 16 + (lane >> 4) * 4 + r) * EPI_LD + j * 16 + (lane & 15)] = acc[4 * h + i][j][r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own-wave LDS writes retired
+    __builtin_amdgcn_wave_barrier();
+    for (int cb = 0; cb < G::WC; cb += 64) {
+      const int col = n0 + wn * G::WC + cb + colw;
+      const bool col_ok = col < g.N;
+      float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (g.bias && col_ok) {
+        const uint2 bv = *reinterpret_cast<const uint2*>(g.bias + col);
+        bias4[0] = __uint_as_float(bv.x << 16); bias4[1] = __uint_as_float(bv.x & 0xffff0000u);
+        bias4[2] = __uint_as_float(bv.y << 16); bias4[3] = __uint_as_float(bv.y & 0xffff0000u);
       }
-      uint2 w;
-      w.x = pack_bf16x2(o[0], o[1]);
-      w.y = pack_bf16x2(o[2], o[3]);
-      *reinterpret_cast<uint2*>(C + (long)row * g.ldc + col) = w;
-    } else {
-      float* C = reinterpret_cast<float*>(g.C) + (long)blockIdx.y * g.split_stride;
-      floatx4* dst = reinterpret_cast<floatx4*>(C + (long)row * g.ldc + col);
-      floatx4 ov = {o[0], o[1], o[2], o[3]};
-      if (g.out_mode == OUT_F32_ACC) ov += *dst;
-      *dst = ov;
+      for (int pass = 0; pass < 16; ++pass) {
+        const int lr = pass * 4 + (lane >> 4);
+        const int row = m0 + wm * G::WR + h * 64 + lr;
+        if (row >= g.M || !col_ok) continue;
+        floatx4 v = *reinterpret_cast<const floatx4*>(st + lr * EPI_LD + cb + colw);
+        float o[4] = {v[0] + bias4[0], v[1] + bias4[1], v[2] + bias4[2], v[3] + bias4[3]};
+        if (g.act == ACT_SILU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = o[e] / (1.f + __expf(-o[e]));
+        }
+        if (g.out_mode == OUT_BF16) {
+          bf16_t* C = reinterpret_cast<bf16_t*>(g.C);
+          if (g.resid) {
+            const uint2 rv = *reinterpret_cast<const uint2*>(g.resid + (long)row * g.ldr + col);
+            // reference semantics: residual + bf16(linear output), rounded again to bf16
+            o[0] = bf2f(f2bf(o[0])) + __uint_as_float(rv.x << 16);
+            o[1] = bf2f(f2bf(o[1])) + __uint_as_float(rv.x & 0xffff0000u);
+            o[2] = bf2f(f2bf(o[2])) + __uint_as_float(rv.y << 16);
+            o[3] = bf2f(f2bf(o[3])) + __uint_as_float(rv.y & 0xffff0000u);
+          }
+          uint2 w;
+          w.x = pack_bf16x2(o[0], o[1]);
+          w.y = pack_bf16x2(o[2], o[3]);
+          *reinterpret_cast<uint2*>(C + (long)row * g.ldc + col) = w;
+        } else {
+          float* C = reinterpret_cast<float*>(g.C) + (long)blockIdx.y * g.split_stride;
+          floatx4* dst = reinterpret_cast<floatx4*>(C + (long)row * g.ldc + col);
+          floatx4 ov = {o[0], o[1], o[2], o[3]};
+          if (g.out_mode == OUT_F32_ACC) ov += *dst;
+          *dst = ov;
+        }
+      }
     }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
-template <bool AK, bool BK_>
+template <bool AK, bool BK_, int TM, int TN, int WGM, int WGN>
 int launch(const GemmArgs& g, int splits, hipStream_t s) {
-  const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  using G = Geo<TM, TN, WGM, WGN>;
+  const int tiles = ((g.M + TM - 1) / TM) * ((g.N + TN - 1) / TN);
   dim3 grid(tiles, splits);
-  hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK_>), grid, dim3(256), LDS_BYTES, s, g);
+  hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK_, TM, TN, WGM, WGN>), grid, dim3(G::T), G::LDS, s, g);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
+}
+
+template <bool AK, bool BK_>
+int launch_geo(const GemmArgs& g, int splits, int geo, hipStream_t s) {
+  if (geo == 256) return launch<AK, BK_, 256, 256, 2, 4>(g, splits, s);
+  return launch<AK, BK_, 128, 128, 2, 2>(g, splits, s);
 }
 
 __global__ void splitk_reduce_kernel(const float* __restrict__ part, long n, int splits, long stride,
@@ -307,6 +331,15 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ part, long n, int
     if (out_mode == OUT_F32_ACC) s += *d;
     *d = s;
   }
+}
+
+// Geometry choice: the 256x256 tile when it still gives >= ~1.5 waves of blocks on 256 CUs,
+// otherwise 128x128 (2 blocks/CU, 4x the tiles).
+int g_geo_override = 0;  // 0 = heuristic; 128 / 256 force a geometry (benchmarking)
+int pick_geo(int M, int N, int splits) {
+  if (g_geo_override == 128 || g_geo_override == 256) return g_geo_override;
+  const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256) * splits;
+  return t256 >= 384 ? 256 : 128;
 }
 
 }  // namespace
@@ -351,11 +384,12 @@ extern "C" int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* 
     g.split_stride = 0;
     g.out_mode = out_mode;
   }
+  const int geo = pick_geo(M, N, splits);
   int rc;
-  if (a_kmajor && b_kmajor) rc = launch<true, true>(g, splits, s);
-  else if (a_kmajor && !b_kmajor) rc = launch<true, false>(g, splits, s);
-  else if (!a_kmajor && b_kmajor) rc = launch<false, true>(g, splits, s);
-  else rc = launch<false, false>(g, splits, s);
+  if (a_kmajor && b_kmajor) rc = launch_geo<true, true>(g, splits, geo, s);
+  else if (a_kmajor && !b_kmajor) rc = launch_geo<true, false>(g, splits, geo, s);
+  else if (!a_kmajor && b_kmajor) rc = launch_geo<false, true>(g, splits, geo, s);
+  else rc = launch_geo<false, false>(g, splits, geo, s);
   if (rc != VPT_OK || splits == 1) return rc;
   const long n = (long)M * N;
   const int threads = 256;
@@ -363,6 +397,12 @@ extern "C" int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* 
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(threads), 0, s,
                      (const float*)workspace, n, splits, (long)M * N, C, final_mode);
   VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_gemm_set_geometry(int geo) {
+  VPT_CHECK_ARG(geo == 0 || geo == 128 || geo == 256, "vpt_gemm_set_geometry: 0, 128 or 256");
+  g_geo_override = geo;
   return VPT_OK;
 }
 

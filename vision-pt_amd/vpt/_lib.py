@@ -23,6 +23,7 @@ LL = C.c_longlong
 SIGNATURES: dict[str, list] = {
     "vpt_gemm_bf16": [P, L, I, P, L, I, P, L, I, I, I, P, P, L, I, I, I, P, P],
     "vpt_gemm_workspace_bytes": [I, I, I, I],
+    "vpt_gemm_set_geometry": [I],
     "vpt_attn_fwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, P, L, I, I, I, I, F, P],
     "vpt_attn_bwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, P, L, L, P, L,
                      P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, F, P],
