@@ -41,7 +41,9 @@ int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* B, long ldb
                   long ldc, int M, int N, int K, const void* bias, const void* resid, long ldr, int out_mode,
                   int act, int splits, void* workspace, void* stream);
 long vpt_gemm_workspace_bytes(int M, int N, int K, int splits);
-/* Tile geometry: 0 = automatic (default), 128 or 256 forces the 128x128 / 256x256 kernel (benchmarking). */
+/* Tile geometry: 0 = automatic (default); 128 = 128x128 2-stage, 256 = 256x256 ping-pong ring,
+ * 2561 = ring unstaggered, 2562 = 256x256 2-stage (benchmarking); 2563/2564 = timing-only ablations
+ * of the ring (forward direction only; results are wrong). */
 int vpt_gemm_set_geometry(int geo);
 
 /* ---- flash attention, head_dim 64 ---------------------------------------------------------
@@ -59,6 +61,9 @@ int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr, const void* k, 
                  long l_sh, const float* kbias, long kb_sb, void* dq, long dq_sb, long dq_sh, long dq_sr,
                  void* dk, long dk_sb, long dk_sh, long dk_sr, void* dv, long dv_sb, long dv_sh, long dv_sr,
                  int B, int H, int n, int n_dense, float scale, void* stream);
+/* Forward lazy-rescale threshold in log2 units (default 8; 0 = rescale whenever the row max grows).
+ * Test hook for the online-softmax rescale branch; process-wide. */
+int vpt_attn_set_rescale_threshold(float tau);
 
 /* ---- RMSNorm over the hidden dim -----------------------------------------------------------
  * Replaces FP32RMSNorm.forward src/modules/norm.py:20-27 (norm1/norm2/norm_final,

@@ -82,11 +82,13 @@ def test_gemm_wgrad(ops, M, N, K, splits):
     assert rel(out, 2 * ref) < 1e-5
 
 
-@pytest.mark.parametrize("geo", [128, 256])
-@pytest.mark.parametrize("M,N,K", [(700, 264, 200), (300, 512, 136), (2100, 768, 768)])
+@pytest.mark.parametrize("geo", [128, 256, 2561, 2562, 2565])
+@pytest.mark.parametrize("M,N,K", [(700, 264, 200), (300, 512, 136), (2100, 768, 768), (520, 264, 40),
+                                   (512, 512, 32), (776, 1032, 96)])
 def test_gemm_geometries_all_directions(ops, geo, M, N, K):
-    """Both tile geometries, all three GEMM directions, ragged M/N and partial K tiles
-    (K % 64 != 0 exercises the clamped-DMA + LDS zeroing path for k-major and mn-major tiles)."""
+    """Every tile geometry (128 = T128, 256 = the BK=32 ping-pong ring, 2561 = the ring unstaggered, 2562 = 2-stage T256), all three GEMM
+    directions, ragged M/N, partial K tiles (K % 32 != 0 exercises the clamped-DMA + LDS zeroing path
+    for k-major and mn-major tiles) and ring depths 1-3 (K = 32, 96)."""
     ops.lib.vpt_gemm_set_geometry(geo)
     try:
         x = rnd(M, K, seed=80)
@@ -229,6 +231,41 @@ def test_attention_fwd_bwd(ops, n, n_dense, masked):
     assert rel(unh(dq), qf.grad) < 2e-2
     assert rel(unh(dk), kf.grad) < 2e-2
     assert rel(unh(dv), vf.grad) < 2e-2
+
+
+@pytest.mark.parametrize("tau", [8.0, 0.0, 64.0])
+def test_attention_fwd_rescale_branch(ops, tau):
+    """Forces the online-softmax rescale branch at later tiles (guide §5.4 rule 26): query 5 meets a
+    score spike at key 300 (tile 4, far past the threshold) and a smaller one at key 130 (tile 2,
+    below an 8-unit threshold); full-tensor fp64 reference, and the threshold sweep 0 / 8 / 64 must
+    agree to rounding."""
+    B, H, n = 1, 2, 400
+    rows, D = 512, 2 * 64
+    qkv = rnd(B * rows, 3 * D, seed=44)
+    u = torch.randn(64, device=DEV)
+    u = u / u.norm()
+    qkv[5, 0:64] = (4.0 * u).bfloat16()
+    qkv[300, D:D + 64] = (12.0 * u).bfloat16()   # score ~48 -> ~69 log2 units above the rest
+    qkv[130, D:D + 64] = (1.2 * u).bfloat16()    # ~+4.8 -> 7 log2 units
+    o = torch.zeros(B * rows, D, dtype=torch.bfloat16, device=DEV)
+    lse = torch.zeros(B, H, rows, device=DEV)
+    q4, k4, v4 = (ops._t4(qkv, B, rows, H, c) for c in (0, D, 2 * D))
+    ops.lib.vpt_attn_set_rescale_threshold(tau)
+    try:
+        ops.attn_fwd(q4, k4, v4, ops._t4(o, B, rows, H, 0), lse, None, B, H, rows, n, n)
+    finally:
+        ops.lib.vpt_attn_set_rescale_threshold(8.0)
+
+    def heads(c0):
+        return qkv[:, c0:c0 + D].double().view(B, rows, H, 64)[:, :n].permute(0, 2, 1, 3)
+
+    s = torch.einsum("bhqd,bhkd->bhqk", heads(0), heads(D)) * 0.125
+    ref = torch.einsum("bhqk,bhkd->bhqd", torch.softmax(s, -1), heads(2 * D))
+    got = o.view(B, rows, H, 64)[:, :n].permute(0, 2, 1, 3).double()
+    assert rel(got, ref) < 1e-2
+    assert (got[0, :, 5] - ref[0, :, 5]).abs().max() < 2e-2
+    ref_lse = torch.logsumexp(s, -1) / math.log(2.0)
+    assert (lse[:, :, :n].double() - ref_lse).abs().max() < 1e-3
 
 
 # ------------------------------------------------------------------------------------ misc

@@ -51,9 +51,9 @@ def main():
             fl = 2.0 * M * N * K
             sp = ops.wgrad_splits(N, K, M)
             t = {}
-            for geo in (0, 128, 256):
+            for geo in (0, 128, 256, 2561, 2562):
                 ops.lib.vpt_gemm_set_geometry(geo)
-                sfx = {0: "", 128: "@128", 256: "@256"}[geo]
+                sfx = {0: "", 128: "@128", 256: "@256pp", 2561: "@256ring", 2562: "@256_2stage"}[geo]
                 t["fwd" + sfx] = timeit(lambda: ops.linear(x, w, out=y))
                 t["dgrad" + sfx] = timeit(lambda: ops.linear_dgrad(dy, w, out=dx))
                 t["wgrad" + sfx] = timeit(lambda: ops.linear_wgrad(dy, x, dw, splits=sp, workspace=ws))

@@ -31,9 +31,22 @@ struct AttnArgs {
   const float* kbias; long kb_sb;                                         // [B][*] f32
   int n, n_dense;
   float scale, scale_log2;
+  float tau;  // forward lazy-rescale threshold
 };
 
 constexpr float kNegInf = -__builtin_huge_valf();
+float g_tau = 8.f;  // forward lazy-rescale threshold, log2 units (vpt_attn_set_rescale_threshold)
+
+// Reductions over the lane pair (l, l^32) with v_permlane32_swap (VALU, no LDS round trip): the two
+// results together hold both halves' values in every lane, whichever half the swap moves.
+__device__ __forceinline__ float pair_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float pair_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 
 __device__ __forceinline__ int sigma(int r) { return ((r >> 1) & 7) ^ ((r & 2) << 1); }
 __device__ __forceinline__ int tile_off(int row, int chunk) { return row * 128 + ((chunk ^ sigma(row)) << 4); }
@@ -101,9 +114,10 @@ __device__ __forceinline__ float key_bias(const AttnArgs& g, int b, int key) {
   if (key < g.n_dense || !g.kbias) return 0.f;
   return g.kbias[(long)b * g.kb_sb + key];
 }
-// Writes a [64 d][32 rows] transposed accumulator pair (rows on the lane) as row-major bf16.
+// Writes a [64 d][32 rows] transposed accumulator pair (rows on the lane) as row-major bf16; `zero`
+// stores exact zeros instead (masked keys, whose accumulators may hold non-finite values).
 __device__ __forceinline__ void store_T(const OTensor4& t, long base_off, const floatx16 (&acc)[2], float mul,
-                                        int row, int n, int lane) {
+                                        int row, int n, int lane, bool zero) {
   if (row >= n) return;
   const int h = lane >> 5;
   bf16_t* dst = t.p + base_off + (long)row * t.sr;
@@ -115,6 +129,7 @@ __device__ __forceinline__ void store_T(const OTensor4& t, long base_off, const 
       uint2 w;
       w.x = pack_bf16x2(acc[db][4 * g4 + 0] * mul, acc[db][4 * g4 + 1] * mul);
       w.y = pack_bf16x2(acc[db][4 * g4 + 2] * mul, acc[db][4 * g4 + 3] * mul);
+      if (zero) w = make_uint2(0u, 0u);
       *reinterpret_cast<uint2*>(dst + d) = w;
     }
 }
@@ -136,7 +151,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs g) {
   floatx16 oacc[2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) { oacc[0][i] = 0.f; oacc[1][i] = 0.f; }
-  float m = kNegInf, lsum = 0.f;
+  float m_c = kNegInf, lsum = 0.f;  // running reference max (scaled log2 units), row sum
 
   const int nt = (g.n + 63) / 64;
   uint4 rk[2], rv[2];
@@ -165,38 +180,44 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs g) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) sacc[kb] = mfma32(frag_rows(lk, 32 * kb, s, lane), qf[s], sacc[kb]);
     }
-    const bool dense = kv0 + 64 <= g.n_dense;
+    // Raw-score max (the scale is positive, so max(s)*c = max(s*c)); key bias is 0 / -inf.
+    if (kv0 + 64 > g.n_dense) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const floatx4 bias = *reinterpret_cast<const floatx4*>(&lbias[cur][32 * kb + 8 * g4 + 4 * h]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sacc[kb][4 * g4 + e] += bias[e];
+        }
+    }
     float mx = kNegInf;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        floatx4 bias = {0.f, 0.f, 0.f, 0.f};
-        if (!dense) bias = *reinterpret_cast<const floatx4*>(&lbias[cur][32 * kb + 8 * g4 + 4 * h]);
+      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[kb][i]);
+    const float mx_c = pair_max(mx) * g.scale_log2;
+    // Lazy rescale: the reference point m_c only moves when this tile's max exceeds it by more
+    // than tau (p <= 2^tau otherwise); wave-uniform branch, taken on the first tile and rarely after.
+    const bool up = mx_c > m_c + g.tau;
+    if (__builtin_amdgcn_ballot_w64(up)) {
+      const float m_new = up ? mx_c : m_c;
+      const float alpha = up ? __builtin_amdgcn_exp2f(m_c - m_new) : 1.f;
+      lsum *= alpha;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float x = sacc[kb][4 * g4 + e] * g.scale_log2 + bias[e];
-          sacc[kb][4 * g4 + e] = x;
-          mx = fmaxf(mx, x);
-        }
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m, mx);
-    const float m_use = m_new == kNegInf ? 0.f : m_new;
-    const float alpha = __builtin_amdgcn_exp2f(m - m_use);
+      for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
+      m_c = m_new;
+    }
     float ps = 0.f;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(sacc[kb][i] - m_use);
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kb][i], g.scale_log2, -m_c));
         sacc[kb][i] = p;
         ps += p;
       }
-    lsum = lsum * alpha + ps;
-    m = m_new;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
+    lsum += ps;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -213,11 +234,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs g) {
     __syncthreads();
     cur ^= 1;
   }
-  const float l = lsum + __shfl_xor(lsum, 32, 64);
+  const float l = pair_sum(lsum);
   const float inv = 1.f / l;
   const int qrow = q0 + (lane & 31);
-  store_T(g.o, (long)b * g.o.sb + hd * g.o.sh, oacc, inv, qrow, g.n, lane);
-  if (lane < 32 && qrow < g.n) g.lse[b * g.l_sb + hd * g.l_sh + qrow] = m + __log2f(l);
+  store_T(g.o, (long)b * g.o.sb + hd * g.o.sh, oacc, inv, qrow, g.n, lane, false);
+  if (lane < 32 && qrow < g.n) g.lse[b * g.l_sb + hd * g.l_sh + qrow] = m_c + __log2f(l);
 }
 
 // ------------------------------------------------------------------ backward preprocess
@@ -259,7 +280,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
   bf16x8 kf[4], vf[4];
   load_row_frags(kf, g.k.p + b * g.k.sb + hd * g.k.sh, g.k.sr, key, g.n, lane);
   load_row_frags(vf, g.v.p + b * g.v.sb + hd * g.v.sh, g.v.sr, key, g.n, lane);
-  const float kbias = key_bias(g, b, key);
+  const bool kmasked = key_bias(g, b, key) == kNegInf;
 
   floatx16 dvT[2], dkT[2];
 #pragma unroll
@@ -311,7 +332,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
         const floatx4 d4 = *reinterpret_cast<const floatx4*>(&lstat[cur][1][qi]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float p = __builtin_amdgcn_exp2f(s[4 * g4 + e] * g.scale_log2 + kbias - l4[e]);
+          // No key bias here: a masked key (bias -inf) only feeds its own lane's dK/dV columns, which
+          // are stored as exact zeros below, so one FMA + exp2 per score.
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[4 * g4 + e], g.scale_log2, -l4[e]));
           P[qb][4 * g4 + e] = p;
           dS[qb][4 * g4 + e] = p * (dp[4 * g4 + e] - d4[e]);
         }
@@ -337,8 +360,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
     __syncthreads();
     cur ^= 1;
   }
-  store_T(g.dv, (long)b * g.dv.sb + hd * g.dv.sh, dvT, 1.f, key, g.n, lane);
-  store_T(g.dk, (long)b * g.dk.sb + hd * g.dk.sh, dkT, g.scale, key, g.n, lane);
+  store_T(g.dv, (long)b * g.dv.sb + hd * g.dv.sh, dvT, 1.f, key, g.n, lane, kmasked);
+  store_T(g.dk, (long)b * g.dk.sb + hd * g.dk.sh, dkT, g.scale, key, g.n, lane, kmasked);
 }
 
 // ------------------------------------------------------------------ backward dQ
@@ -395,15 +418,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs g) {
         dp = mfma32(frag_rows(lv, 32 * kb, ks, lane), df[ks], dp);
       }
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        floatx4 bias = {0.f, 0.f, 0.f, 0.f};
-        if (!dense) bias = *reinterpret_cast<const floatx4*>(&lbias[cur][32 * kb + 8 * g4 + 4 * h]);
+      for (int i = 0; i < 16; ++i) s[i] = __builtin_fmaf(s[i], g.scale_log2, -lse);
+      if (!dense) {  // scalar branch: only the context / padding key tiles carry a bias
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float p = __builtin_amdgcn_exp2f(s[4 * g4 + e] * g.scale_log2 + bias[e] - lse);
-          dS[kb][4 * g4 + e] = p * (dp[4 * g4 + e] - del);
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const floatx4 bias = *reinterpret_cast<const floatx4*>(&lbias[cur][32 * kb + 8 * g4 + 4 * h]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) s[4 * g4 + e] += bias[e];
         }
       }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dS[kb][i] = __builtin_amdgcn_exp2f(s[i]) * (dp[i] - del);
     }
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
@@ -421,7 +446,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs g) {
     __syncthreads();
     cur ^= 1;
   }
-  store_T(g.dq, (long)b * g.dq.sb + hd * g.dq.sh, dqT, g.scale, qrow, g.n, lane);
+  store_T(g.dq, (long)b * g.dq.sb + hd * g.dq.sh, dqT, g.scale, qrow, g.n, lane, false);
 }
 
 int check_common(int B, int H, int n) {
@@ -451,6 +476,7 @@ extern "C" int vpt_attn_fwd(const void* q, long q_sb, long q_sh, long q_sr,
   g.kbias = kbias; g.kb_sb = kb_sb;
   g.n = n; g.n_dense = n_dense < n ? n_dense : n;
   g.scale = scale; g.scale_log2 = scale * 1.4426950408889634f;
+  g.tau = g_tau;
   dim3 grid((n + 127) / 128, H, B);
   hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, g);
   VPT_LAUNCH_CHECK();
@@ -493,5 +519,12 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
   VPT_LAUNCH_CHECK();
   hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, s, g);
   VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+// Test hook: the forward lazy-rescale threshold (log2 units; 0 = rescale whenever the max grows).
+extern "C" int vpt_attn_set_rescale_threshold(float tau) {
+  VPT_CHECK_ARG(tau >= 0.f && tau <= 64.f, "vpt_attn_set_rescale_threshold: tau in [0, 64]");
+  g_tau = tau;
   return VPT_OK;
 }

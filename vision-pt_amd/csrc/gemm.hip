@@ -177,6 +177,70 @@ __device__ __forceinline__ void mma_tile(const char* la, floatx4 (&acc)[G::MI][G
   }
 }
 
+// Epilogue: per 64-row slab of the wave tile, stage the f32 accumulators in the wave's own LDS region,
+// then a vectorised row pass applies bias / SiLU / residual and stores 8-16 B per lane.
+template <typename G>
+__device__ __forceinline__ void epilogue(const GemmArgs& g, floatx4 (&acc)[G::MI][G::NI], char* smem, int wid, int lane,
+                                         int m0, int n0, int wm, int wn) {
+  float* st = reinterpret_cast<float*>(smem) + wid * 64 * EPI_LD;
+  const int colw = (lane & 15) * 4;
+#pragma unroll
+  for (int h = 0; h < G::MI / 4; ++h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < G::NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          st[(i * 16 + (lane >> 4) * 4 + r) * EPI_LD + j * 16 + (lane & 15)] = acc[4 * h + i][j][r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own-wave LDS writes retired
+    __builtin_amdgcn_wave_barrier();
+    for (int cb = 0; cb < G::WC; cb += 64) {
+      const int col = n0 + wn * G::WC + cb + colw;
+      const bool col_ok = col < g.N;
+      float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (g.bias && col_ok) {
+        const uint2 bv = *reinterpret_cast<const uint2*>(g.bias + col);
+        bias4[0] = __uint_as_float(bv.x << 16); bias4[1] = __uint_as_float(bv.x & 0xffff0000u);
+        bias4[2] = __uint_as_float(bv.y << 16); bias4[3] = __uint_as_float(bv.y & 0xffff0000u);
+      }
+      for (int pass = 0; pass < 16; ++pass) {
+        const int lr = pass * 4 + (lane >> 4);
+        const int row = m0 + wm * G::WR + h * 64 + lr;
+        if (row >= g.M || !col_ok) continue;
+        floatx4 v = *reinterpret_cast<const floatx4*>(st + lr * EPI_LD + cb + colw);
+        float o[4] = {v[0] + bias4[0], v[1] + bias4[1], v[2] + bias4[2], v[3] + bias4[3]};
+        if (g.act == ACT_SILU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = o[e] / (1.f + __expf(-o[e]));
+        }
+        if (g.out_mode == OUT_BF16) {
+          bf16_t* C = reinterpret_cast<bf16_t*>(g.C);
+          if (g.resid) {
+            const uint2 rv = *reinterpret_cast<const uint2*>(g.resid + (long)row * g.ldr + col);
+            // reference semantics: residual + bf16(linear output), rounded again to bf16
+            o[0] = bf2f(f2bf(o[0])) + __uint_as_float(rv.x << 16);
+            o[1] = bf2f(f2bf(o[1])) + __uint_as_float(rv.x & 0xffff0000u);
+            o[2] = bf2f(f2bf(o[2])) + __uint_as_float(rv.y << 16);
+            o[3] = bf2f(f2bf(o[3])) + __uint_as_float(rv.y & 0xffff0000u);
+          }
+          uint2 w;
+          w.x = pack_bf16x2(o[0], o[1]);
+          w.y = pack_bf16x2(o[2], o[3]);
+          *reinterpret_cast<uint2*>(C + (long)row * g.ldc + col) = w;
+        } else {
+          float* C = reinterpret_cast<float*>(g.C) + (long)blockIdx.y * g.split_stride;
+          floatx4* dst = reinterpret_cast<floatx4*>(C + (long)row * g.ldc + col);
+          floatx4 ov = {o[0], o[1], o[2], o[3]};
+          if (g.out_mode == OUT_F32_ACC) ov += *dst;
+          *dst = ov;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 template <bool AK, bool BK_, int TM, int TN, int WGM, int WGN>
 __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_bf16_kernel(GemmArgs g) {
   using G = Geo<TM, TN, WGM, WGN>;
@@ -239,64 +303,214 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_bf16_kernel(GemmArgs g
     cur ^= 1;
   }
 
-  // ---- epilogue: per 64-row slab of the wave tile, stage f32 in LDS, then a vectorised row pass
-  float* st = reinterpret_cast<float*>(smem) + wid * 64 * EPI_LD;
-  const int colw = (lane & 15) * 4;
+  epilogue<G>(g, acc, smem, wid, lane, m0, n0, wm, wn);
+}
+
+// ---- T256 ring kernel: 256x256 block tile, 8 waves (2x4) of 128x64, BK = 32 stages ------------
+// A 4-deep LDS ring of 32-deep K tiles (32 KB each: A 256x32 + B 256x32) keeps up to three tiles of
+// LDS-DMA in flight; waits are counted (`s_waitcnt vmcnt(8)`: the two younger tiles' 4 + 4 pieces
+// per wave stay outstanding), never vmcnt(0) in the steady state (guide §5 "Pipelining across
+// barriers", T3/T4). Each K step is two phases separated by raw s_barriers:
+//   L_t: DMA tile t+3 into the stage of tile t-1; ds_read all A/B fragments of tile t into registers;
+//        wait for this wave's pieces of tile t+1; barrier Y_t
+//   C_t: 32 MFMAs from registers (s_setprio 1); barrier X_t+1
+// PP (ping-pong): wave group 1 (waves 4-7, one per SIMD) executes one extra barrier up front and
+// group 0 one at the end, so on every SIMD one wave is in C while the other is in L. The data wait for
+// tile t+1 sits before Y_t (one phase earlier than an unstaggered loop needs), so that all 8 waves'
+// pieces of a tile have landed before the earlier group's barrier that precedes its reads; a stage is
+// re-filled in L_t only, after both groups' reads of it (L_t-1, each closed by lgkmcnt(0) + barrier).
+// k-major stages are [row][32k] (64-B rows, chunk ^= 2*bit2(row): conflict-free for ds_read_b128's
+// lane groups); mn-major stages are [32k][R] as in T128. A partial last K tile is DMA'd from clamped
+// (finite, in-bounds) addresses and its k >= K lanes of the A fragments are zeroed in registers.
+constexpr int RBK = 32;
+constexpr int RSTAGES = 4;
+
+__device__ __forceinline__ int kmaj32_off(int row, int chunk) {  // [R][32] bf16, 64-B rows
+  return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4);
+}
+
+// One 32-deep operand tile of R rows = R*64 B = R/16 pieces of 1 KB; each of the 8 waves issues R/128
+// = 2 (q = 2*wid + i). tile_voff gives lane's byte offset for piece i from the tile's (row0, k0)
+// element: loop-invariant for full tiles, so it is computed once; only a partial last tile (kvalid <
+// 32) recomputes it with k clamped. Rows past the matrix edge are clamped to a valid row.
+template <bool KMAJ, int R>
+__device__ __forceinline__ uint32_t tile_voff(long ld, int row0, int nrows, int kvalid, int wid, int lane, int i) {
+  const int q = wid * (R / 128) + i;
+  if (KMAJ) {
+    const int row = q * 16 + (lane >> 2);
+    int c = (lane & 3) ^ (((row >> 2) & 1) << 1);
+    c = c * 8 < kvalid ? c : 0;  // k past the end: any in-bounds chunk (masked in registers)
+    const int r = row0 + row < nrows ? row : nrows - 1 - row0;
+    return (uint32_t)(((long)r * ld + c * 8) * 2);
+  } else {
+    constexpr int CH = R / 8;  // 16-B chunks per k-row
+    const int krow = q * (64 / CH) + lane / CH;
+    const int c = (lane % CH) ^ (mnmaj_f(krow) << 1);
+    const int m = row0 + c * 8 < nrows ? c * 8 : nrows - 8 - row0;
+    const int kr = krow < kvalid ? krow : kvalid - 1;
+    return (uint32_t)(((long)kr * ld + m) * 2);
+  }
+}
+
+// The 4 pieces of one K tile (A: 2, B: 2) in one asm statement: one hazard pad for the SGPR operands
+// (which may come from v_readfirstlane), M0 set per piece from precomputed SGPRs, restored at the end.
+__device__ __forceinline__ void glds_step(const void* abase, const void* bbase, uint32_t va0, uint32_t va1,
+                                          uint32_t vb0, uint32_t vb1, uint32_t la0, uint32_t la1, uint32_t lb0,
+                                          uint32_t lb1) {
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %7\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %5\n\t"
+      "s_mov_b32 m0, %8\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %5\n\t"
+      "s_mov_b32 m0, %9\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %3, %6\n\t"
+      "s_mov_b32 m0, %10\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %4, %6\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(va0), "v"(va1), "v"(vb0), "v"(vb1), "s"(abase), "s"(bbase), "s"(la0), "s"(la1), "s"(lb0), "s"(lb1)
+      : "memory");
+}
+
+__device__ __forceinline__ const void* uniform_ptr(const void* p) {
+  const unsigned long long v = (unsigned long long)p;
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (const void*)(((unsigned long long)hi << 32) | lo);
+}
+
+template <bool KMAJ, int R>
+__device__ __forceinline__ bf16x8 read_frag32(const char* lds, int row_base, int lane) {
+  if (KMAJ) {
+    const int row = row_base + (lane & 15);
+    return as_frag(*reinterpret_cast<const uint4*>(lds + kmaj32_off(row, lane >> 4)));
+  } else {
+    return read_frag<false, R>(lds, row_base, 0, lane);
+  }
+}
+
+// Zero the elements k = kbase + 0..7 of a fragment that lie at or past klast.
+__device__ __forceinline__ unsigned keep2(int k, int klast) {
+  return (k < klast ? 0x0000ffffu : 0u) | (k + 1 < klast ? 0xffff0000u : 0u);
+}
+__device__ __forceinline__ bf16x8 mask_k(bf16x8 f, int kbase, int klast) {
+  uint4 v = __builtin_bit_cast(uint4, f);
+  v.x &= keep2(kbase, klast);
+  v.y &= keep2(kbase + 2, klast);
+  v.z &= keep2(kbase + 4, klast);
+  v.w &= keep2(kbase + 6, klast);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ void wait_younger(int younger) {  // 4 pieces per tile per wave
+  if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void bare_barrier() {
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+using GR = Geo<256, 256, 2, 4>;
+
+// ABL (timing-only ablations, wrong results): 1 = no LDS-DMA inside the loop, 2 = no vmcnt waits.
+// DMAC: issue tile t+3's LDS-DMA at the start of the MFMA phase C_t instead of in L_t. It overwrites
+// the stage of tile t-1, which every wave consumed by MFMAs before its previous barrier, so the
+// barriers need no lgkmcnt(0) and L_t shrinks to the ds_reads; tile t+1 is then waited for with only
+// tile t+2 younger (vmcnt(4)).
+template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false>
+__global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g) {
+  using G = GR;
+  constexpr int A32 = 256 * RBK * 2, STAGE32 = 2 * A32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / 4, wn = wid % 4;
+
+  const int tiles_n = (g.N + 255) / 256;
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tm = wgid / tiles_n, tn = wgid % tiles_n;
+  const int m0 = tm * 256, n0 = tn * 256;
+
+  const int kbeg = blockIdx.y * g.k_split;
+  const int kend = min(g.K, kbeg + g.k_split);
+  const int nk = (kend - kbeg + RBK - 1) / RBK;
+  const int klast = kend - kbeg - (nk - 1) * RBK;  // valid k of the last tile (1..32)
+
+  floatx4 acc[G::MI][G::NI];
 #pragma unroll
-  for (int h = 0; h < G::MI / 4; ++h) {
+  for (int i = 0; i < G::MI; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < G::NI; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // Loop-invariant per-lane piece offsets (full tiles) and LDS piece addresses (stage 0).
+  const uint32_t va0 = tile_voff<AK, 256>(g.lda, m0, g.M, RBK, wid, lane, 0);
+  const uint32_t va1 = tile_voff<AK, 256>(g.lda, m0, g.M, RBK, wid, lane, 1);
+  const uint32_t vb0 = tile_voff<BK_, 256>(g.ldb, n0, g.N, RBK, wid, lane, 0);
+  const uint32_t vb1 = tile_voff<BK_, 256>(g.ldb, n0, g.N, RBK, wid, lane, 1);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(VPT_LDS char*)smem + wid * 2048;
+  auto issue = [&](int t) {  // 4 pieces per wave: 2 of A, 2 of B
+    const uint32_t la = __builtin_amdgcn_readfirstlane(lds0 + (t & (RSTAGES - 1)) * STAGE32);
+    const int k0 = kbeg + t * RBK;
+    const int kv = min(RBK, kend - k0);
+    const void* ab = uniform_ptr(tile_ptr<AK>(g.A, g.lda, m0, k0));
+    const void* bb = uniform_ptr(tile_ptr<BK_>(g.B, g.ldb, n0, k0));
+    if (kv == RBK) {
+      glds_step(ab, bb, va0, va1, vb0, vb1, la, la + 1024, la + A32, la + A32 + 1024);
+    } else {
+      glds_step(ab, bb, tile_voff<AK, 256>(g.lda, m0, g.M, kv, wid, lane, 0),
+                tile_voff<AK, 256>(g.lda, m0, g.M, kv, wid, lane, 1), tile_voff<BK_, 256>(g.ldb, n0, g.N, kv, wid, lane, 0),
+                tile_voff<BK_, 256>(g.ldb, n0, g.N, kv, wid, lane, 1), la, la + 1024, la + A32, la + A32 + 1024);
+    }
+  };
+  issue(0);
+  if (nk > 1) issue(1);
+  if (nk > 2) issue(2);
+  wait_younger(min(2, nk - 1));  // tile 0
+  if (PP && wm == 1) raw_barrier();
+  raw_barrier();  // X_0
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* st = smem + (kt & (RSTAGES - 1)) * STAGE32;
+    if (!DMAC && ABL != 1 && kt + 3 < nk) issue(kt + 3);
+    bf16x8 bfr[G::NI], af[G::MI];
+#pragma unroll
+    for (int j = 0; j < G::NI; ++j) bfr[j] = read_frag32<BK_, 256>(st + A32, wn * G::WC + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < G::MI; ++i) af[i] = read_frag32<AK, 256>(st, wm * G::WR + i * 16, lane);
+    if (kt == nk - 1 && klast < RBK) {
+#pragma unroll
+      for (int i = 0; i < G::MI; ++i) af[i] = mask_k(af[i], 8 * (lane >> 4), klast);
+    }
+    if (ABL != 2) wait_younger(min(DMAC ? 1 : 2, nk - 2 - kt));  // tile kt+1 (if any) landed for this wave
+    if (DMAC) bare_barrier(); else raw_barrier();                // Y_kt
+    if (DMAC && ABL != 1 && kt + 3 < nk) issue(kt + 3);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < G::MI; ++i)
 #pragma unroll
       for (int j = 0; j < G::NI; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          st[(i * 16 + (lane >> 4) * 4 + r) * EPI_LD + j * 16 + (lane & 15)] = acc[4 * h + i][j][r];
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own-wave LDS writes retired
-    __builtin_amdgcn_wave_barrier();
-    for (int cb = 0; cb < G::WC; cb += 64) {
-      const int col = n0 + wn * G::WC + cb + colw;
-      const bool col_ok = col < g.N;
-      float bias4[4] = {0.f, 0.f, 0.f, 0.f};
-      if (g.bias && col_ok) {
-        const uint2 bv = *reinterpret_cast<const uint2*>(g.bias + col);
-        bias4[0] = __uint_as_float(bv.x << 16); bias4[1] = __uint_as_float(bv.x & 0xffff0000u);
-        bias4[2] = __uint_as_float(bv.y << 16); bias4[3] = __uint_as_float(bv.y & 0xffff0000u);
-      }
-      for (int pass = 0; pass < 16; ++pass) {
-        const int lr = pass * 4 + (lane >> 4);
-        const int row = m0 + wm * G::WR + h * 64 + lr;
-        if (row >= g.M || !col_ok) continue;
-        floatx4 v = *reinterpret_cast<const floatx4*>(st + lr * EPI_LD + cb + colw);
-        float o[4] = {v[0] + bias4[0], v[1] + bias4[1], v[2] + bias4[2], v[3] + bias4[3]};
-        if (g.act == ACT_SILU) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = o[e] / (1.f + __expf(-o[e]));
-        }
-        if (g.out_mode == OUT_BF16) {
-          bf16_t* C = reinterpret_cast<bf16_t*>(g.C);
-          if (g.resid) {
-            const uint2 rv = *reinterpret_cast<const uint2*>(g.resid + (long)row * g.ldr + col);
-            // reference semantics: residual + bf16(linear output), rounded again to bf16
-            o[0] = bf2f(f2bf(o[0])) + __uint_as_float(rv.x << 16);
-            o[1] = bf2f(f2bf(o[1])) + __uint_as_float(rv.x & 0xffff0000u);
-            o[2] = bf2f(f2bf(o[2])) + __uint_as_float(rv.y << 16);
-            o[3] = bf2f(f2bf(o[3])) + __uint_as_float(rv.y & 0xffff0000u);
-          }
-          uint2 w;
-          w.x = pack_bf16x2(o[0], o[1]);
-          w.y = pack_bf16x2(o[2], o[3]);
-          *reinterpret_cast<uint2*>(C + (long)row * g.ldc + col) = w;
-        } else {
-          float* C = reinterpret_cast<float*>(g.C) + (long)blockIdx.y * g.split_stride;
-          floatx4* dst = reinterpret_cast<floatx4*>(C + (long)row * g.ldc + col);
-          floatx4 ov = {o[0], o[1], o[2], o[3]};
-          if (g.out_mode == OUT_F32_ACC) ov += *dst;
-          *dst = ov;
-        }
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    if (DMAC) bare_barrier(); else raw_barrier();  // X_kt+1
   }
+  if (PP && wm == 0) raw_barrier();
+  __syncthreads();  // the ring is reused as epilogue staging
+  epilogue<G>(g, acc, smem, wid, lane, m0, n0, wm, wn);
 }
 
 template <bool AK, bool BK_, int TM, int TN, int WGM, int WGN>
@@ -309,9 +523,23 @@ int launch(const GemmArgs& g, int splits, hipStream_t s) {
   return VPT_OK;
 }
 
+template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false>
+int launch_ring(const GemmArgs& g, int splits, hipStream_t s) {
+  constexpr int LDS = RSTAGES * 2 * 256 * RBK * 2 > GR::EPI ? RSTAGES * 2 * 256 * RBK * 2 : GR::EPI;
+  const int tiles = ((g.M + 255) / 256) * ((g.N + 255) / 256);
+  hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC>), dim3(tiles, splits), dim3(512), LDS, s, g);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
 template <bool AK, bool BK_>
 int launch_geo(const GemmArgs& g, int splits, int geo, hipStream_t s) {
-  if (geo == 256) return launch<AK, BK_, 256, 256, 2, 4>(g, splits, s);
+  if (geo == 256) return launch_ring<AK, BK_, true>(g, splits, s);
+  if (geo == 2561) return launch_ring<AK, BK_, false>(g, splits, s);  // ring without the stagger (A/B only)
+  if (AK && BK_ && geo == 2563) return launch_ring<AK, BK_, true, 1>(g, splits, s);  // ablation, wrong results
+  if (AK && BK_ && geo == 2564) return launch_ring<AK, BK_, true, 2>(g, splits, s);  // ablation, wrong results
+  if (geo == 2565) return launch_ring<AK, BK_, true, 0, true>(g, splits, s);  // DMA in the MFMA phase
+  if (geo == 2562) return launch<AK, BK_, 256, 256, 2, 4>(g, splits, s);  // 2-stage BK=64 T256 (A/B only)
   return launch<AK, BK_, 128, 128, 2, 2>(g, splits, s);
 }
 
@@ -335,9 +563,9 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ part, long n, int
 
 // Geometry choice: the 256x256 tile when it still gives >= ~1.5 waves of blocks on 256 CUs,
 // otherwise 128x128 (2 blocks/CU, 4x the tiles).
-int g_geo_override = 0;  // 0 = heuristic; 128 / 256 force a geometry (benchmarking)
+int g_geo_override = 0;  // 0 = heuristic; 128 / 256 / 2561 / 2562 force a geometry (benchmarking)
 int pick_geo(int M, int N, int splits) {
-  if (g_geo_override == 128 || g_geo_override == 256) return g_geo_override;
+  if (g_geo_override) return g_geo_override;
   const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256) * splits;
   return t256 >= 384 ? 256 : 128;
 }
@@ -401,7 +629,8 @@ extern "C" int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* 
 }
 
 extern "C" int vpt_gemm_set_geometry(int geo) {
-  VPT_CHECK_ARG(geo == 0 || geo == 128 || geo == 256, "vpt_gemm_set_geometry: 0, 128 or 256");
+  VPT_CHECK_ARG(geo == 0 || geo == 128 || geo == 256 || (geo >= 2561 && geo <= 2565),
+                "vpt_gemm_set_geometry: 0, 128, 256 or 2561-2565");
   g_geo_override = geo;
   return VPT_OK;
 }
