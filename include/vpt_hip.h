@@ -64,6 +64,9 @@ int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr, const void* k, 
 /* Forward lazy-rescale threshold in log2 units (default 8; 0 = rescale whenever the row max grows).
  * Test hook for the online-softmax rescale branch; process-wide. */
 int vpt_attn_set_rescale_threshold(float tau);
+/* Benchmark hook: backward kernel variant (0 = production; 1 / 2 = timing-only ablations with wrong
+ * results: no in-loop tile staging / row reads in place of transposed reads). Process-wide. */
+int vpt_attn_set_variant(int v);
 
 /* ---- RMSNorm over the hidden dim -----------------------------------------------------------
  * Replaces FP32RMSNorm.forward src/modules/norm.py:20-27 (norm1/norm2/norm_final,

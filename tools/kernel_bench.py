@@ -81,6 +81,13 @@ def main():
         tb = timeit(lambda: ops.attn_bwd(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, None,
                                          ops._t4(dq, B, rows, H), ops._t4(dk, B, rows, H), ops._t4(dv, B, rows, H),
                                          B, H, rows, n, n))
+        for var in (1, 2):  # timing-only ablations of the backward (wrong results)
+            ops.lib.vpt_attn_set_variant(var)
+            tv = timeit(lambda: ops.attn_bwd(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, None,
+                                             ops._t4(dq, B, rows, H), ops._t4(dk, B, rows, H),
+                                             ops._t4(dv, B, rows, H), B, H, rows, n, n))
+            ops.lib.vpt_attn_set_variant(0)
+            res.setdefault(f"attn.bwd_alg_abl{var}", []).append(2 * fl / (tv * 1e-3) / 1e12)
         res.setdefault("attn.fwd", []).append(fl / (tf * 1e-3) / 1e12)
         res.setdefault("attn.bwd_alg", []).append(2 * fl / (tb * 1e-3) / 1e12)
         res.setdefault("attn.fwd_ms", []).append(tf)

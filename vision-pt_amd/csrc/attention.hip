@@ -35,6 +35,7 @@ struct AttnArgs {
 };
 
 constexpr float kNegInf = -__builtin_huge_valf();
+int g_variant = 0;  // backward kernel variant (vpt_attn_set_variant; 1, 2 = timing-only ablations)
 float g_tau = 8.f;  // forward lazy-rescale threshold, log2 units (vpt_attn_set_rescale_threshold)
 
 // Reductions over the lane pair (l, l^32) with v_permlane32_swap (VALU, no LDS round trip): the two
@@ -175,10 +176,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs g) {
     floatx16 sacc[2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
+      sacc[kb] = mfma32(frag_rows(lk, 32 * kb, 0, lane), qf[0], floatx16{});
 #pragma unroll
-      for (int i = 0; i < 16; ++i) sacc[kb][i] = 0.f;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) sacc[kb] = mfma32(frag_rows(lk, 32 * kb, s, lane), qf[s], sacc[kb]);
+      for (int s = 1; s < 4; ++s) sacc[kb] = mfma32(frag_rows(lk, 32 * kb, s, lane), qf[s], sacc[kb]);
     }
     // Raw-score max (the scale is positive, so max(s)*c = max(s*c)); key bias is 0 / -inf.
     if (kv0 + 64 > g.n_dense) {
@@ -265,6 +265,9 @@ __global__ void attn_bwd_pre_kernel(AttnArgs g, int H, long rows_total) {
 }
 
 // ------------------------------------------------------------------ backward dK, dV
+// ABL (timing-only ablations, wrong results): 1 = no next-tile staging (global -> regs -> LDS) in
+// the loop, 2 = transposed fragment reads replaced by row reads.
+template <int ABL = 0>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][8192];     // [buf][Q / dO]
   __shared__ __attribute__((aligned(16))) float lstat[2][2][64];     // [buf][lse / delta]
@@ -306,7 +309,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
 
   int cur = 0;
   for (int t = 0; t < nt; ++t) {
-    const bool more = t + 1 < nt;
+    const bool more = ABL != 1 && t + 1 < nt;
     if (more) {
       load_rows(rq, Q, g.q.sr, (t + 1) * 64, g.n, tid);
       load_rows(rd, dO, g.dO.sr, (t + 1) * 64, g.n, tid);
@@ -318,10 +321,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
       floatx16 s, dp;
+      s = mfma32(frag_rows(lq, 32 * qb, 0, lane), kf[0], floatx16{});  // zero C: inline constant
+      dp = mfma32(frag_rows(ld, 32 * qb, 0, lane), vf[0], floatx16{});
 #pragma unroll
-      for (int i = 0; i < 16; ++i) { s[i] = 0.f; dp[i] = 0.f; }
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
+      for (int ks = 1; ks < 4; ++ks) {
         s = mfma32(frag_rows(lq, 32 * qb, ks, lane), kf[ks], s);
         dp = mfma32(frag_rows(ld, 32 * qb, ks, lane), vf[ks], dp);
       }
@@ -348,8 +351,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
         const bf16x8 pd = pack_acc(dS[qb], s2);
 #pragma unroll
         for (int db = 0; db < 2; ++db) {
-          dvT[db] = mfma32(frag_tr(ld, db, 2 * qb + s2, lane), pp, dvT[db]);
-          dkT[db] = mfma32(frag_tr(lq, db, 2 * qb + s2, lane), pd, dkT[db]);
+          if (ABL == 2) {
+            dvT[db] = mfma32(frag_rows(ld, 32 * db, 2 * qb + s2, lane), pp, dvT[db]);
+            dkT[db] = mfma32(frag_rows(lq, 32 * db, 2 * qb + s2, lane), pd, dkT[db]);
+          } else {
+            dvT[db] = mfma32(frag_tr(ld, db, 2 * qb + s2, lane), pp, dvT[db]);
+            dkT[db] = mfma32(frag_tr(lq, db, 2 * qb + s2, lane), pd, dkT[db]);
+          }
         }
       }
     if (more) {
@@ -358,13 +366,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
       if (tid < 64) { lstat[cur ^ 1][0][tid] = st_l; lstat[cur ^ 1][1][tid] = st_d; }
     }
     __syncthreads();
-    cur ^= 1;
+    if (ABL != 1) cur ^= 1;
   }
   store_T(g.dv, (long)b * g.dv.sb + hd * g.dv.sh, dvT, 1.f, key, g.n, lane, kmasked);
   store_T(g.dk, (long)b * g.dk.sb + hd * g.dk.sh, dkT, g.scale, key, g.n, lane, kmasked);
 }
 
 // ------------------------------------------------------------------ backward dQ
+template <int ABL = 0>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][8192];  // [buf][K / V]
   __shared__ __attribute__((aligned(16))) float lbias[2][64];
@@ -398,7 +407,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs g) {
   int cur = 0;
   for (int t = 0; t < nt; ++t) {
     const int kv0 = t * 64;
-    const bool more = t + 1 < nt;
+    const bool more = ABL != 1 && t + 1 < nt;
     if (more) {
       load_rows(rk, K, g.k.sr, kv0 + 64, g.n, tid);
       load_rows(rv, V, g.v.sr, kv0 + 64, g.n, tid);
@@ -410,10 +419,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs g) {
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       floatx16 s, dp;
+      s = mfma32(frag_rows(lk, 32 * kb, 0, lane), qf[0], floatx16{});
+      dp = mfma32(frag_rows(lv, 32 * kb, 0, lane), df[0], floatx16{});
 #pragma unroll
-      for (int i = 0; i < 16; ++i) { s[i] = 0.f; dp[i] = 0.f; }
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
+      for (int ks = 1; ks < 4; ++ks) {
         s = mfma32(frag_rows(lk, 32 * kb, ks, lane), qf[ks], s);
         dp = mfma32(frag_rows(lv, 32 * kb, ks, lane), df[ks], dp);
       }
@@ -436,7 +445,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs g) {
       for (int s2 = 0; s2 < 2; ++s2) {
         const bf16x8 pd = pack_acc(dS[kb], s2);
 #pragma unroll
-        for (int db = 0; db < 2; ++db) dqT[db] = mfma32(frag_tr(lk, db, 2 * kb + s2, lane), pd, dqT[db]);
+        for (int db = 0; db < 2; ++db)
+          dqT[db] = mfma32(ABL == 2 ? frag_rows(lk, 32 * db, 2 * kb + s2, lane) : frag_tr(lk, db, 2 * kb + s2, lane), pd,
+                           dqT[db]);
       }
     if (more) {
       store_rows(lds[cur ^ 1][0], rk, tid);
@@ -444,7 +455,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs g) {
       if (tid < 64) lbias[cur ^ 1][tid] = key_bias(g, b, kv0 + 64 + tid);
     }
     __syncthreads();
-    cur ^= 1;
+    if (ABL != 1) cur ^= 1;
   }
   store_T(g.dq, (long)b * g.dq.sb + hd * g.dq.sh, dqT, g.scale, qrow, g.n, lane, false);
 }
@@ -515,9 +526,17 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, s, g, H, rows);
   VPT_LAUNCH_CHECK();
   dim3 grid((n + 127) / 128, H, B);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, s, g);
-  VPT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, s, g);
+  if (g_variant == 1) {
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<1>, grid, dim3(256), 0, s, g);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<1>, grid, dim3(256), 0, s, g);
+  } else if (g_variant == 2) {
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, grid, dim3(256), 0, s, g);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<2>, grid, dim3(256), 0, s, g);
+  } else {
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<0>, grid, dim3(256), 0, s, g);
+    VPT_LAUNCH_CHECK();
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<0>, grid, dim3(256), 0, s, g);
+  }
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
@@ -526,5 +545,13 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
 extern "C" int vpt_attn_set_rescale_threshold(float tau) {
   VPT_CHECK_ARG(tau >= 0.f && tau <= 64.f, "vpt_attn_set_rescale_threshold: tau in [0, 64]");
   g_tau = tau;
+  return VPT_OK;
+}
+
+// Benchmark hook: backward kernel variant (0 = production; 1, 2 = timing-only ablations whose
+// results are wrong: 1 = no in-loop tile staging, 2 = row reads in place of transposed reads).
+extern "C" int vpt_attn_set_variant(int v) {
+  VPT_CHECK_ARG(v >= 0 && v <= 2, "vpt_attn_set_variant: 0, 1 or 2");
+  g_variant = v;
   return VPT_OK;
 }

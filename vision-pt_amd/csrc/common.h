@@ -30,8 +30,14 @@ __device__ __forceinline__ unsigned short f2h(float f) {
   return __builtin_bit_cast(unsigned short, v);
 }
 
+typedef float float2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+// Two f32 -> packed bf16 pair (RNE) as ONE v_cvt_pk_bf16_f32 (a per-element cast costs a convert per
+// half plus an OR to merge).
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  const float2_t v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -561,13 +561,13 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ part, long n, int
   }
 }
 
-// Geometry choice: the 256x256 tile when it still gives >= ~1.5 waves of blocks on 256 CUs,
+// Geometry choice: the 256x256 ring when its grid (x split-K slices) fills most of the 256 CUs,
 // otherwise 128x128 (2 blocks/CU, 4x the tiles).
 int g_geo_override = 0;  // 0 = heuristic; 128 / 256 / 2561 / 2562 force a geometry (benchmarking)
 int pick_geo(int M, int N, int splits) {
   if (g_geo_override) return g_geo_override;
   const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256) * splits;
-  return t256 >= 384 ? 256 : 128;
+  return t256 >= 160 ? 256 : 128;
 }
 
 }  // namespace

@@ -28,6 +28,7 @@ SIGNATURES: dict[str, list] = {
     "vpt_attn_bwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, P, L, L, P, L,
                      P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, F, P],
     "vpt_attn_set_rescale_threshold": [F],
+    "vpt_attn_set_variant": [I],
     "vpt_rmsnorm_fwd": [P, L, P, P, L, P, I, I, F, P],
     "vpt_rmsnorm_bwd_blocks": [I],
     "vpt_rmsnorm_bwd": [P, L, P, L, P, P, P, L, P, L, P, I, I, P],

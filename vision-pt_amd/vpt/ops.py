@@ -121,11 +121,24 @@ def linear_wgrad(dy, x, out, accumulate=False, splits=1, workspace=None):
 
 
 def wgrad_splits(N: int, K: int, M: int) -> int:
-    """Split-K factor so that the wgrad grid has ~2 blocks per CU (256 CUs)."""
-    tiles = ((N + 127) // 128) * ((K + 127) // 128)
-    s = max(1, min(64, (512 + tiles - 1) // tiles))
-    s = min(s, max(1, M // 256))
-    return s
+    """Split-K factor for a weight gradient dW[N,K] = dy[M,N]^T x[M,K] (reduction over M tokens).
+
+    Cost model for the 256x256 ring kernel (one block per CU, 256 CUs): the tile grid runs in
+    ceil(tiles*s/256) rounds of M/s tokens each (~33 ns per token per tile at ~1 PF/s chip-wide, plus
+    ~3 us prologue/epilogue), and the split-K reduction streams s*N*K*4 bytes (~4 TB/s, ~5 us launch).
+    """
+    tiles = ((N + 255) // 256) * ((K + 255) // 256)
+    best_s, best_t = 1, None
+    for s in range(1, 65):
+        if s > 1 and M // s < 256:
+            break
+        rounds = -(-tiles * s // 256)
+        t = rounds * ((M / s) * 0.0336 + 3.0)
+        if s > 1:
+            t += (s + 1) * N * K * 4 / 4.0e6 + 5.0
+        if best_t is None or t < best_t:
+            best_s, best_t = s, t
+    return best_s
 
 
 # ----------------------------------------------------------------------------- norms
