@@ -37,6 +37,17 @@ PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip 
 PEAK_HBM_GBS = 8000.0
 
 
+def measured_traffic(op: str):
+    """HBM bytes per launch of `op` from the committed rocprofv3 PMC summary (tools/round_profile.sh ->
+    tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE passes, gfx950 read correction), or None."""
+    path = os.path.join(ROOT, "profiles", "traffic_latest.json")
+    try:
+        d = json.load(open(path))
+        return d[op]["hbm_bytes_per_launch"], f"profiles/traffic_latest.json ({d.get('_tag', '?')})"
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def train_flops_per_image(np_: int, D=768, F=2048, depth=12, cs=4, bd=128) -> float:
     """3x forward matmul FLOPs + 3x attention forward (no recompute credit)."""
     f = 2 * np_ * (768 * bd + bd * D)
@@ -179,6 +190,7 @@ def main():
                         mean_gflop=fl / 1e9)
     dom = max(stats, key=lambda k: stats[k]["total_ms"])
     ach = stats[dom]["tflops"]
+    traffic, traffic_src = measured_traffic(dom)
     np_avg = sum((W // 16) * (H // 16) for W, H in BUCKETS) / len(BUCKETS)
     step_tflop = train_flops_per_image(np_avg) * args.batch / 1e12
     result = {
@@ -190,7 +202,8 @@ def main():
                    "seq_len": "4042-4170 tokens", "buckets_wh": BUCKETS, "parallelism": f"dp{world}",
                    "loss_target": "image", "optimizer": "RAdamScheduleFree (fused HIP)", "grad_checkpointing": False},
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                     "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
                      "algorithmic_gflop_per_launch": round(stats[dom]["mean_gflop"], 3),
                      "mean_launch_ms": round(stats[dom]["mean_ms"], 4)},
         "kernels": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in stats.items()},

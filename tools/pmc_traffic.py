@@ -1,0 +1,87 @@
+"""Per-launch HBM traffic of the bench's probed ops from two rocprofv3 counter passes
+(FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950: MI355X_MICROARCH.md §rocprofv3 PMC slots).
+
+  python tools/pmc_traffic.py FETCH_DIR WRITE_DIR KTRACE_DIR OUT.json
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch. gfx950 correction (MI355X_MICROARCH.md §HBM):
+FETCH_SIZE reports exactly half of the bytes of a wide coalesced streaming read (16 B per lane,
+global_load and LDS-DMA alike) -- every operand load of the GEMM and attention kernels is such a
+read -- so read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE is exact for 16-B streaming stores.
+The kernel-trace stats of the same command give each op's mean duration per launch (sum of its
+kernels' durations / launches), to check against bench.py's HIP-event probe.
+"""
+
+import collections
+import csv
+import glob
+import json
+import sys
+
+# op -> (kernel-name substrings that belong to it, the substring counted as one launch of the op)
+OPS = {
+    "gemm": (("gemm_ring_kernel", "gemm_bf16_kernel", "splitk_reduce_kernel"), ("gemm_ring_kernel", "gemm_bf16_kernel")),
+    "attn_fwd": (("attn_fwd_kernel",), ("attn_fwd_kernel",)),
+    "attn_bwd": (("attn_bwd_pre_kernel", "attn_bwd_dkdv_kernel", "attn_bwd_dq_kernel"), ("attn_bwd_dkdv_kernel",)),
+}
+
+
+def _op_of(name):
+    for op, (members, _) in OPS.items():
+        if any(m in name for m in members):
+            return op
+    return None
+
+
+def _counter(dirname, counter):
+    path = glob.glob(f"{dirname}/**/*counter_collection.csv", recursive=True)[0]
+    tot = collections.defaultdict(float)
+    launches = collections.Counter()
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        op = _op_of(r["Kernel_Name"])
+        if op is None:
+            continue
+        tot[op] += float(r["Counter_Value"])
+        if any(m in r["Kernel_Name"] for m in OPS[op][1]):
+            launches[op] += 1
+    return tot, launches
+
+
+def main():
+    fdir, wdir, kdir, out = sys.argv[1:5]
+    fetch, nf = _counter(fdir, "FETCH_SIZE")
+    write, nw = _counter(wdir, "WRITE_SIZE")
+    stats = glob.glob(f"{kdir}/**/*kernel_stats.csv", recursive=True)[0]
+    dur = collections.defaultdict(float)
+    calls = collections.Counter()
+    for r in csv.DictReader(open(stats)):
+        op = _op_of(r["Name"])
+        if op is None:
+            continue
+        dur[op] += float(r["TotalDurationNs"])
+        if any(m in r["Name"] for m in OPS[op][1]):
+            calls[op] += int(r["Calls"])
+    res = {}
+    for op in OPS:
+        if not nf[op] or not nw[op]:
+            continue
+        rd = 2.0 * fetch[op] * 1024 / nf[op]
+        wr = write[op] * 1024 / nw[op]
+        res[op] = {
+            "hbm_bytes_per_launch": round(rd + wr),
+            "read_bytes_per_launch": round(rd), "write_bytes_per_launch": round(wr),
+            "fetch_size_kib_per_launch_raw": round(fetch[op] / nf[op], 1),
+            "launches_pmc": nf[op],
+            "rocprof_mean_ms_per_launch": round(dur[op] / calls[op] / 1e6, 4) if calls[op] else None,
+            "rocprof_launches": calls[op],
+        }
+    res["_method"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of the same "
+                      "command; read bytes = 2 x FETCH_SIZE x 1024 (gfx950 half-count of 16-B/lane reads), "
+                      "write bytes = WRITE_SIZE x 1024; per launch of the op")
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -32,6 +32,7 @@ struct AttnArgs {
   int n, n_dense;
   float scale, scale_log2;
   float tau;  // forward lazy-rescale threshold
+  int kb0;    // start of the key-bias LDS array: n_dense rounded down to 64 (fwd, dq)
 };
 
 constexpr float kNegInf = -__builtin_huge_valf();
@@ -55,21 +56,50 @@ __device__ __forceinline__ int tile_unit_off(int row, int unit) {
   return row * 128 + (((unit >> 1) ^ sigma(row)) << 4) + ((unit & 1) << 3);
 }
 
-// 64x64 bf16 tile (rows r0..r0+63 of one (b,h)) -> 2 uint4 per thread (256 threads).
-__device__ __forceinline__ void load_rows(uint4 (&r)[2], const bf16_t* base, long sr, int r0, int n, int tid) {
+// ---- LDS-DMA staging (global_load_lds; guide §5.7): one wave-instruction moves 1 KB (dwordx4, 16 B
+// per lane) or 256 B (dword) from a wave-uniform SGPR base + per-lane 32-bit offset straight into LDS
+// at M0 + lane*width. No VGPR round trip and no ds_write; completion is `s_waitcnt vmcnt(0)` by the
+// issuing wave, then a barrier. The opening s_nop covers SGPR operands written by v_readfirstlane.
+__device__ __forceinline__ const void* uniform_ptr(const void* p) {
+  const unsigned long long v = (unsigned long long)p;
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (const void*)(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(VPT_LDS const char*)p);
+}
+__device__ __forceinline__ void dma_x4(const void* sbase, uint32_t voff, uint32_t m0v) {
+  unsigned keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(m0v) : "memory");
+}
+__device__ __forceinline__ void dma_x1(const void* sbase, uint32_t voff, uint32_t m0v) {
+  unsigned keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(m0v) : "memory");
+}
+// Rows r0..r0+63 of a (b,h) slice -> the tile_off LDS image: 8 pieces of 1 KB (rows 8q..8q+7), two
+// per wave (q = 2*wid + i). The image is written lane-linearly, so position p of a row receives its
+// logical chunk p ^ sigma(row) (sigma-swizzle moved to the source address). Rows >= n are clamped to
+// n-1: finite values the callers mask (keys: -inf bias; queries: zeroed rows).
+__device__ __forceinline__ void dma_rows(char* lds, const void* head, long sr, int r0, int n, int wid, int lane) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int c = tid + 256 * i, row = c >> 3, ch = c & 7;
-    if (r0 + row < n) r[i] = *reinterpret_cast<const uint4*>(base + (long)(r0 + row) * sr + ch * 8);
-    else r[i] = make_uint4(0, 0, 0, 0);
+    const int q = 2 * wid + i, row = 8 * q + (lane >> 3);
+    const int c = (lane & 7) ^ sigma(row);
+    const int r = min(r0 + row, n - 1);
+    dma_x4(head, (uint32_t)(((long)r * sr + c * 8) * 2), lds_addr(lds + q * 1024));
   }
 }
-__device__ __forceinline__ void store_rows(char* lds, const uint4 (&r)[2], int tid) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = tid + 256 * i;
-    *reinterpret_cast<uint4*>(lds + tile_off(c >> 3, c & 7)) = r[i];
-  }
+// 64 f32 statistics (rows r0..r0+63, clamped to n-1) -> lds, one 256-B piece.
+__device__ __forceinline__ void dma_stat(float* lds, const void* head, int r0, int n, int lane) {
+  dma_x1(head, (uint32_t)(min(r0 + lane, n - 1) * 4), lds_addr(lds));
+}
+// Zero rows nv..63 of a staged 64x64 tile (all 8 chunks of each row).
+__device__ __forceinline__ void zero_rows(char* lds, int nv, int tid) {
+  for (int idx = tid; idx < (64 - nv) * 8; idx += 256)
+    *reinterpret_cast<uint4*>(lds + (nv + (idx >> 3)) * 128 + (idx & 7) * 16) = make_uint4(0, 0, 0, 0);
 }
 
 // A-operand (32 rows x 16 k) read by rows: lane row = rbase + (lane&31), k = 16s + 8h + j.
@@ -135,10 +165,18 @@ __device__ __forceinline__ void store_T(const OTensor4& t, long base_off, const 
     }
 }
 
+// Key bias for keys [kb0, round_up(n, 64)) in LDS, filled once per block: 0 below n_dense,
+// kbias[b][key] in [n_dense, n), -inf for the padding keys >= n. Dense tiles (kv0 + 64 <= n_dense)
+// never read it.
+__device__ __forceinline__ void fill_key_bias(float* kbl, const AttnArgs& g, int b, int tid) {
+  const int nk = (g.n + 63) / 64 * 64 - g.kb0;
+  for (int i = tid; i < nk; i += 256) kbl[i] = key_bias(g, b, g.kb0 + i);
+}
+
 // ------------------------------------------------------------------ forward
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][8192];
-  __shared__ __attribute__((aligned(16))) float lbias[2][64];
+  extern __shared__ __attribute__((aligned(16))) float kbl[];  // key bias of keys kb0.. (fill_key_bias)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
   const int b = blockIdx.z, hd = blockIdx.y;
   const int q0 = blockIdx.x * 128 + wid * 32;
@@ -155,21 +193,21 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs g) {
   float m_c = kNegInf, lsum = 0.f;  // running reference max (scaled log2 units), row sum
 
   const int nt = (g.n + 63) / 64;
-  uint4 rk[2], rv[2];
-  load_rows(rk, K, g.k.sr, 0, g.n, tid);
-  load_rows(rv, V, g.v.sr, 0, g.n, tid);
-  store_rows(lds[0][0], rk, tid);
-  store_rows(lds[0][1], rv, tid);
-  if (tid < 64) lbias[0][tid] = key_bias(g, b, tid);
+  const void* Ku = uniform_ptr(K);
+  const void* Vu = uniform_ptr(V);
+  fill_key_bias(kbl, g, b, tid);
+  dma_rows(lds[0][0], Ku, g.k.sr, 0, g.n, wid, lane);
+  dma_rows(lds[0][1], Vu, g.v.sr, 0, g.n, wid, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   int cur = 0;
   for (int t = 0; t < nt; ++t) {
     const int kv0 = t * 64;
     const bool more = t + 1 < nt;
-    if (more) {
-      load_rows(rk, K, g.k.sr, kv0 + 64, g.n, tid);
-      load_rows(rv, V, g.v.sr, kv0 + 64, g.n, tid);
+    if (more) {  // next K/V tile by LDS-DMA into the other buffer, in flight during this tile
+      dma_rows(lds[cur ^ 1][0], Ku, g.k.sr, kv0 + 64, g.n, wid, lane);
+      dma_rows(lds[cur ^ 1][1], Vu, g.v.sr, kv0 + 64, g.n, wid, lane);
     }
     const char* lk = lds[cur][0];
     const char* lv = lds[cur][1];
@@ -186,7 +224,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs g) {
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          const floatx4 bias = *reinterpret_cast<const floatx4*>(&lbias[cur][32 * kb + 8 * g4 + 4 * h]);
+          const floatx4 bias = *reinterpret_cast<const floatx4*>(&kbl[kv0 - g.kb0 + 32 * kb + 8 * g4 + 4 * h]);
 #pragma unroll
           for (int e = 0; e < 4; ++e) sacc[kb][4 * g4 + e] += bias[e];
         }
@@ -226,12 +264,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs g) {
 #pragma unroll
         for (int db = 0; db < 2; ++db) oacc[db] = mfma32(frag_tr(lv, db, 2 * kb + s, lane), pf, oacc[db]);
       }
-    if (more) {
-      store_rows(lds[cur ^ 1][0], rk, tid);
-      store_rows(lds[cur ^ 1][1], rv, tid);
-      if (tid < 64) lbias[cur ^ 1][tid] = key_bias(g, b, kv0 + 64 + tid);
-    }
-    __syncthreads();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of the next tile landed
+    __syncthreads();                                    // ... and every wave's; this tile fully read
     cur ^= 1;
   }
   const float l = pair_sum(lsum);
@@ -290,31 +324,35 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
   for (int i = 0; i < 16; ++i) { dvT[0][i] = dvT[1][i] = dkT[0][i] = dkT[1][i] = 0.f; }
 
   const int nt = (g.n + 63) / 64;
-  uint4 rq[2], rd[2];
-  float st_l = 0.f, st_d = 0.f;
-  auto load_stats = [&](int q0) {
-    if (tid < 64) {
-      const int qq = q0 + tid;
-      st_l = qq < g.n ? LSE[qq] : __builtin_huge_valf();
-      st_d = qq < g.n ? DEL[qq] : 0.f;
+  const void* Qu = uniform_ptr(Q);
+  const void* Du = uniform_ptr(dO);
+  const void* Lu = uniform_ptr(LSE);
+  const void* Eu = uniform_ptr(DEL);
+  // Q / dO tiles and their lse / delta rows by LDS-DMA (waves 0 and 1 also move one stats piece each).
+  auto stage = [&](int buf, int r0) {
+    dma_rows(lds[buf][0], Qu, g.q.sr, r0, g.n, wid, lane);
+    dma_rows(lds[buf][1], Du, g.dO.sr, r0, g.n, wid, lane);
+    if (wid == 0) dma_stat(lstat[buf][0], Lu, r0, g.n, lane);
+    else if (wid == 1) dma_stat(lstat[buf][1], Eu, r0, g.n, lane);
+  };
+  // After the DMA into `buf` landed for every wave: a partial last query tile gets its padding rows of
+  // Q and dO zeroed, so the clamped duplicates contribute nothing to dK (dS.Q) or dV (P^T.dO).
+  auto settle = [&](int buf, int r0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (g.n - r0 < 64) {
+      zero_rows(lds[buf][0], g.n - r0, tid);
+      zero_rows(lds[buf][1], g.n - r0, tid);
+      __syncthreads();
     }
   };
-  load_rows(rq, Q, g.q.sr, 0, g.n, tid);
-  load_rows(rd, dO, g.dO.sr, 0, g.n, tid);
-  load_stats(0);
-  store_rows(lds[0][0], rq, tid);
-  store_rows(lds[0][1], rd, tid);
-  if (tid < 64) { lstat[0][0][tid] = st_l; lstat[0][1][tid] = st_d; }
-  __syncthreads();
+  stage(0, 0);
+  settle(0, 0);
 
   int cur = 0;
   for (int t = 0; t < nt; ++t) {
     const bool more = ABL != 1 && t + 1 < nt;
-    if (more) {
-      load_rows(rq, Q, g.q.sr, (t + 1) * 64, g.n, tid);
-      load_rows(rd, dO, g.dO.sr, (t + 1) * 64, g.n, tid);
-      load_stats((t + 1) * 64);
-    }
+    if (more) stage(cur ^ 1, (t + 1) * 64);
     const char* lq = lds[cur][0];
     const char* ld = lds[cur][1];
     floatx16 P[2], dS[2];
@@ -360,12 +398,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
           }
         }
       }
-    if (more) {
-      store_rows(lds[cur ^ 1][0], rq, tid);
-      store_rows(lds[cur ^ 1][1], rd, tid);
-      if (tid < 64) { lstat[cur ^ 1][0][tid] = st_l; lstat[cur ^ 1][1][tid] = st_d; }
-    }
-    __syncthreads();
+    if (more) settle(cur ^ 1, (t + 1) * 64);
     if (ABL != 1) cur ^= 1;
   }
   store_T(g.dv, (long)b * g.dv.sb + hd * g.dv.sh, dvT, 1.f, key, g.n, lane, kmasked);
@@ -376,7 +409,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
 template <int ABL = 0>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][8192];  // [buf][K / V]
-  __shared__ __attribute__((aligned(16))) float lbias[2][64];
+  extern __shared__ __attribute__((aligned(16))) float kbl[];   // key bias of keys kb0.. (fill_key_bias)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
   const int b = blockIdx.z, hd = blockIdx.y;
   const int q0 = blockIdx.x * 128 + wid * 32;
@@ -396,12 +429,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs g) {
   for (int i = 0; i < 16; ++i) { dqT[0][i] = 0.f; dqT[1][i] = 0.f; }
 
   const int nt = (g.n + 63) / 64;
-  uint4 rk[2], rv[2];
-  load_rows(rk, K, g.k.sr, 0, g.n, tid);
-  load_rows(rv, V, g.v.sr, 0, g.n, tid);
-  store_rows(lds[0][0], rk, tid);
-  store_rows(lds[0][1], rv, tid);
-  if (tid < 64) lbias[0][tid] = key_bias(g, b, tid);
+  const void* Ku = uniform_ptr(K);
+  const void* Vu = uniform_ptr(V);
+  fill_key_bias(kbl, g, b, tid);
+  dma_rows(lds[0][0], Ku, g.k.sr, 0, g.n, wid, lane);
+  dma_rows(lds[0][1], Vu, g.v.sr, 0, g.n, wid, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   int cur = 0;
@@ -409,8 +442,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs g) {
     const int kv0 = t * 64;
     const bool more = ABL != 1 && t + 1 < nt;
     if (more) {
-      load_rows(rk, K, g.k.sr, kv0 + 64, g.n, tid);
-      load_rows(rv, V, g.v.sr, kv0 + 64, g.n, tid);
+      dma_rows(lds[cur ^ 1][0], Ku, g.k.sr, kv0 + 64, g.n, wid, lane);
+      dma_rows(lds[cur ^ 1][1], Vu, g.v.sr, kv0 + 64, g.n, wid, lane);
     }
     const char* lk = lds[cur][0];
     const char* lv = lds[cur][1];
@@ -431,7 +464,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs g) {
       if (!dense) {  // scalar branch: only the context / padding key tiles carry a bias
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          const floatx4 bias = *reinterpret_cast<const floatx4*>(&lbias[cur][32 * kb + 8 * g4 + 4 * h]);
+          const floatx4 bias = *reinterpret_cast<const floatx4*>(&kbl[kv0 - g.kb0 + 32 * kb + 8 * g4 + 4 * h]);
 #pragma unroll
           for (int e = 0; e < 4; ++e) s[4 * g4 + e] += bias[e];
         }
@@ -449,19 +482,19 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs g) {
           dqT[db] = mfma32(ABL == 2 ? frag_rows(lk, 32 * db, 2 * kb + s2, lane) : frag_tr(lk, db, 2 * kb + s2, lane), pd,
                            dqT[db]);
       }
-    if (more) {
-      store_rows(lds[cur ^ 1][0], rk, tid);
-      store_rows(lds[cur ^ 1][1], rv, tid);
-      if (tid < 64) lbias[cur ^ 1][tid] = key_bias(g, b, kv0 + 64 + tid);
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (ABL != 1) cur ^= 1;
   }
   store_T(g.dq, (long)b * g.dq.sb + hd * g.dq.sh, dqT, g.scale, qrow, g.n, lane, false);
 }
 
+// Dynamic LDS of the key-bias array (fill_key_bias); n <= 32768 keeps it within 128 KB.
+size_t key_bias_lds_bytes(const AttnArgs& g) { return (size_t)((g.n + 63) / 64 * 64 - g.kb0) * sizeof(float); }
+
 int check_common(int B, int H, int n) {
   VPT_CHECK_ARG(B > 0 && H > 0 && n > 0, "attention: empty shape");
+  VPT_CHECK_ARG(n <= 32768, "attention: n <= 32768 (key-bias LDS array)");
   return VPT_OK;
 }
 
@@ -488,8 +521,9 @@ extern "C" int vpt_attn_fwd(const void* q, long q_sb, long q_sh, long q_sr,
   g.n = n; g.n_dense = n_dense < n ? n_dense : n;
   g.scale = scale; g.scale_log2 = scale * 1.4426950408889634f;
   g.tau = g_tau;
+  g.kb0 = g.n_dense / 64 * 64;
   dim3 grid((n + 127) / 128, H, B);
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, g);
+  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), key_bias_lds_bytes(g), (hipStream_t)stream, g);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
@@ -521,21 +555,23 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
   g.kbias = kbias; g.kb_sb = kb_sb;
   g.n = n; g.n_dense = n_dense < n ? n_dense : n;
   g.scale = scale; g.scale_log2 = scale * 1.4426950408889634f;
+  g.kb0 = g.n_dense / 64 * 64;
   hipStream_t s = (hipStream_t)stream;
   const long rows = (long)B * H * n;
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, s, g, H, rows);
   VPT_LAUNCH_CHECK();
   dim3 grid((n + 127) / 128, H, B);
+  const size_t kbl = key_bias_lds_bytes(g);
   if (g_variant == 1) {
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<1>, grid, dim3(256), 0, s, g);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<1>, grid, dim3(256), 0, s, g);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<1>, grid, dim3(256), kbl, s, g);
   } else if (g_variant == 2) {
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, grid, dim3(256), 0, s, g);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<2>, grid, dim3(256), 0, s, g);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<2>, grid, dim3(256), kbl, s, g);
   } else {
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<0>, grid, dim3(256), 0, s, g);
     VPT_LAUNCH_CHECK();
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<0>, grid, dim3(256), 0, s, g);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<0>, grid, dim3(256), kbl, s, g);
   }
   VPT_LAUNCH_CHECK();
   return VPT_OK;
