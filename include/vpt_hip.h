@@ -133,7 +133,10 @@ int vpt_swiglu_fwd(const void* x12, long M, int F, void* h, void* stream);
 int vpt_swiglu_bwd(const void* dh, const void* x12, long M, int F, void* dx12, void* stream);
 int vpt_silu(const void* x, const void* dy, void* out, long n, int backward, void* stream);
 int vpt_colsum_blocks(long M);
-int vpt_colsum(const void* in, long ld, long M, int N, float* part, void* stream);
+/* Linear bias gradient out[N] (=|+=) sum over M rows of in (bf16, row stride ld): column partials into
+ * part [vpt_colsum_blocks(M)][N] f32 scratch, then a fixed-order row reduction (deterministic).
+ * Replaces the autograd bias gradients of every nn.Linear on the path. */
+int vpt_bias_grad(const void* in, long ld, long M, int N, float* part, float* out, int accumulate, void* stream);
 int vpt_cast_f32_bf16(const float* in, long n, void* out, void* stream);
 
 /* ---- optimizer -------------------------------------------------------------------------------

@@ -284,11 +284,21 @@ def test_swiglu(ops):
     assert rel(dx, xf.grad) < 1e-2
 
 
-def test_bias_grad(ops):
-    dy = rnd(5000, 768, seed=52)
-    out = torch.zeros(768, device=DEV)
+@pytest.mark.parametrize("M,N", [(5000, 768), (33360, 776), (100, 4096)])
+def test_bias_grad(ops, M, N):
+    """Column sums (slice partials + fixed-order reduction): ragged column blocks, accumulate, and
+    bitwise-repeatable back-to-back launches."""
+    dy = rnd(M, N, seed=52)
+    ref = dy.double().sum(0)
+    out = torch.zeros(N, device=DEV)
     ops.bias_grad(dy, out)
-    assert rel(out, dy.float().sum(0)) < 1e-5
+    assert rel(out, ref) < 1e-5
+    first = out.clone()
+    for _ in range(3):
+        ops.bias_grad(dy, out)
+        assert torch.equal(out, first)  # deterministic
+    ops.bias_grad(dy, out, accumulate=True)
+    assert rel(out, 2 * ref) < 1e-5
 
 
 def test_patchify_unpatchify_roundtrip(ops):

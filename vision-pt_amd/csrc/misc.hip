@@ -304,6 +304,8 @@ __global__ void swiglu_bwd_kernel(const bf16_t* __restrict__ dh, const bf16_t* _
 // ---------------------------------------------------------------- column sums (bias grads)
 // Column sums of a bf16 [M][N] matrix into f32 partial rows part[slice][N]. Grid (N/256, slices);
 // block = 32 lanes x 16-B chunks (256 columns, 512 B per row segment) x 8 row groups.
+// Column sums of a bf16 [M][N] matrix into per-slice partials part[S][N] (grid: N/256 column blocks x
+// S row slices); vpt_bias_grad then sums the S partial rows in slice order (deterministic).
 __global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ in, long ld, long M, int N,
                                                      long rows_per_slice, float* __restrict__ part) {
   __shared__ float red[8][257];
@@ -313,7 +315,20 @@ __global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ 
   const long r1 = min(M, r0 + rows_per_slice);
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (col < N) {
-    for (long r = r0 + rg; r < r1; r += 8) {
+    long r = r0 + rg;
+    for (; r + 24 < r1; r += 32) {  // 4 independent 16-B loads in flight per lane
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4*>(in + (r + 8 * u) * ld + col);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float f[8];
+        unpack8(v[u], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[e] += f[e];
+      }
+    }
+    for (; r < r1; r += 8) {
       float f[8];
       unpack8(*reinterpret_cast<const uint4*>(in + r * ld + col), f);
 #pragma unroll
@@ -554,18 +569,23 @@ extern "C" int vpt_swiglu_bwd(const void* dh, const void* x12, long M, int F, vo
 }
 
 extern "C" int vpt_colsum_blocks(long M) {  // number of partial rows written by vpt_colsum
-  long b = (M + 255) / 256;
-  return (int)(b > 64 ? 64 : (b < 1 ? 1 : b));
+  // up to 256 row slices of >= 128 rows: with the (N/256)-wide column grid this keeps >= 3 blocks per
+  // CU even at N = 768
+  long b = (M + 127) / 128;
+  return (int)(b > 256 ? 256 : (b < 1 ? 1 : b));
 }
 
-extern "C" int vpt_colsum(const void* in, long ld, long M, int N, float* part, void* stream) {
-  VPT_CHECK_ARG(in && part && N % 8 == 0 && M > 0, "vpt_colsum: bad args");
+extern "C" int vpt_reduce_rows(const float* in, int R, int C, float* out, int accumulate, void* stream);
+
+extern "C" int vpt_bias_grad(const void* in, long ld, long M, int N, float* part, float* out, int accumulate,
+                             void* stream) {
+  VPT_CHECK_ARG(in && part && out && N % 8 == 0 && M > 0, "vpt_bias_grad: bad args");
   const int nb = vpt_colsum_blocks(M);
   const long per = (M + nb - 1) / nb;
   hipLaunchKernelGGL(colsum_kernel, dim3((N + 255) / 256, nb), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)in,
                      ld, M, N, per, part);
   VPT_LAUNCH_CHECK();
-  return VPT_OK;
+  return vpt_reduce_rows(part, nb, N, out, accumulate, stream);
 }
 
 extern "C" int vpt_embed_gather(const void* table, const long long* ids, long R, int D, void* out, void* stream) {

@@ -74,40 +74,63 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const bf16_t* __restri
     const int c = lane + 64 * i;
     if (c < nch) unpack8(*reinterpret_cast<const uint4*>(w + c * 8), wf[i]);
   }
-  for (long row = (long)blockIdx.x * 4 + wid; row < M; row += (long)gridDim.x * 4) {
-    const float r = rstd[row];
-    float xh[2][8], gg[2][8];
-    float dot = 0.f;
+  // Two rows per wave per iteration: all loads of both rows (x, dy, dres) are issued before any use,
+  // doubling the bytes in flight per wave (the kernel is HBM-latency-bound at one row).
+  const long stride = (long)gridDim.x * 4;
+  for (long row0 = (long)blockIdx.x * 4 + wid; row0 < M; row0 += 2 * stride) {
+    long rows[2] = {row0, row0 + stride};
+    uint4 vx[2][2], vd[2][2], vr[2][2];
+    float r[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = lane + 64 * i;
-      if (c < nch) {
-        float fx[8], fd[8];
-        unpack8(*reinterpret_cast<const uint4*>(x + row * ldx + c * 8), fx);
-        unpack8(*reinterpret_cast<const uint4*>(dy + row * lddy + c * 8), fd);
+    for (int k = 0; k < 2; ++k) {
+      const bool ok = rows[k] < M;
+      r[k] = ok ? rstd[rows[k]] : 0.f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          xh[i][e] = fx[e] * r;
-          gg[i][e] = fd[e] * wf[i][e];
-          dot += gg[i][e] * xh[i][e];
-          dwp[i][e] += fd[e] * xh[i][e];
-        }
+      for (int i = 0; i < 2; ++i) {
+        const int c = lane + 64 * i;
+        const bool in = ok && c < nch;
+        vx[k][i] = in ? *reinterpret_cast<const uint4*>(x + rows[k] * ldx + c * 8) : make_uint4(0, 0, 0, 0);
+        vd[k][i] = in ? *reinterpret_cast<const uint4*>(dy + rows[k] * lddy + c * 8) : make_uint4(0, 0, 0, 0);
+        vr[k][i] = in && dres ? *reinterpret_cast<const uint4*>(dres + rows[k] * ldr + c * 8) : make_uint4(0, 0, 0, 0);
       }
     }
-    dot = wave_sum(dot) / (float)D;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = lane + 64 * i;
-      if (c < nch) {
-        float o[8], fr[8];
-        if (dres) unpack8(*reinterpret_cast<const uint4*>(dres + row * ldr + c * 8), fr);
+    for (int k = 0; k < 2; ++k) {
+      if (rows[k] >= M) break;
+      const long row = rows[k];
+      float xh[2][8], gg[2][8];
+      float dot = 0.f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float d = r * (gg[i][e] - xh[i][e] * dot);
-          // reference: the residual branch and the norm branch gradients are bf16 tensors summed
-          o[e] = dres ? fr[e] + bf2f(f2bf(d)) : d;
+      for (int i = 0; i < 2; ++i) {
+        const int c = lane + 64 * i;
+        if (c < nch) {
+          float fx[8], fd[8];
+          unpack8(vx[k][i], fx);
+          unpack8(vd[k][i], fd);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            xh[i][e] = fx[e] * r[k];
+            gg[i][e] = fd[e] * wf[i][e];
+            dot += gg[i][e] * xh[i][e];
+            dwp[i][e] += fd[e] * xh[i][e];
+          }
         }
-        *reinterpret_cast<uint4*>(dx + row * lddx + c * 8) = pack8(o);
+      }
+      dot = wave_sum(dot) / (float)D;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = lane + 64 * i;
+        if (c < nch) {
+          float o[8], fr[8];
+          unpack8(vr[k][i], fr);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = r[k] * (gg[i][e] - xh[i][e] * dot);
+            // reference: the residual branch and the norm branch gradients are bf16 tensors summed
+            o[e] = dres ? fr[e] + bf2f(f2bf(d)) : d;
+          }
+          *reinterpret_cast<uint4*>(dx + row * lddx + c * 8) = pack8(o);
+        }
       }
     }
   }
@@ -245,6 +268,7 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
   floatx4 s = {0.f, 0.f, 0.f, 0.f};
   if (c < C) {
     if (C % 4 == 0) {
+#pragma unroll 8
       for (int r = rg; r < R; r += 16) s += *reinterpret_cast<const floatx4*>(in + (long)r * C + c);
     } else {
       for (int r = rg; r < R; r += 16)

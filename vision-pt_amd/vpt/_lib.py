@@ -47,7 +47,7 @@ SIGNATURES: dict[str, list] = {
     "vpt_swiglu_fwd": [P, L, I, P, P],
     "vpt_swiglu_bwd": [P, P, L, I, P, P],
     "vpt_colsum_blocks": [L],
-    "vpt_colsum": [P, L, L, I, P, P],
+    "vpt_bias_grad": [P, L, L, I, P, P, I, P],
     "vpt_embed_gather": [P, P, L, I, P, P],
     "vpt_embed_scatter_add": [P, P, L, I, LL, P, P],
     "vpt_cast_f32_bf16": [P, L, P, P],

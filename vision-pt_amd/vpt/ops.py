@@ -290,21 +290,16 @@ def colsum_blocks(M: int) -> int:
     return lib.vpt_colsum_blocks(M)
 
 
-def colsum(x, part):
-    M, N = x.shape
-    call("vpt_colsum", x.data_ptr(), x.stride(0), M, N, part.data_ptr(), stream())
-    return part
-
-
 def bias_grad(dy, out, part=None, accumulate=False):
-    """out[N] (=|+=) sum over rows of dy [M,N] (bf16) in f32."""
+    """out[N] (=|+=) sum over rows of dy [M,N] (bf16) in f32 (slice partials + fixed-order row sum)."""
     M, N = dy.shape
     nb = colsum_blocks(M)
     if part is None:
         part = torch.empty(nb, N, dtype=F32, device=dy.device)
-    part = part.view(-1)[: nb * N].view(nb, N)
-    colsum(dy, part)
-    return reduce_rows(part, out, accumulate)
+    part = part.view(-1)[: nb * N]
+    call("vpt_bias_grad", dy.data_ptr(), dy.stride(0), M, N, part.data_ptr(), out.data_ptr(), int(accumulate),
+         stream())
+    return out
 
 
 def embed_gather(table, ids, out):
