@@ -45,6 +45,9 @@ long vpt_gemm_workspace_bytes(int M, int N, int K, int splits);
  * 2561 = ring unstaggered, 2562 = 256x256 2-stage (benchmarking); 2563/2564 = timing-only ablations
  * of the ring (forward direction only; results are wrong). */
 int vpt_gemm_set_geometry(int geo);
+/* Diagnostic: u64 buffer [256][8][8] receiving per-wave K-step segment cycle sums from the stamped
+ * ring build (geometry 2566, forward direction); nullptr disables. */
+int vpt_gemm_set_debug(unsigned long long* buf);
 
 /* ---- flash attention, head_dim 64 ---------------------------------------------------------
  * Tensors addressed p[b*sb + h*sh + row*sr + d]. Keys < n_dense always valid; keys in
@@ -64,8 +67,9 @@ int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr, const void* k, 
 /* Forward lazy-rescale threshold in log2 units (default 8; 0 = rescale whenever the row max grows).
  * Test hook for the online-softmax rescale branch; process-wide. */
 int vpt_attn_set_rescale_threshold(float tau);
-/* Benchmark hook: backward kernel variant (0 = production; 1 / 2 = timing-only ablations with wrong
- * results: no in-loop tile staging / row reads in place of transposed reads). Process-wide. */
+/* Benchmark hook: kernel variant (0 = production, 4-wave blocks; 1 / 2 = timing-only backward
+ * ablations with wrong results: no in-loop tile staging / row reads in place of transposed reads;
+ * 3 = 8-wave blocks, correct). Process-wide. */
 int vpt_attn_set_variant(int v);
 
 /* ---- RMSNorm over the hidden dim -----------------------------------------------------------
@@ -101,6 +105,13 @@ int vpt_reduce_rows(const float* in, int R, int C, float* out, int accumulate, v
 int vpt_patchify(const void* img, int in_kind, const void* noise, const float* t, float noise_scale,
                  unsigned long long seed, int B, int H, int W, void* out, void* stream);
 int vpt_unpatchify(const void* patches, int B, int H, int W, void* img, int reverse, void* stream);
+/* Sampler: one Euler step with classifier-free guidance over the bf16 image z [B,3,H,W], the
+ * prediction read from the final-layer patch layout [n*np, 768] (n = 2B when cfg, positive half
+ * first); mode 0 = image prediction (v = (x - z) / clamp(1 - t, 1e-5)), 1 = velocity prediction;
+ * every op rounds to bf16 like the reference's bf16 tensors. Replaces the denoising loop body of
+ * JiTModel.generate (src/models/jit/pipeline.py:436-477). */
+int vpt_euler_cfg_step(void* z, const void* pred, int B, int H, int W, int cfg, float cfg_scale, int mode, float t,
+                       float dt, void* stream);
 int vpt_loss_blocks(void);
 int vpt_flow_loss(const void* pred, const void* img, const void* noise, const float* t, float noise_scale,
                   unsigned long long seed, int target, float t_eps, int B, int H, int W, void* dpred, float* part,

@@ -399,3 +399,46 @@ def find_nearest_bucket(buckets: list[tuple[int, int]], width: int, height: int)
     if best is None:
         raise AssertionError(f"No bucket found for image size {width}x{height}")
     return best
+
+
+# ------------------------------------------------------------------------------- sampler
+def generate(model: OracleJiT, emb: torch.Tensor, pos_ids: torch.Tensor, pos_mask: torch.Tensor,
+             neg_ids: torch.Tensor, noise: torch.Tensor, num_inference_steps: int = 20, cfg_scale: float = 2.0,
+             model_pred: str = "image", cfg_time_range=(0.0, 1.0)) -> torch.Tensor:
+    """Euler sampler with classifier-free guidance -- JiTModel.generate (src/models/jit/pipeline.py:378-488)
+    in execution dtype float32, class context. `noise` is the starting image (prepare_noisy_image,
+    :124-148); timesteps = linspace(0, 1, steps + 1) (prepare_timesteps, :150-161); the negative prompts'
+    embeddings are paired with the POSITIVE attention mask (prepare_context_embeddings, :193-219);
+    size inputs (H, W) / (H, W) / (0, 0) (:221-248). Returns the final (clean) image, f32."""
+    B, _, H, W = noise.shape
+    do_cfg = cfg_scale > 1.0
+    timesteps = torch.linspace(0.0, 1.0, num_inference_steps + 1)
+    pad = emb.shape[0] - 1
+    ctx_pos = F.embedding(pos_ids, emb, padding_idx=pad)
+    ctx_neg = F.embedding(neg_ids, emb, padding_idx=pad)
+    ctx = torch.cat([ctx_pos, ctx_neg]) if do_cfg else ctx_pos
+    mask = torch.cat([pos_mask, pos_mask]) if do_cfg else pos_mask
+    bb = 2 * B if do_cfg else B
+    size = torch.tensor([[H, W]], dtype=torch.float32).repeat(bb, 1)
+    crop = torch.zeros(bb, 2)
+    z = noise.float().clone()
+    for i, t in enumerate(timesteps[:-1]):
+        in_cfg = do_cfg and cfg_time_range[0] <= float(t) <= cfg_time_range[1]   # pipeline.py:437-439
+        x_in = torch.cat([z, z]) if in_cfg else z
+        n = x_in.shape[0]
+        pred = model(image=x_in, timestep=t.expand(n), context=ctx[:n], original_size=size[:n],
+                     target_size=size[:n], crop_coords=crop[:n], context_mask=mask[:n])
+        tb = t.expand(B).view(-1, 1, 1, 1)
+        if model_pred == "image":                                               # :312-319, :340-353
+            def to_v(img):
+                return (img - z) / (1 - tb).clamp_min(1e-5)                     # image_to_velocity :254-260
+        else:
+            def to_v(v):
+                return v
+        if in_cfg:
+            vp, vn = to_v(pred[:B]), to_v(pred[B:])
+            v = vp + cfg_scale * (vp - vn)                                      # make_cfg_velocity_pred :351-357
+        else:
+            v = to_v(pred[:B])
+        z = z + v * (timesteps[i + 1] - t)                                      # :477
+    return z

@@ -1,6 +1,6 @@
 """Generates the golden fixtures in tests/golden/ by running the REFERENCE (p1atdev/vision-pt at
 /root/reference) on CPU in the survey container. Only the resulting tensors are committed (no
-reference source travels). Re-run: `python tests/golden/make_golden.py` (needs /root/reference).
+reference source travels). Re-run: `python tests/golden/make_golden.py [sampler]` (needs /root/reference).
 
 Import recipe: SURVEY.md Appendix A (Recipe A for the denoiser/config/class encoder, Recipe B
 stubs for train/jit/arb_class_to_image.py to reach JiTModel.image_to_velocity).
@@ -15,6 +15,11 @@ Fixtures:
   ops.safetensors        timestep embedding (t = 0..9999 subsample + fractional), RoPE tables of
                          the 7 benchmark buckets (checksums + head/tail rows), tokenizer ids/masks,
                          bucket lists.
+  sampler.safetensors    JiTModel.generate (src/models/jit/pipeline.py:378-488) on the micro config,
+                         float32 execution, class context, 4 Euler steps, 2 x 64x48: starting noise,
+                         token ids/masks and the final image for four cases (CFG 2.0; no CFG; CFG 3.0
+                         inside cfg_time_range [0.2, 0.6]; velocity prediction). Metadata: the
+                         reference JiTModel state-dict keys and shapes (checkpoint layout).
 Weights are not stored: they are regenerated from oracle.jit_oracle.make_weights(cfg, seed).
 """
 
@@ -137,9 +142,53 @@ def grad_summary(prefix, grads, out, full_small=4096):
             out[f"{prefix}gfull/{n}"] = g.clone()
 
 
+def sampler_fixture(R, meta):
+    """Runs the reference's own JiTModel.generate; the PIL conversion is swapped for the raw tensor."""
+    pipe = importlib.import_module("src.models.jit.pipeline")
+    oc = micro_config()
+    V = 20
+    w = make_weights(oc, seed=1, n_classes=V)
+    l2i = os.path.join("/tmp", "vpt_golden_label2id.json")
+    json.dump({f"c{i}": i for i in range(V)}, open(l2i, "w"))
+    prompts = ["c1 c3", "c5 c7 c2"]
+    out = {}
+    keys = None
+    cases = {"cfg2": dict(cfg_scale=2.0), "nocfg": dict(cfg_scale=1.0),
+             "cfg3_window": dict(cfg_scale=3.0, cfg_time_range=[0.2, 0.6]), "vel_cfg2": dict(cfg_scale=2.0)}
+    for name, kw in cases.items():
+        cfg = R.cfg.JiTConfig(context_encoder=R.cfg.ClassContextConfig(label2id_map_path=l2i),
+                              denoiser=ref_config(R, oc), model_pred="velocity" if name.startswith("vel") else "image")
+        model = pipe.JiTModel(cfg)
+        model.denoiser.load_state_dict({k: v for k, v in w.items() if not k.startswith("class_encoder.")}, strict=True)
+        with torch.no_grad():
+            model.class_encoder.embedding.weight.copy_(w["class_encoder.embedding.weight"])
+        model.eval()
+        model.to_pil_images = lambda t: t.clone()
+        model.progress_bar = lambda total: __import__("contextlib").nullcontext(types.SimpleNamespace(update=lambda: None))
+        img = model.generate(prompts, width=48, height=64, num_inference_steps=4, max_token_length=8, seed=7,
+                             execution_dtype=torch.float32, device="cpu", **kw)
+        out[f"{name}/image"] = img
+        if keys is None:
+            keys = {k: list(v.shape) for k, v in model.state_dict().items()}
+    g = torch.Generator(device="cpu").manual_seed(7)
+    out["noise"] = torch.randn((2, 3, 64, 48), dtype=torch.float32, generator=g)  # pipeline.py:133-140
+    tok = model.class_encoder.tokenizer
+    o = tok.tokenize(prompts, max_length=8)
+    out["pos_ids"], out["pos_mask"] = o.class_ids, o.attention_mask
+    o = tok.tokenize([""] * 2, max_length=8)
+    out["neg_ids"], out["neg_mask"] = o.class_ids, o.attention_mask
+    save_file({k: v.contiguous() for k, v in out.items()}, os.path.join(HERE, "sampler.safetensors"),
+              metadata=dict(meta, prompts=json.dumps(prompts), state_dict=json.dumps(keys), cases=json.dumps(
+                  {k: {kk: vv for kk, vv in v.items()} for k, v in cases.items()})))
+
+
 def main():
     R = import_reference()
     meta = {"torch": torch.__version__, "threads": str(torch.get_num_threads()), "reference": REF}
+    if len(sys.argv) > 1 and sys.argv[1] == "sampler":
+        sampler_fixture(R, meta)
+        print("sampler", os.path.getsize(os.path.join(HERE, "sampler.safetensors")))
+        return
 
     # ---------------- micro
     oc = micro_config()
@@ -217,7 +266,8 @@ def main():
     ops["rms/w"] = nw
     ops["rms/out"] = norm(xq).detach()
     save_file({k: v.contiguous() for k, v in ops.items()}, os.path.join(HERE, "ops.safetensors"), metadata=meta_ops)
-    for f in ("jit_micro", "jit_c1", "ops"):
+    sampler_fixture(R, meta)
+    for f in ("jit_micro", "jit_c1", "ops", "sampler"):
         print(f, os.path.getsize(os.path.join(HERE, f + ".safetensors")))
 
 

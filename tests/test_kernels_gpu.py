@@ -186,8 +186,16 @@ def _attn_ref(q, k, v, bias, scale):
     return torch.einsum("bhqk,bhkd->bhqd", p, v)
 
 
-@pytest.mark.parametrize("n,n_dense,masked", [(200, 150, True), (330, 330, False), (64, 40, True), (1034, 1024, True)])
-def test_attention_fwd_bwd(ops, n, n_dense, masked):
+@pytest.fixture(params=[0, 3], ids=["4wave", "8wave"])
+def attn_variant(ops, request):
+    ops.lib.vpt_attn_set_variant(request.param)
+    yield request.param
+    ops.lib.vpt_attn_set_variant(0)
+
+
+@pytest.mark.parametrize("n,n_dense,masked", [(200, 150, True), (330, 330, False), (64, 40, True), (1034, 1024, True),
+                                              (700, 520, True)])
+def test_attention_fwd_bwd(ops, attn_variant, n, n_dense, masked):
     B, H, rows = 2, 3, ((n + 127) // 128) * 128
     D = H * 64
     qkv = rnd(B * rows, 3 * D, seed=40)

@@ -88,6 +88,14 @@ def main():
                                              ops._t4(dv, B, rows, H), B, H, rows, n, n))
             ops.lib.vpt_attn_set_variant(0)
             res.setdefault(f"attn.bwd_alg_abl{var}", []).append(2 * fl / (tv * 1e-3) / 1e12)
+        ops.lib.vpt_attn_set_variant(3)  # 8-wave blocks (A/B)
+        tf4 = timeit(lambda: ops.attn_fwd(q4, k4, v4, o4, lse, None, B, H, rows, n, n))
+        tb4 = timeit(lambda: ops.attn_bwd(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, None,
+                                          ops._t4(dq, B, rows, H), ops._t4(dk, B, rows, H), ops._t4(dv, B, rows, H),
+                                          B, H, rows, n, n))
+        ops.lib.vpt_attn_set_variant(0)
+        res.setdefault("attn.fwd_8wave", []).append(fl / (tf4 * 1e-3) / 1e12)
+        res.setdefault("attn.bwd_alg_8wave", []).append(2 * fl / (tb4 * 1e-3) / 1e12)
         res.setdefault("attn.fwd", []).append(fl / (tf * 1e-3) / 1e12)
         res.setdefault("attn.bwd_alg", []).append(2 * fl / (tb * 1e-3) / 1e12)
         res.setdefault("attn.fwd_ms", []).append(tf)

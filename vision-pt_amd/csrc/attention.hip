@@ -37,6 +37,7 @@ struct AttnArgs {
 
 constexpr float kNegInf = -__builtin_huge_valf();
 int g_variant = 0;  // backward kernel variant (vpt_attn_set_variant; 1, 2 = timing-only ablations)
+int g_waves = 4;    // waves per block (vpt_attn_set_variant 3 -> 8-wave blocks, A/B only)
 float g_tau = 8.f;  // forward lazy-rescale threshold, log2 units (vpt_attn_set_rescale_threshold)
 
 // Reductions over the lane pair (l, l^32) with v_permlane32_swap (VALU, no LDS round trip): the two
@@ -79,14 +80,15 @@ __device__ __forceinline__ void dma_x1(const void* sbase, uint32_t voff, uint32_
   asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(m0v) : "memory");
 }
-// Rows r0..r0+63 of a (b,h) slice -> the tile_off LDS image: 8 pieces of 1 KB (rows 8q..8q+7), two
-// per wave (q = 2*wid + i). The image is written lane-linearly, so position p of a row receives its
+// Rows r0..r0+63 of a (b,h) slice -> the tile_off LDS image: 8 pieces of 1 KB (rows 8q..8q+7), 8/NW
+// per wave (q = (8/NW)*wid + i). The image is written lane-linearly, so position p of a row receives its
 // logical chunk p ^ sigma(row) (sigma-swizzle moved to the source address). Rows >= n are clamped to
 // n-1: finite values the callers mask (keys: -inf bias; queries: zeroed rows).
+template <int NW>
 __device__ __forceinline__ void dma_rows(char* lds, const void* head, long sr, int r0, int n, int wid, int lane) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int q = 2 * wid + i, row = 8 * q + (lane >> 3);
+  for (int i = 0; i < 8 / NW; ++i) {
+    const int q = (8 / NW) * wid + i, row = 8 * q + (lane >> 3);
     const int c = (lane & 7) ^ sigma(row);
     const int r = min(r0 + row, n - 1);
     dma_x4(head, (uint32_t)(((long)r * sr + c * 8) * 2), lds_addr(lds + q * 1024));
@@ -97,8 +99,9 @@ __device__ __forceinline__ void dma_stat(float* lds, const void* head, int r0, i
   dma_x1(head, (uint32_t)(min(r0 + lane, n - 1) * 4), lds_addr(lds));
 }
 // Zero rows nv..63 of a staged 64x64 tile (all 8 chunks of each row).
+template <int NW>
 __device__ __forceinline__ void zero_rows(char* lds, int nv, int tid) {
-  for (int idx = tid; idx < (64 - nv) * 8; idx += 256)
+  for (int idx = tid; idx < (64 - nv) * 8; idx += 64 * NW)
     *reinterpret_cast<uint4*>(lds + (nv + (idx >> 3)) * 128 + (idx & 7) * 16) = make_uint4(0, 0, 0, 0);
 }
 
@@ -168,18 +171,23 @@ __device__ __forceinline__ void store_T(const OTensor4& t, long base_off, const 
 // Key bias for keys [kb0, round_up(n, 64)) in LDS, filled once per block: 0 below n_dense,
 // kbias[b][key] in [n_dense, n), -inf for the padding keys >= n. Dense tiles (kv0 + 64 <= n_dense)
 // never read it.
+template <int NW>
 __device__ __forceinline__ void fill_key_bias(float* kbl, const AttnArgs& g, int b, int tid) {
   const int nk = (g.n + 63) / 64 * 64 - g.kb0;
-  for (int i = tid; i < nk; i += 256) kbl[i] = key_bias(g, b, g.kb0 + i);
+  for (int i = tid; i < nk; i += 64 * NW) kbl[i] = key_bias(g, b, g.kb0 + i);
 }
 
 // ------------------------------------------------------------------ forward
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs g) {
+// NW waves per block, 32 query rows per wave: one K/V tile staged per block serves 32*NW queries.
+// Occupancy: 134 VGPRs -> 3 waves per SIMD with 4-wave blocks (forcing <= 128 VGPRs for 4 waves
+// spills inside the tile loop and measured slower: 749 vs 823 TFLOP/s).
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][8192];
   extern __shared__ __attribute__((aligned(16))) float kbl[];  // key bias of keys kb0.. (fill_key_bias)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
   const int b = blockIdx.z, hd = blockIdx.y;
-  const int q0 = blockIdx.x * 128 + wid * 32;
+  const int q0 = blockIdx.x * (32 * NW) + wid * 32;
   const bf16_t* Q = g.q.p + b * g.q.sb + hd * g.q.sh;
   const bf16_t* K = g.k.p + b * g.k.sb + hd * g.k.sh;
   const bf16_t* V = g.v.p + b * g.v.sb + hd * g.v.sh;
@@ -195,9 +203,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs g) {
   const int nt = (g.n + 63) / 64;
   const void* Ku = uniform_ptr(K);
   const void* Vu = uniform_ptr(V);
-  fill_key_bias(kbl, g, b, tid);
-  dma_rows(lds[0][0], Ku, g.k.sr, 0, g.n, wid, lane);
-  dma_rows(lds[0][1], Vu, g.v.sr, 0, g.n, wid, lane);
+  fill_key_bias<NW>(kbl, g, b, tid);
+  dma_rows<NW>(lds[0][0], Ku, g.k.sr, 0, g.n, wid, lane);
+  dma_rows<NW>(lds[0][1], Vu, g.v.sr, 0, g.n, wid, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -206,8 +214,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs g) {
     const int kv0 = t * 64;
     const bool more = t + 1 < nt;
     if (more) {  // next K/V tile by LDS-DMA into the other buffer, in flight during this tile
-      dma_rows(lds[cur ^ 1][0], Ku, g.k.sr, kv0 + 64, g.n, wid, lane);
-      dma_rows(lds[cur ^ 1][1], Vu, g.v.sr, kv0 + 64, g.n, wid, lane);
+      dma_rows<NW>(lds[cur ^ 1][0], Ku, g.k.sr, kv0 + 64, g.n, wid, lane);
+      dma_rows<NW>(lds[cur ^ 1][1], Vu, g.v.sr, kv0 + 64, g.n, wid, lane);
     }
     const char* lk = lds[cur][0];
     const char* lv = lds[cur][1];
@@ -301,13 +309,13 @@ __global__ void attn_bwd_pre_kernel(AttnArgs g, int H, long rows_total) {
 // ------------------------------------------------------------------ backward dK, dV
 // ABL (timing-only ablations, wrong results): 1 = no next-tile staging (global -> regs -> LDS) in
 // the loop, 2 = transposed fragment reads replaced by row reads.
-template <int ABL = 0>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
+template <int ABL, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][8192];     // [buf][Q / dO]
   __shared__ __attribute__((aligned(16))) float lstat[2][2][64];     // [buf][lse / delta]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
   const int b = blockIdx.z, hd = blockIdx.y;
-  const int k0 = blockIdx.x * 128 + wid * 32;
+  const int k0 = blockIdx.x * (32 * NW) + wid * 32;
   const bf16_t* Q = g.q.p + b * g.q.sb + hd * g.q.sh;
   const bf16_t* dO = g.dO.p + b * g.dO.sb + hd * g.dO.sh;
   const float* LSE = g.lse + b * g.l_sb + hd * g.l_sh;
@@ -330,8 +338,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
   const void* Eu = uniform_ptr(DEL);
   // Q / dO tiles and their lse / delta rows by LDS-DMA (waves 0 and 1 also move one stats piece each).
   auto stage = [&](int buf, int r0) {
-    dma_rows(lds[buf][0], Qu, g.q.sr, r0, g.n, wid, lane);
-    dma_rows(lds[buf][1], Du, g.dO.sr, r0, g.n, wid, lane);
+    dma_rows<NW>(lds[buf][0], Qu, g.q.sr, r0, g.n, wid, lane);
+    dma_rows<NW>(lds[buf][1], Du, g.dO.sr, r0, g.n, wid, lane);
     if (wid == 0) dma_stat(lstat[buf][0], Lu, r0, g.n, lane);
     else if (wid == 1) dma_stat(lstat[buf][1], Eu, r0, g.n, lane);
   };
@@ -341,8 +349,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (g.n - r0 < 64) {
-      zero_rows(lds[buf][0], g.n - r0, tid);
-      zero_rows(lds[buf][1], g.n - r0, tid);
+      zero_rows<NW>(lds[buf][0], g.n - r0, tid);
+      zero_rows<NW>(lds[buf][1], g.n - r0, tid);
       __syncthreads();
     }
   };
@@ -406,13 +414,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
 }
 
 // ------------------------------------------------------------------ backward dQ
-template <int ABL = 0>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs g) {
+template <int ABL, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dq_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][8192];  // [buf][K / V]
   extern __shared__ __attribute__((aligned(16))) float kbl[];   // key bias of keys kb0.. (fill_key_bias)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
   const int b = blockIdx.z, hd = blockIdx.y;
-  const int q0 = blockIdx.x * 128 + wid * 32;
+  const int q0 = blockIdx.x * (32 * NW) + wid * 32;
   const int qrow = q0 + (lane & 31);
   const bf16_t* K = g.k.p + b * g.k.sb + hd * g.k.sh;
   const bf16_t* V = g.v.p + b * g.v.sb + hd * g.v.sh;
@@ -431,9 +439,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs g) {
   const int nt = (g.n + 63) / 64;
   const void* Ku = uniform_ptr(K);
   const void* Vu = uniform_ptr(V);
-  fill_key_bias(kbl, g, b, tid);
-  dma_rows(lds[0][0], Ku, g.k.sr, 0, g.n, wid, lane);
-  dma_rows(lds[0][1], Vu, g.v.sr, 0, g.n, wid, lane);
+  fill_key_bias<NW>(kbl, g, b, tid);
+  dma_rows<NW>(lds[0][0], Ku, g.k.sr, 0, g.n, wid, lane);
+  dma_rows<NW>(lds[0][1], Vu, g.v.sr, 0, g.n, wid, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -442,8 +450,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs g) {
     const int kv0 = t * 64;
     const bool more = ABL != 1 && t + 1 < nt;
     if (more) {
-      dma_rows(lds[cur ^ 1][0], Ku, g.k.sr, kv0 + 64, g.n, wid, lane);
-      dma_rows(lds[cur ^ 1][1], Vu, g.v.sr, kv0 + 64, g.n, wid, lane);
+      dma_rows<NW>(lds[cur ^ 1][0], Ku, g.k.sr, kv0 + 64, g.n, wid, lane);
+      dma_rows<NW>(lds[cur ^ 1][1], Vu, g.v.sr, kv0 + 64, g.n, wid, lane);
     }
     const char* lk = lds[cur][0];
     const char* lv = lds[cur][1];
@@ -522,8 +530,12 @@ extern "C" int vpt_attn_fwd(const void* q, long q_sb, long q_sh, long q_sr,
   g.scale = scale; g.scale_log2 = scale * 1.4426950408889634f;
   g.tau = g_tau;
   g.kb0 = g.n_dense / 64 * 64;
-  dim3 grid((n + 127) / 128, H, B);
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), key_bias_lds_bytes(g), (hipStream_t)stream, g);
+  if (g_waves == 4)
+    hipLaunchKernelGGL(attn_fwd_kernel<4>, dim3((n + 127) / 128, H, B), dim3(256), key_bias_lds_bytes(g),
+                       (hipStream_t)stream, g);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<8>, dim3((n + 255) / 256, H, B), dim3(512), key_bias_lds_bytes(g),
+                       (hipStream_t)stream, g);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
@@ -560,18 +572,22 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
   const long rows = (long)B * H * n;
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, s, g, H, rows);
   VPT_LAUNCH_CHECK();
-  dim3 grid((n + 127) / 128, H, B);
   const size_t kbl = key_bias_lds_bytes(g);
+  const dim3 g4((n + 127) / 128, H, B), g8((n + 255) / 256, H, B);
   if (g_variant == 1) {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<1>, grid, dim3(256), 0, s, g);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<1>, grid, dim3(256), kbl, s, g);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 4>), g4, dim3(256), 0, s, g);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<1, 4>), g4, dim3(256), kbl, s, g);
   } else if (g_variant == 2) {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, grid, dim3(256), 0, s, g);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<2>, grid, dim3(256), kbl, s, g);
-  } else {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<0>, grid, dim3(256), 0, s, g);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, 4>), g4, dim3(256), 0, s, g);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<2, 4>), g4, dim3(256), kbl, s, g);
+  } else if (g_waves == 4) {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 4>), g4, dim3(256), 0, s, g);
     VPT_LAUNCH_CHECK();
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<0>, grid, dim3(256), kbl, s, g);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 4>), g4, dim3(256), kbl, s, g);
+  } else {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 8>), g8, dim3(512), 0, s, g);
+    VPT_LAUNCH_CHECK();
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 8>), g8, dim3(512), kbl, s, g);
   }
   VPT_LAUNCH_CHECK();
   return VPT_OK;
@@ -584,10 +600,12 @@ extern "C" int vpt_attn_set_rescale_threshold(float tau) {
   return VPT_OK;
 }
 
-// Benchmark hook: backward kernel variant (0 = production; 1, 2 = timing-only ablations whose
-// results are wrong: 1 = no in-loop tile staging, 2 = row reads in place of transposed reads).
+// Benchmark hook: kernel variant (0 = production: 4-wave blocks; 1, 2 = timing-only backward ablations
+// whose results are wrong: 1 = no in-loop tile staging, 2 = row reads in place of transposed reads;
+// 3 = 8-wave blocks, correct, A/B only).
 extern "C" int vpt_attn_set_variant(int v) {
-  VPT_CHECK_ARG(v >= 0 && v <= 2, "vpt_attn_set_variant: 0, 1 or 2");
-  g_variant = v;
+  VPT_CHECK_ARG(v >= 0 && v <= 3, "vpt_attn_set_variant: 0..3");
+  g_variant = v == 3 ? 0 : v;
+  g_waves = v == 3 ? 8 : 4;
   return VPT_OK;
 }

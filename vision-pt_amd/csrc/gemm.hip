@@ -41,6 +41,7 @@ struct GemmArgs {
   int k_split;          // reduction length per split slice (multiple of BK)
   long split_stride;    // elements between partial slabs (f32 outputs)
   int out_mode, act;
+  unsigned long long* dbg;  // stamp-diagnostic output (geometry 2566 only)
 };
 
 // ---- LDS images -----------------------------------------------------------------------------
@@ -430,7 +431,18 @@ using GR = Geo<256, 256, 2, 4>;
 // the stage of tile t-1, which every wave consumed by MFMAs before its previous barrier, so the
 // barriers need no lgkmcnt(0) and L_t shrinks to the ds_reads; tile t+1 is then waited for with only
 // tile t+2 younger (vmcnt(4)).
-template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false>
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+// STAMP (diagnostic build, geometry 2566): per-wave cycle sums of the K-step segments (DMA issue,
+// ds_reads, vmcnt wait, barrier Y, MFMA issue, barrier X) to g.dbg[(block*8 + wave)*8 + seg]; read the
+// shares, not the length (the stamps' lgkmcnt(0) forbids overlaps the real kernel has).
+template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false, bool STAMP = false>
 __global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g) {
   using G = GR;
   constexpr int A32 = 256 * RBK * 2, STAGE32 = 2 * A32;
@@ -484,9 +496,13 @@ __global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g) {
   if (PP && wm == 1) raw_barrier();
   raw_barrier();  // X_0
 
+  unsigned long long seg[6] = {0, 0, 0, 0, 0, 0};
   for (int kt = 0; kt < nk; ++kt) {
     const char* st = smem + (kt & (RSTAGES - 1)) * STAGE32;
+    unsigned long long t0 = 0, t1 = 0;
+    if (STAMP) t0 = stamp();
     if (!DMAC && ABL != 1 && kt + 3 < nk) issue(kt + 3);
+    if (STAMP) { t1 = stamp(); seg[0] += t1 - t0; t0 = t1; }
     bf16x8 bfr[G::NI], af[G::MI];
 #pragma unroll
     for (int j = 0; j < G::NI; ++j) bfr[j] = read_frag32<BK_, 256>(st + A32, wn * G::WC + j * 16, lane);
@@ -496,8 +512,11 @@ __global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < G::MI; ++i) af[i] = mask_k(af[i], 8 * (lane >> 4), klast);
     }
+    if (STAMP) { t1 = stamp(); seg[1] += t1 - t0; t0 = t1; }
     if (ABL != 2) wait_younger(min(DMAC ? 1 : 2, nk - 2 - kt));  // tile kt+1 (if any) landed for this wave
+    if (STAMP) { t1 = stamp(); seg[2] += t1 - t0; t0 = t1; }
     if (DMAC) bare_barrier(); else raw_barrier();                // Y_kt
+    if (STAMP) { t1 = stamp(); seg[3] += t1 - t0; t0 = t1; }
     if (DMAC && ABL != 1 && kt + 3 < nk) issue(kt + 3);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -506,7 +525,15 @@ __global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g) {
       for (int j = 0; j < G::NI; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
+    if (STAMP) { t1 = stamp(); seg[4] += t1 - t0; t0 = t1; }
     if (DMAC) bare_barrier(); else raw_barrier();  // X_kt+1
+    if (STAMP) { t1 = stamp(); seg[5] += t1 - t0; }
+  }
+  if (STAMP && lane == 0 && blockIdx.x < 256 && blockIdx.y == 0) {
+    unsigned long long* o = g.dbg + ((long)blockIdx.x * 8 + wid) * 8;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) o[i] = seg[i];
+    o[6] = nk;
   }
   if (PP && wm == 0) raw_barrier();
   __syncthreads();  // the ring is reused as epilogue staging
@@ -523,11 +550,11 @@ int launch(const GemmArgs& g, int splits, hipStream_t s) {
   return VPT_OK;
 }
 
-template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false>
+template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false, bool STAMP = false>
 int launch_ring(const GemmArgs& g, int splits, hipStream_t s) {
   constexpr int LDS = RSTAGES * 2 * 256 * RBK * 2 > GR::EPI ? RSTAGES * 2 * 256 * RBK * 2 : GR::EPI;
   const int tiles = ((g.M + 255) / 256) * ((g.N + 255) / 256);
-  hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC>), dim3(tiles, splits), dim3(512), LDS, s, g);
+  hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP>), dim3(tiles, splits), dim3(512), LDS, s, g);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
@@ -539,6 +566,7 @@ int launch_geo(const GemmArgs& g, int splits, int geo, hipStream_t s) {
   if (AK && BK_ && geo == 2563) return launch_ring<AK, BK_, true, 1>(g, splits, s);  // ablation, wrong results
   if (AK && BK_ && geo == 2564) return launch_ring<AK, BK_, true, 2>(g, splits, s);  // ablation, wrong results
   if (geo == 2565) return launch_ring<AK, BK_, true, 0, true>(g, splits, s);  // DMA in the MFMA phase
+  if (AK && BK_ && geo == 2566 && g.dbg) return launch_ring<AK, BK_, true, 0, false, true>(g, splits, s);  // stamps
   if (geo == 2562) return launch<AK, BK_, 256, 256, 2, 4>(g, splits, s);  // 2-stage BK=64 T256 (A/B only)
   return launch<AK, BK_, 128, 128, 2, 2>(g, splits, s);
 }
@@ -563,6 +591,7 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ part, long n, int
 
 // Geometry choice: the 256x256 ring when its grid (x split-K slices) fills most of the 256 CUs,
 // otherwise 128x128 (2 blocks/CU, 4x the tiles).
+unsigned long long* g_dbg = nullptr;  // vpt_gemm_set_debug
 int g_geo_override = 0;  // 0 = heuristic; 128 / 256 / 2561 / 2562 force a geometry (benchmarking)
 int pick_geo(int M, int N, int splits) {
   if (g_geo_override) return g_geo_override;
@@ -593,6 +622,7 @@ extern "C" int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* 
   g.resid = (const bf16_t*)resid; g.ldr = ldr;
   g.M = M; g.N = N; g.K = K;
   g.act = act;
+  g.dbg = g_dbg;
   hipStream_t s = (hipStream_t)stream;
   int final_mode = out_mode;
   if (splits > 1) {
@@ -629,8 +659,8 @@ extern "C" int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* 
 }
 
 extern "C" int vpt_gemm_set_geometry(int geo) {
-  VPT_CHECK_ARG(geo == 0 || geo == 128 || geo == 256 || (geo >= 2561 && geo <= 2565),
-                "vpt_gemm_set_geometry: 0, 128, 256 or 2561-2565");
+  VPT_CHECK_ARG(geo == 0 || geo == 128 || geo == 256 || (geo >= 2561 && geo <= 2566),
+                "vpt_gemm_set_geometry: 0, 128, 256 or 2561-2566");
   g_geo_override = geo;
   return VPT_OK;
 }
@@ -639,4 +669,10 @@ extern "C" long vpt_gemm_workspace_bytes(int M, int N, int K, int splits) {
   (void)K;
   if (splits <= 1) return 0;
   return (long)splits * M * N * 4;
+}
+
+// Diagnostic hook: output buffer for the stamped ring build (geometry 2566), [256 blocks][8 waves][8] u64.
+extern "C" int vpt_gemm_set_debug(unsigned long long* buf) {
+  g_dbg = buf;
+  return VPT_OK;
 }

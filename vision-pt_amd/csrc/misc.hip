@@ -89,6 +89,37 @@ __global__ void unpatchify_kernel(const bf16_t* __restrict__ patches, int B, int
   else img[i] = patches[prow * 768 + col];
 }
 
+// One Euler step of the sampler with classifier-free guidance (JiTModel.generate,
+// src/models/jit/pipeline.py:436-477): z <- z + v * (t_next - t) over the [B,3,H,W] bf16 image, v from
+// the model prediction read straight from the patch layout [(n*np), 768] (the unpatchify index map,
+// denoiser.py:828-860; positive half rows [0, B*np), negative half [B*np, 2B*np)). Every binary op
+// rounds to bf16 as the reference's bf16 tensor arithmetic does: image_to_velocity (:254-260)
+// v = bf16(bf16(x - z) / clamp(1 - t, 1e-5)), CFG (:351-357) v = bf16(vp + bf16(s * bf16(vp - vn))),
+// update bf16(z + bf16(v * dt)).
+__device__ __forceinline__ float rbf(float x) { return bf2f(f2bf(x)); }
+
+__global__ void euler_cfg_kernel(bf16_t* __restrict__ z, const bf16_t* __restrict__ pred, int B, int H, int W,
+                                 int cfg, float cfg_scale, int mode, float t, float dt) {
+  const long total = (long)B * 3 * H * W;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int x = i % W, y = (i / W) % H, c = (i / ((long)W * H)) % 3, b = i / ((long)3 * W * H);
+  const int wp = W / 16;
+  const long np_ = (long)(H / 16) * wp;
+  const long prow = b * np_ + (y / 16) * wp + (x / 16);
+  const int col = ((y % 16) * 16 + (x % 16)) * 3 + c;
+  const float zf = bf2f(z[i]);
+  const float den = fmaxf(1.f - t, 1e-5f);
+  auto to_v = [&](float p) { return mode == 0 ? rbf(rbf(p - zf) / den) : p; };
+  const float vp = to_v(bf2f(pred[prow * 768 + col]));
+  float v = vp;
+  if (cfg) {
+    const float vn = to_v(bf2f(pred[(prow + (long)B * np_) * 768 + col]));
+    v = rbf(vp + rbf(cfg_scale * rbf(vp - vn)));
+  }
+  z[i] = f2bf(zf + rbf(v * dt));
+}
+
 // Flow-matching MSE over patch-layout predictions; also writes d(loss)/d(pred) (bf16, patch layout).
 // target 0 ("image"): mse(pred, x); target 1 ("velocity"): mse((pred-z)/c, (x-z)/c), c = clamp(1-t, eps).
 __global__ __launch_bounds__(256) void loss_kernel(const bf16_t* __restrict__ pred, const unsigned short* __restrict__ img,
@@ -491,6 +522,17 @@ extern "C" int vpt_unpatchify(const void* patches, int B, int H, int W, void* im
   const long total = (long)B * 3 * H * W;
   hipLaunchKernelGGL(unpatchify_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)patches, B, H,
                      W, (bf16_t*)img, reverse);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_euler_cfg_step(void* z, const void* pred, int B, int H, int W, int cfg, float cfg_scale, int mode,
+                                  float t, float dt, void* stream) {
+  VPT_CHECK_ARG(z && pred && B > 0 && H % 16 == 0 && W % 16 == 0 && (mode == 0 || mode == 1),
+                "vpt_euler_cfg_step: bad args");
+  const long total = (long)B * 3 * H * W;
+  hipLaunchKernelGGL(euler_cfg_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream, (bf16_t*)z,
+                     (const bf16_t*)pred, B, H, W, cfg, cfg_scale, mode, t, dt);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

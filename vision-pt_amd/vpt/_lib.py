@@ -24,6 +24,7 @@ SIGNATURES: dict[str, list] = {
     "vpt_gemm_bf16": [P, L, I, P, L, I, P, L, I, I, I, P, P, L, I, I, I, P, P],
     "vpt_gemm_workspace_bytes": [I, I, I, I],
     "vpt_gemm_set_geometry": [I],
+    "vpt_gemm_set_debug": [P],
     "vpt_attn_fwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, P, L, I, I, I, I, F, P],
     "vpt_attn_bwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, P, L, L, P, L,
                      P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, F, P],
@@ -39,6 +40,7 @@ SIGNATURES: dict[str, list] = {
     "vpt_patchify": [P, I, P, P, F, U64, I, I, I, P, P],
     "vpt_unpatchify": [P, I, I, I, P, I, P],
     "vpt_loss_blocks": [],
+    "vpt_euler_cfg_step": [P, P, I, I, I, I, F, I, F, F, P],
     "vpt_flow_loss": [P, P, P, P, F, U64, I, F, I, I, I, P, P, P, P],
     "vpt_timestep_embed": [P, I, P, P],
     "vpt_assemble_tokens": [P, P, P, P, P, I, I, I, I, I, P, P],

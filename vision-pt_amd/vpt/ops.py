@@ -243,6 +243,13 @@ def unpatchify(patches, B, H, W, img, reverse=False):
     return img
 
 
+def euler_cfg_step(z, pred, B, H, W, cfg, cfg_scale, mode, t, dt):
+    """z [B,3,H,W] bf16 (in place) <- Euler step from the patch-layout prediction (see vpt_euler_cfg_step)."""
+    call("vpt_euler_cfg_step", z.data_ptr(), pred.data_ptr(), B, H, W, int(cfg), float(cfg_scale), int(mode),
+         float(t), float(dt), stream())
+    return z
+
+
 def loss_blocks() -> int:
     return lib.vpt_loss_blocks()
 
