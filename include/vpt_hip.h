@@ -39,7 +39,7 @@ const char* vpt_build_info(void);
  *   :715-719,997 (context_embedder). */
 int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* B, long ldb, int b_kmajor, void* C,
                   long ldc, int M, int N, int K, const void* bias, const void* resid, long ldr, int out_mode,
-                  int act, int splits, void* workspace, void* stream);
+                  int act, int splits, void* workspace, float alpha, void* stream);
 long vpt_gemm_workspace_bytes(int M, int N, int K, int splits);
 /* Tile geometry: 0 = automatic (default); 128 = 128x128 2-stage, 256 = 256x256 ping-pong ring,
  * 2561 = ring unstaggered, 2562 = 256x256 2-stage (benchmarking); 2563/2564 = timing-only ablations
@@ -50,20 +50,21 @@ int vpt_gemm_set_geometry(int geo);
 int vpt_gemm_set_debug(unsigned long long* buf);
 
 /* ---- flash attention, head_dim 64 ---------------------------------------------------------
- * Tensors addressed p[b*sb + h*sh + row*sr + d]. Keys < n_dense always valid; keys in
- * [n_dense, n) get kbias[b*kb_sb + key] (0 or -inf); keys >= n masked. lse/delta [b*l_sb+h*l_sh+q].
+ * Tensors addressed p[b*sb + h*sh + row*sr + d]; n query rows, nk key rows (nk = n for
+ * self-attention; SDXL cross-attention nk = context length). Keys < n_dense always valid; keys in
+ * [n_dense, nk) get kbias[b*kb_sb + key] (0 or -inf); keys >= nk masked. lse/delta [b*l_sb+h*l_sh+q].
  * Replaces src/modules/attention.py:98-159 scaled_dot_product_attention (eager SDPA with the
  * [B,H,N,N] bool mask of src/models/jit/denoiser.py:375-390) and its autograd backward. */
 int vpt_attn_fwd(const void* q, long q_sb, long q_sh, long q_sr, const void* k, long k_sb, long k_sh, long k_sr,
                  const void* v, long v_sb, long v_sh, long v_sr, void* o, long o_sb, long o_sh, long o_sr,
                  float* lse, long l_sb, long l_sh, const float* kbias, long kb_sb, int B, int H, int n,
-                 int n_dense, float scale, void* stream);
+                 int nk, int n_dense, float scale, void* stream);
 int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr, const void* k, long k_sb, long k_sh, long k_sr,
                  const void* v, long v_sb, long v_sh, long v_sr, const void* o, long o_sb, long o_sh, long o_sr,
                  const void* dO, long do_sb, long do_sh, long do_sr, const float* lse, float* delta, long l_sb,
                  long l_sh, const float* kbias, long kb_sb, void* dq, long dq_sb, long dq_sh, long dq_sr,
                  void* dk, long dk_sb, long dk_sh, long dk_sr, void* dv, long dv_sb, long dv_sh, long dv_sr,
-                 int B, int H, int n, int n_dense, float scale, void* stream);
+                 int B, int H, int n, int nk, int n_dense, float scale, void* stream);
 /* Forward lazy-rescale threshold in log2 units (default 8; 0 = rescale whenever the row max grows).
  * Test hook for the online-softmax rescale branch; process-wide. */
 int vpt_attn_set_rescale_threshold(float tau);
@@ -160,6 +161,33 @@ int vpt_radam_sf_step(void* y, const float* grad, float* z, float* v, long n, fl
                       void* stream);
 int vpt_sf_lerp(void* y, const float* z, long n, float w, void* stream);
 int vpt_sf_init(const void* y, float* z, float* v, long n, void* stream);
+
+
+/* ---- SDXL QLoRA transformer block ------------------------------------
+ * LayerNorm: nn.LayerNorm norm1/2/3 (src/models/sdxl/denoiser.py:254-256), eps 1e-5, f32 statistics;
+ * backward dx = dres + LN'(dy), per-block dw/db partials [vpt_layernorm_bwd_blocks(M)][D]. D <= 2048. */
+int vpt_layernorm_fwd(const void* x, long ldx, const void* w, const void* b, void* y, long ldy, float* mean,
+                      float* rstd, int M, int D, float eps, void* stream);
+int vpt_layernorm_bwd_blocks(int M);
+int vpt_layernorm_bwd(const void* dy, long lddy, const void* x, long ldx, const float* mean, const float* rstd,
+                      const void* w, const void* dres, long ldr, void* dx, long lddx, float* dw_part, float* db_part,
+                      int M, int D, void* stream);
+/* GeGLU (denoiser.py:174-186): out[M,F] = h * gelu_erf(gate), (h | gate) = x12[M, 2F] halves; backward
+ * writes d(h) | d(gate) into dx12 [M, 2F]; bf16 rounding of the reference's bf16 tensor graph. */
+int vpt_geglu_fwd(const void* x12, long ldx, int F, long M, void* out, void* stream);
+int vpt_geglu_bwd(const void* dy, const void* x12, long ldx, int F, long M, void* dx12, long lddx, void* stream);
+/* NF4 weights in the bitsandbytes 0.48.2 layout (quant_type nf4, blocksize 64, compress_statistics):
+ * packed uint8 [n/2] (first element in the high nibble), qabsmax uint8 [n/64], absmax2 f32 [ceil(n/64/256)],
+ * code2 f32 [256] (signed dynamic map), offset f32 [1]. Dequant -> bf16 [n] in the original [out][in]
+ * layout (replaces bnb dequantize_4bit inside Linear4bit.forward, src/modules/quant/bnb.py:37-129);
+ * quantize (quantize_4bit, load time) uses absmax_scratch f32 [n/64]. */
+int vpt_nf4_dequant(const void* packed, const void* qabsmax, const float* absmax2, const float* code2,
+                    const float* offset, long n, void* out, void* stream);
+/* Elementwise bf16: out = a + b (residual sums), out = s * a (LoRA scale gradient); n % 8 == 0. */
+int vpt_add_bf16(const void* a, const void* b, long n, void* out, void* stream);
+int vpt_scale_bf16(const void* a, long n, float s, void* out, void* stream);
+int vpt_nf4_quantize(const void* w, long n, const float* code2, void* packed, void* qabsmax, float* absmax2,
+                     float* offset, float* absmax_scratch, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,6 +1,6 @@
 """Generates the golden fixtures in tests/golden/ by running the REFERENCE (p1atdev/vision-pt at
 /root/reference) on CPU in the survey container. Only the resulting tensors are committed (no
-reference source travels). Re-run: `python tests/golden/make_golden.py [sampler]` (needs /root/reference).
+reference source travels). Re-run: `python tests/golden/make_golden.py [sampler|sdxl]` (needs /root/reference).
 
 Import recipe: SURVEY.md Appendix A (Recipe A for the denoiser/config/class encoder, Recipe B
 stubs for train/jit/arb_class_to_image.py to reach JiTModel.image_to_velocity).
@@ -15,6 +15,12 @@ Fixtures:
   ops.safetensors        timestep embedding (t = 0..9999 subsample + fractional), RoPE tables of
                          the 7 benchmark buckets (checksums + head/tail rows), tokenizer ids/masks,
                          bucket lists.
+  sdxl_block.safetensors the reference's SDXL TransformerBlock (src/models/sdxl/denoiser.py:208-280) with
+                         its 10 Linear layers wrapped by the reference LoRALinear (src/modules/peft/lora.py,
+                         rank 16, alpha 8), base weights = NF4-dequantised (oracle.sdxl_oracle, restated bnb format):
+                         dim 128, 2 heads, context_dim 96, 2 x 80 tokens, 20 context tokens. Forward output
+                         and gradients (input, context, every LoRA weight) of sum(out * dy), once in fp32
+                         with fp32 attention and once in the reference's native bf16.
   sampler.safetensors    JiTModel.generate (src/models/jit/pipeline.py:378-488) on the micro config,
                          float32 execution, class context, 4 Euler steps, 2 x 64x48: starting noise,
                          token ids/masks and the final image for four cases (CFG 2.0; no CFG; CFG 3.0
@@ -182,12 +188,86 @@ def sampler_fixture(R, meta):
                   {k: {kk: vv for kk, vv in v.items()} for k, v in cases.items()})))
 
 
+def sdxl_block_fixture(meta):
+    """Reference SDXL TransformerBlock + LoRALinear (Recipe A, sdxl variant)."""
+    import functools
+    from oracle import sdxl_oracle as SO
+
+    def load(name, path):
+        spec = importlib.util.spec_from_file_location(name, path)
+        m = importlib.util.module_from_spec(spec)
+        sys.modules[name] = m
+        spec.loader.exec_module(m)
+        return m
+
+    pkg = types.ModuleType("src.models.sdxl")
+    pkg.__path__ = [REF + "/src/models/sdxl"]
+    sys.modules["src.models.sdxl"] = pkg
+    load("src.models.sdxl.config", REF + "/src/models/sdxl/config.py")
+    den = load("src.models.sdxl.denoiser", REF + "/src/models/sdxl/denoiser.py")
+    lora = importlib.import_module("src.modules.peft.lora")
+    dim, heads, cdim, rank, alpha, B, n, nc = 128, 2, 96, 16, 8.0, 2, 80, 20
+    w = SO.make_block_weights(dim, heads, cdim, rank, seed=11)
+    nf4 = {}
+    for t in SO.LORA_TARGETS:
+        st = SO.nf4_quantize(w[f"{t}.linear.weight"])
+        nf4[t] = st
+        w[f"{t}.linear.weight"] = SO.nf4_dequantize(st)
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(B, n, dim, generator=g)
+    ctx = torch.randn(B, nc, cdim, generator=g)
+    dy = torch.randn(B, n, dim, generator=g)
+    out = {"x": x, "ctx": ctx, "dy": dy}
+    for t, st in nf4.items():
+        for k, v in st.items():
+            out[f"nf4/{t}/{k}"] = v
+    orig_sdpa = den.scaled_dot_product_attention
+    for mode in ("fp32", "bf16"):
+        dt = torch.float32 if mode == "fp32" else torch.bfloat16
+        blk = den.TransformerBlock(hidden_dim=dim, num_heads=heads, head_dim=64, context_dim=cdim)
+        for t in SO.LORA_TARGETS:
+            parent_path, last = t.rsplit(".", 1)
+            parent = blk.get_submodule(parent_path)
+            wrapped = lora.LoRALinear(lora.LoRAConfig(rank=rank, alpha=alpha, dtype="float32"),
+                                      parent.get_submodule(last))
+            setattr(parent, last, wrapped)
+        sd = blk.state_dict()
+        for k in list(sd):
+            if k.endswith(".alpha"):
+                continue
+            sd[k] = w[k].clone()
+        blk.load_state_dict(sd, strict=True)
+        blk = blk.to(dt)
+        if mode == "fp32":  # the reference casts fp32 q/k/v to bf16 inside SDPA (attention.py:113-118)
+            den.scaled_dot_product_attention = functools.partial(orig_sdpa, attention_dtype=torch.float32)
+        try:
+            xi = x.detach().clone().to(dt).requires_grad_(True)
+            ci = ctx.detach().clone().to(dt).requires_grad_(True)
+            y = blk(xi, context=ci, time_embedding=None)
+            (y.float() * dy).sum().backward()
+        finally:
+            den.scaled_dot_product_attention = orig_sdpa
+        out[f"{mode}/out"] = y.detach().float()
+        out[f"{mode}/dx"] = xi.grad.float()
+        out[f"{mode}/dctx"] = ci.grad.float()
+        for nme, prm in blk.named_parameters():
+            if "lora_" in nme and prm.grad is not None:
+                out[f"{mode}/grad/{nme}"] = prm.grad.float()
+    save_file({k: v.contiguous() for k, v in out.items()}, os.path.join(HERE, "sdxl_block.safetensors"),
+              metadata=dict(meta, dims=json.dumps(dict(dim=dim, heads=heads, context_dim=cdim, rank=rank, alpha=alpha,
+                                                       B=B, n=n, nc=nc, weight_seed=11))))
+
+
 def main():
     R = import_reference()
     meta = {"torch": torch.__version__, "threads": str(torch.get_num_threads()), "reference": REF}
     if len(sys.argv) > 1 and sys.argv[1] == "sampler":
         sampler_fixture(R, meta)
         print("sampler", os.path.getsize(os.path.join(HERE, "sampler.safetensors")))
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "sdxl":
+        sdxl_block_fixture(meta)
+        print("sdxl_block", os.path.getsize(os.path.join(HERE, "sdxl_block.safetensors")))
         return
 
     # ---------------- micro
@@ -267,7 +347,8 @@ def main():
     ops["rms/out"] = norm(xq).detach()
     save_file({k: v.contiguous() for k, v in ops.items()}, os.path.join(HERE, "ops.safetensors"), metadata=meta_ops)
     sampler_fixture(R, meta)
-    for f in ("jit_micro", "jit_c1", "ops", "sampler"):
+    sdxl_block_fixture(meta)
+    for f in ("jit_micro", "jit_c1", "ops", "sampler", "sdxl_block"):
         print(f, os.path.getsize(os.path.join(HERE, f + ".safetensors")))
 
 

@@ -132,6 +132,6 @@ def test_capi_exports_every_declared_symbol():
 def test_capi_reports_errors_without_gpu_work():
     """Argument validation happens before any launch: a bad shape returns VPT_EINVAL + message."""
     from vpt import _lib
-    rc = _lib.lib.vpt_gemm_bf16(None, 0, 1, None, 0, 1, None, 0, 0, 0, 0, None, None, 0, 0, 0, 1, None, None)
+    rc = _lib.lib.vpt_gemm_bf16(None, 0, 1, None, 0, 1, None, 0, 0, 0, 0, None, None, 0, 0, 0, 1, None, 1.0, None)
     assert rc == 1
     assert b"null operand" in _lib.lib.vpt_last_error_string()

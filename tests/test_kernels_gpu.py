@@ -241,6 +241,46 @@ def test_attention_fwd_bwd(ops, attn_variant, n, n_dense, masked):
     assert rel(unh(dv), vf.grad) < 2e-2
 
 
+@pytest.mark.parametrize("n,nk,masked", [(300, 231, False), (1000, 77, True), (64, 500, True)])
+def test_cross_attention_fwd_bwd(ops, n, nk, masked):
+    """SDXL cross-attention shape (src/models/sdxl/denoiser.py:101-171): n query rows attend to nk
+    context rows (separate tensors); optional key mask; fp32 PyTorch reference."""
+    B, H = 2, 3
+    D = H * 64
+    q = rnd(B * n, D, seed=60)
+    kv = rnd(B * nk, 2 * D, seed=61)
+    kb = torch.zeros(B, nk, device=DEV)
+    n_dense = nk
+    if masked:
+        n_dense = nk // 2
+        kb[0, nk - nk // 3:] = float("-inf")
+    o = torch.zeros(B * n, D, dtype=torch.bfloat16, device=DEV)
+    lse = torch.zeros(B, H, n, device=DEV)
+    q4 = ops._t4(q, B, n, H, 0)
+    k4 = ops._t4(kv, B, nk, H, 0)
+    v4 = ops._t4(kv, B, nk, H, D)
+    ops.attn_fwd(q4, k4, v4, ops._t4(o, B, n, H, 0), lse, kb, B, H, n, n, n_dense, nk=nk)
+
+    def heads(t, rows, c0):
+        return t[:, c0:c0 + D].float().view(B, rows, H, 64).permute(0, 2, 1, 3).contiguous()
+
+    qf = heads(q, n, 0).requires_grad_(True)
+    kf = heads(kv, nk, 0).requires_grad_(True)
+    vf = heads(kv, nk, D).requires_grad_(True)
+    ref = _attn_ref(qf, kf, vf, kb, 0.125)
+    assert rel(o.view(B, n, H, 64).permute(0, 2, 1, 3), ref) < 1e-2
+    do = rnd(B * n, D, seed=62)
+    dq = torch.zeros(B * n, D, dtype=torch.bfloat16, device=DEV)
+    dkv = torch.zeros(B * nk, 2 * D, dtype=torch.bfloat16, device=DEV)
+    delta = torch.zeros(B, H, n, device=DEV)
+    ops.attn_bwd(q4, k4, v4, ops._t4(o, B, n, H, 0), ops._t4(do, B, n, H, 0), lse, delta, kb, ops._t4(dq, B, n, H, 0),
+                 ops._t4(dkv, B, nk, H, 0), ops._t4(dkv, B, nk, H, D), B, H, n, n, n_dense, nk=nk)
+    ref.backward(do.float().view(B, n, H, 64).permute(0, 2, 1, 3))
+    assert rel(dq.view(B, n, H, 64).permute(0, 2, 1, 3), qf.grad) < 2e-2
+    assert rel(dkv[:, :D].reshape(B, nk, H, 64).permute(0, 2, 1, 3), kf.grad) < 2e-2
+    assert rel(dkv[:, D:].reshape(B, nk, H, 64).permute(0, 2, 1, 3), vf.grad) < 2e-2
+
+
 @pytest.mark.parametrize("tau", [8.0, 0.0, 64.0])
 def test_attention_fwd_rescale_branch(ops, tau):
     """Forces the online-softmax rescale branch at later tiles (guide §5.4 rule 26): query 5 meets a

@@ -4,7 +4,9 @@
 // [B,H,N,N] bool mask built at src/models/jit/denoiser.py:375-381). Instead of materialising the
 // expanded mask, keys carry an additive bias row (0 / -inf) per batch: keys < n_dense are always
 // valid (patch / image-size / time tokens), keys in [n_dense, n) read `kbias[b][key]`, keys >= n
-// are -inf. Softmax scale is 1/sqrt(64) (reference default scale=None).
+// are -inf. Softmax scale is 1/sqrt(64) (reference default scale=None). Queries (n rows) and keys
+// (nk rows) may differ: SDXL cross-attention (src/models/sdxl/denoiser.py:101-171) attends image
+// tokens to the text context.
 //
 // All products use v_mfma_f32_32x32x16_bf16 with the reduction axis chosen so that every
 // accumulator is directly the next product's operand (guide §3 "accumulator tile as operand"):
@@ -29,7 +31,7 @@ struct AttnArgs {
   OTensor4 o, dq, dk, dv;
   float* lse; const float* delta_in; float* delta_out; long l_sb, l_sh;  // [B][H][*] f32
   const float* kbias; long kb_sb;                                         // [B][*] f32
-  int n, n_dense;
+  int n, nk, n_dense;  // query rows, key rows (cross-attention: nk != n), always-valid keys
   float scale, scale_log2;
   float tau;  // forward lazy-rescale threshold
   int kb0;    // start of the key-bias LDS array: n_dense rounded down to 64 (fwd, dq)
@@ -144,7 +146,7 @@ __device__ __forceinline__ floatx16 mfma32(bf16x8 a, bf16x8 b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ float key_bias(const AttnArgs& g, int b, int key) {
-  if (key >= g.n) return kNegInf;
+  if (key >= g.nk) return kNegInf;
   if (key < g.n_dense || !g.kbias) return 0.f;
   return g.kbias[(long)b * g.kb_sb + key];
 }
@@ -173,7 +175,7 @@ __device__ __forceinline__ void store_T(const OTensor4& t, long base_off, const 
 // never read it.
 template <int NW>
 __device__ __forceinline__ void fill_key_bias(float* kbl, const AttnArgs& g, int b, int tid) {
-  const int nk = (g.n + 63) / 64 * 64 - g.kb0;
+  const int nk = (g.nk + 63) / 64 * 64 - g.kb0;
   for (int i = tid; i < nk; i += 64 * NW) kbl[i] = key_bias(g, b, g.kb0 + i);
 }
 
@@ -200,12 +202,12 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnArgs g) {
   for (int i = 0; i < 16; ++i) { oacc[0][i] = 0.f; oacc[1][i] = 0.f; }
   float m_c = kNegInf, lsum = 0.f;  // running reference max (scaled log2 units), row sum
 
-  const int nt = (g.n + 63) / 64;
+  const int nt = (g.nk + 63) / 64;
   const void* Ku = uniform_ptr(K);
   const void* Vu = uniform_ptr(V);
   fill_key_bias<NW>(kbl, g, b, tid);
-  dma_rows<NW>(lds[0][0], Ku, g.k.sr, 0, g.n, wid, lane);
-  dma_rows<NW>(lds[0][1], Vu, g.v.sr, 0, g.n, wid, lane);
+  dma_rows<NW>(lds[0][0], Ku, g.k.sr, 0, g.nk, wid, lane);
+  dma_rows<NW>(lds[0][1], Vu, g.v.sr, 0, g.nk, wid, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -214,8 +216,8 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnArgs g) {
     const int kv0 = t * 64;
     const bool more = t + 1 < nt;
     if (more) {  // next K/V tile by LDS-DMA into the other buffer, in flight during this tile
-      dma_rows<NW>(lds[cur ^ 1][0], Ku, g.k.sr, kv0 + 64, g.n, wid, lane);
-      dma_rows<NW>(lds[cur ^ 1][1], Vu, g.v.sr, kv0 + 64, g.n, wid, lane);
+      dma_rows<NW>(lds[cur ^ 1][0], Ku, g.k.sr, kv0 + 64, g.nk, wid, lane);
+      dma_rows<NW>(lds[cur ^ 1][1], Vu, g.v.sr, kv0 + 64, g.nk, wid, lane);
     }
     const char* lk = lds[cur][0];
     const char* lv = lds[cur][1];
@@ -323,8 +325,8 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
 
   const int key = k0 + (lane & 31);
   bf16x8 kf[4], vf[4];
-  load_row_frags(kf, g.k.p + b * g.k.sb + hd * g.k.sh, g.k.sr, key, g.n, lane);
-  load_row_frags(vf, g.v.p + b * g.v.sb + hd * g.v.sh, g.v.sr, key, g.n, lane);
+  load_row_frags(kf, g.k.p + b * g.k.sb + hd * g.k.sh, g.k.sr, key, g.nk, lane);
+  load_row_frags(vf, g.v.p + b * g.v.sb + hd * g.v.sh, g.v.sr, key, g.nk, lane);
   const bool kmasked = key_bias(g, b, key) == kNegInf;
 
   floatx16 dvT[2], dkT[2];
@@ -409,8 +411,8 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
     if (more) settle(cur ^ 1, (t + 1) * 64);
     if (ABL != 1) cur ^= 1;
   }
-  store_T(g.dv, (long)b * g.dv.sb + hd * g.dv.sh, dvT, 1.f, key, g.n, lane, kmasked);
-  store_T(g.dk, (long)b * g.dk.sb + hd * g.dk.sh, dkT, g.scale, key, g.n, lane, kmasked);
+  store_T(g.dv, (long)b * g.dv.sb + hd * g.dv.sh, dvT, 1.f, key, g.nk, lane, kmasked);
+  store_T(g.dk, (long)b * g.dk.sb + hd * g.dk.sh, dkT, g.scale, key, g.nk, lane, kmasked);
 }
 
 // ------------------------------------------------------------------ backward dQ
@@ -436,12 +438,12 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dq_kernel(AttnArgs g) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) { dqT[0][i] = 0.f; dqT[1][i] = 0.f; }
 
-  const int nt = (g.n + 63) / 64;
+  const int nt = (g.nk + 63) / 64;
   const void* Ku = uniform_ptr(K);
   const void* Vu = uniform_ptr(V);
   fill_key_bias<NW>(kbl, g, b, tid);
-  dma_rows<NW>(lds[0][0], Ku, g.k.sr, 0, g.n, wid, lane);
-  dma_rows<NW>(lds[0][1], Vu, g.v.sr, 0, g.n, wid, lane);
+  dma_rows<NW>(lds[0][0], Ku, g.k.sr, 0, g.nk, wid, lane);
+  dma_rows<NW>(lds[0][1], Vu, g.v.sr, 0, g.nk, wid, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -450,8 +452,8 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dq_kernel(AttnArgs g) {
     const int kv0 = t * 64;
     const bool more = ABL != 1 && t + 1 < nt;
     if (more) {
-      dma_rows<NW>(lds[cur ^ 1][0], Ku, g.k.sr, kv0 + 64, g.n, wid, lane);
-      dma_rows<NW>(lds[cur ^ 1][1], Vu, g.v.sr, kv0 + 64, g.n, wid, lane);
+      dma_rows<NW>(lds[cur ^ 1][0], Ku, g.k.sr, kv0 + 64, g.nk, wid, lane);
+      dma_rows<NW>(lds[cur ^ 1][1], Vu, g.v.sr, kv0 + 64, g.nk, wid, lane);
     }
     const char* lk = lds[cur][0];
     const char* lv = lds[cur][1];
@@ -498,11 +500,11 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dq_kernel(AttnArgs g) {
 }
 
 // Dynamic LDS of the key-bias array (fill_key_bias); n <= 32768 keeps it within 128 KB.
-size_t key_bias_lds_bytes(const AttnArgs& g) { return (size_t)((g.n + 63) / 64 * 64 - g.kb0) * sizeof(float); }
+size_t key_bias_lds_bytes(const AttnArgs& g) { return (size_t)((g.nk + 63) / 64 * 64 - g.kb0) * sizeof(float); }
 
-int check_common(int B, int H, int n) {
-  VPT_CHECK_ARG(B > 0 && H > 0 && n > 0, "attention: empty shape");
-  VPT_CHECK_ARG(n <= 32768, "attention: n <= 32768 (key-bias LDS array)");
+int check_common(int B, int H, int n, int nk) {
+  VPT_CHECK_ARG(B > 0 && H > 0 && n > 0 && nk > 0, "attention: empty shape");
+  VPT_CHECK_ARG(nk <= 32768, "attention: nk <= 32768 (key-bias LDS array)");
   return VPT_OK;
 }
 
@@ -515,8 +517,8 @@ extern "C" int vpt_attn_fwd(const void* q, long q_sb, long q_sh, long q_sr,
                             void* o, long o_sb, long o_sh, long o_sr,
                             float* lse, long l_sb, long l_sh,
                             const float* kbias, long kb_sb,
-                            int B, int H, int n, int n_dense, float scale, void* stream) {
-  int rc = check_common(B, H, n);
+                            int B, int H, int n, int nk, int n_dense, float scale, void* stream) {
+  int rc = check_common(B, H, n, nk);
   if (rc) return rc;
   VPT_CHECK_ARG(q && k && v && o && lse, "vpt_attn_fwd: null pointer");
   AttnArgs g = {};
@@ -526,7 +528,7 @@ extern "C" int vpt_attn_fwd(const void* q, long q_sb, long q_sh, long q_sr,
   g.o = {(bf16_t*)o, o_sb, o_sh, o_sr};
   g.lse = lse; g.l_sb = l_sb; g.l_sh = l_sh;
   g.kbias = kbias; g.kb_sb = kb_sb;
-  g.n = n; g.n_dense = n_dense < n ? n_dense : n;
+  g.n = n; g.nk = nk; g.n_dense = n_dense < nk ? n_dense : nk;
   g.scale = scale; g.scale_log2 = scale * 1.4426950408889634f;
   g.tau = g_tau;
   g.kb0 = g.n_dense / 64 * 64;
@@ -550,8 +552,8 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
                             void* dq, long dq_sb, long dq_sh, long dq_sr,
                             void* dk, long dk_sb, long dk_sh, long dk_sr,
                             void* dv, long dv_sb, long dv_sh, long dv_sr,
-                            int B, int H, int n, int n_dense, float scale, void* stream) {
-  int rc = check_common(B, H, n);
+                            int B, int H, int n, int nk, int n_dense, float scale, void* stream) {
+  int rc = check_common(B, H, n, nk);
   if (rc) return rc;
   VPT_CHECK_ARG(q && k && v && o && dO && lse && delta && dq && dk && dv, "vpt_attn_bwd: null pointer");
   AttnArgs g = {};
@@ -565,7 +567,7 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
   g.dv = {(bf16_t*)dv, dv_sb, dv_sh, dv_sr};
   g.lse = (float*)lse; g.delta_in = delta; g.delta_out = delta; g.l_sb = l_sb; g.l_sh = l_sh;
   g.kbias = kbias; g.kb_sb = kb_sb;
-  g.n = n; g.n_dense = n_dense < n ? n_dense : n;
+  g.n = n; g.nk = nk; g.n_dense = n_dense < nk ? n_dense : nk;
   g.scale = scale; g.scale_log2 = scale * 1.4426950408889634f;
   g.kb0 = g.n_dense / 64 * 64;
   hipStream_t s = (hipStream_t)stream;
@@ -573,19 +575,20 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, s, g, H, rows);
   VPT_LAUNCH_CHECK();
   const size_t kbl = key_bias_lds_bytes(g);
-  const dim3 g4((n + 127) / 128, H, B), g8((n + 255) / 256, H, B);
+  const dim3 g4((n + 127) / 128, H, B), g8((n + 255) / 256, H, B);  // dQ: over queries
+  const dim3 k4((nk + 127) / 128, H, B), k8((nk + 255) / 256, H, B);  // dK/dV: over keys
   if (g_variant == 1) {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 4>), g4, dim3(256), 0, s, g);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 4>), k4, dim3(256), 0, s, g);
     hipLaunchKernelGGL((attn_bwd_dq_kernel<1, 4>), g4, dim3(256), kbl, s, g);
   } else if (g_variant == 2) {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, 4>), g4, dim3(256), 0, s, g);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, 4>), k4, dim3(256), 0, s, g);
     hipLaunchKernelGGL((attn_bwd_dq_kernel<2, 4>), g4, dim3(256), kbl, s, g);
   } else if (g_waves == 4) {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 4>), g4, dim3(256), 0, s, g);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 4>), k4, dim3(256), 0, s, g);
     VPT_LAUNCH_CHECK();
     hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 4>), g4, dim3(256), kbl, s, g);
   } else {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 8>), g8, dim3(512), 0, s, g);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 8>), k8, dim3(512), 0, s, g);
     VPT_LAUNCH_CHECK();
     hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 8>), g8, dim3(512), kbl, s, g);
   }

@@ -15,6 +15,6 @@ extern "C" void vpt_set_error(const char* msg) {
 
 extern "C" const char* vpt_last_error_string(void) { return g_err; }
 
-extern "C" int vpt_abi_version(void) { return 1; }
+extern "C" int vpt_abi_version(void) { return 2; }  // 2: attention takes nk (cross-attention)
 
-extern "C" const char* vpt_build_info(void) { return "vpt_hip gfx950 (CDNA4) bf16-MFMA abi=1"; }
+extern "C" const char* vpt_build_info(void) { return "vpt_hip gfx950 (CDNA4) bf16-MFMA abi=2"; }

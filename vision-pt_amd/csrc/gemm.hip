@@ -41,6 +41,7 @@ struct GemmArgs {
   int k_split;          // reduction length per split slice (multiple of BK)
   long split_stride;    // elements between partial slabs (f32 outputs)
   int out_mode, act;
+  float alpha;              // output scale applied to the accumulator before bias (LoRA alpha / rank)
   unsigned long long* dbg;  // stamp-diagnostic output (geometry 2566 only)
 };
 
@@ -210,7 +211,8 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, floatx4 (&acc)[G::MI
         const int row = m0 + wm * G::WR + h * 64 + lr;
         if (row >= g.M || !col_ok) continue;
         floatx4 v = *reinterpret_cast<const floatx4*>(st + lr * EPI_LD + cb + colw);
-        float o[4] = {v[0] + bias4[0], v[1] + bias4[1], v[2] + bias4[2], v[3] + bias4[3]};
+        float o[4] = {v[0] * g.alpha + bias4[0], v[1] * g.alpha + bias4[1], v[2] * g.alpha + bias4[2],
+                      v[3] * g.alpha + bias4[3]};
         if (g.act == ACT_SILU) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = o[e] / (1.f + __expf(-o[e]));
@@ -604,7 +606,7 @@ int pick_geo(int M, int N, int splits) {
 extern "C" int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* B, long ldb,
                              int b_kmajor, void* C, long ldc, int M, int N, int K,
                              const void* bias, const void* resid, long ldr, int out_mode, int act,
-                             int splits, void* workspace, void* stream) {
+                             int splits, void* workspace, float alpha, void* stream) {
   VPT_CHECK_ARG(A && B && C, "vpt_gemm_bf16: null operand");
   VPT_CHECK_ARG(M > 0 && N > 0 && K > 0, "vpt_gemm_bf16: empty shape");
   VPT_CHECK_ARG(N % 4 == 0, "vpt_gemm_bf16: N%4 required");
@@ -622,12 +624,13 @@ extern "C" int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* 
   g.resid = (const bf16_t*)resid; g.ldr = ldr;
   g.M = M; g.N = N; g.K = K;
   g.act = act;
+  g.alpha = alpha;
   g.dbg = g_dbg;
   hipStream_t s = (hipStream_t)stream;
   int final_mode = out_mode;
   if (splits > 1) {
     VPT_CHECK_ARG(workspace != nullptr, "vpt_gemm_bf16: split-K needs a workspace");
-    VPT_CHECK_ARG(!bias && !resid && act == ACT_NONE, "vpt_gemm_bf16: split-K has no fused epilogue");
+    VPT_CHECK_ARG(!bias && !resid && act == ACT_NONE && alpha == 1.f, "vpt_gemm_bf16: split-K has no fused epilogue");
     VPT_CHECK_ARG(ldc == N, "vpt_gemm_bf16: split-K needs dense C");
     int per = (K + splits - 1) / splits;
     per = (per + BK - 1) / BK * BK;

@@ -120,6 +120,29 @@ __global__ void euler_cfg_kernel(bf16_t* __restrict__ z, const bf16_t* __restric
   z[i] = f2bf(zf + rbf(v * dt));
 }
 
+// out = bf16(a + b) and out = bf16(s * a) over n bf16 elements (n % 8 == 0): the residual sums and the
+// LoRA output-scale gradient of the SDXL block (bf16 tensor arithmetic of the reference).
+__global__ void add_bf16_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b, long n8,
+                                bf16_t* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n8) return;
+  float fa[8], fb[8];
+  unpack8(reinterpret_cast<const uint4*>(a)[i], fa);
+  unpack8(reinterpret_cast<const uint4*>(b)[i], fb);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) fa[e] += fb[e];
+  reinterpret_cast<uint4*>(out)[i] = pack8(fa);
+}
+__global__ void scale_bf16_kernel(const bf16_t* __restrict__ a, long n8, float s, bf16_t* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n8) return;
+  float fa[8];
+  unpack8(reinterpret_cast<const uint4*>(a)[i], fa);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) fa[e] *= s;
+  reinterpret_cast<uint4*>(out)[i] = pack8(fa);
+}
+
 // Flow-matching MSE over patch-layout predictions; also writes d(loss)/d(pred) (bf16, patch layout).
 // target 0 ("image"): mse(pred, x); target 1 ("velocity"): mse((pred-z)/c, (x-z)/c), c = clamp(1-t, eps).
 __global__ __launch_bounds__(256) void loss_kernel(const bf16_t* __restrict__ pred, const unsigned short* __restrict__ img,
@@ -533,6 +556,22 @@ extern "C" int vpt_euler_cfg_step(void* z, const void* pred, int B, int H, int W
   const long total = (long)B * 3 * H * W;
   hipLaunchKernelGGL(euler_cfg_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream, (bf16_t*)z,
                      (const bf16_t*)pred, B, H, W, cfg, cfg_scale, mode, t, dt);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_add_bf16(const void* a, const void* b, long n, void* out, void* stream) {
+  VPT_CHECK_ARG(a && b && out && n % 8 == 0, "vpt_add_bf16: n must be a multiple of 8");
+  hipLaunchKernelGGL(add_bf16_kernel, grid1(n / 8), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)a,
+                     (const bf16_t*)b, n / 8, (bf16_t*)out);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_scale_bf16(const void* a, long n, float s, void* out, void* stream) {
+  VPT_CHECK_ARG(a && out && n % 8 == 0, "vpt_scale_bf16: n must be a multiple of 8");
+  hipLaunchKernelGGL(scale_bf16_kernel, grid1(n / 8), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)a, n / 8, s,
+                     (bf16_t*)out);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

@@ -1,0 +1,356 @@
+// SDXL QLoRA transformer-block kernels for gfx950:
+//   LayerNorm fwd/bwd        nn.LayerNorm (norm1/2/3, src/models/sdxl/denoiser.py:254-256), eps 1e-5, affine
+//   GeGLU fwd/bwd            GeGLU.forward (denoiser.py:174-186): hidden * gelu(gate), exact (erf) GELU
+//   NF4 dequant / quantize   bitsandbytes 0.48.2 nf4 (src/modules/quant/bnb.py:37-129 wraps it): blocksize 64,
+//                            nested absmax (8-bit blockwise over the signed dynamic map, blocksize 256, + offset)
+// Row kernels: one wave per row, 16-B (8 x bf16) vector accesses, up to 4 chunks per lane (D <= 2048).
+#include "common.h"
+
+namespace {
+
+constexpr int MAXC = 4;  // 16-B chunks per lane: D <= 64 * 8 * 4 = 2048
+
+// ---------------------------------------------------------------- LayerNorm
+// y = (x - mean) * rstd * w + b, statistics in f32 (nn.LayerNorm runs in f32 under autocast).
+__global__ __launch_bounds__(256) void layernorm_fwd_kernel(const bf16_t* __restrict__ x, long ldx,
+                                                            const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
+                                                            bf16_t* __restrict__ y, long ldy, float* __restrict__ mean_out,
+                                                            float* __restrict__ rstd_out, int M, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nch = D >> 3;
+  float f[MAXC][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      unpack8(*reinterpret_cast<const uint4*>(x + row * ldx + c * 8), f[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += f[i][e];
+    }
+  }
+  const float mean = wave_sum(s) / (float)D;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    if (lane + 64 * i < nch) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = f[i][e] - mean;
+        ss += d * d;
+      }
+    }
+  }
+  const float r = rsqrtf(wave_sum(ss) / (float)D + eps);
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      float wf[8], bf[8], o[8];
+      unpack8(*reinterpret_cast<const uint4*>(w + c * 8), wf);
+      unpack8(*reinterpret_cast<const uint4*>(b + c * 8), bf);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (f[i][e] - mean) * r * wf[e] + bf[e];
+      *reinterpret_cast<uint4*>(y + row * ldy + c * 8) = pack8(o);
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = r;
+  }
+}
+
+// dx = dres + rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * w; per-block partials of
+// dw = sum dy * xhat and db = sum dy (reduced by vpt_reduce_rows).
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16_t* __restrict__ dy, long lddy,
+                                                            const bf16_t* __restrict__ x, long ldx,
+                                                            const float* __restrict__ mean_in,
+                                                            const float* __restrict__ rstd_in,
+                                                            const bf16_t* __restrict__ w,
+                                                            const bf16_t* __restrict__ dres, long ldr,
+                                                            bf16_t* __restrict__ dx, long lddx,
+                                                            float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                            int M, int D) {
+  __shared__ float red[4][2048];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nch = D >> 3;
+  float dwp[MAXC][8], dbp[MAXC][8], wf[MAXC][8];
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = lane + 64 * i;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dwp[i][e] = dbp[i][e] = 0.f;
+    if (c < nch) unpack8(*reinterpret_cast<const uint4*>(w + c * 8), wf[i]);
+  }
+  for (long row = (long)blockIdx.x * 4 + wid; row < M; row += (long)gridDim.x * 4) {
+    const float mu = mean_in[row], r = rstd_in[row];
+    float xh[MAXC][8], gg[MAXC][8];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        float fx[8], fd[8];
+        unpack8(*reinterpret_cast<const uint4*>(x + row * ldx + c * 8), fx);
+        unpack8(*reinterpret_cast<const uint4*>(dy + row * lddy + c * 8), fd);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          xh[i][e] = (fx[e] - mu) * r;
+          gg[i][e] = fd[e] * wf[i][e];
+          sg += gg[i][e];
+          sgx += gg[i][e] * xh[i][e];
+          dwp[i][e] += fd[e] * xh[i][e];
+          dbp[i][e] += fd[e];
+        }
+      }
+    }
+    const float mg = wave_sum(sg) / (float)D, mgx = wave_sum(sgx) / (float)D;
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        float o[8], fr[8];
+        if (dres) unpack8(*reinterpret_cast<const uint4*>(dres + row * ldr + c * 8), fr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = r * (gg[i][e] - mg - xh[i][e] * mgx);
+          o[e] = dres ? fr[e] + bf2f(f2bf(d)) : d;  // residual and norm branch grads are bf16 tensors
+        }
+        *reinterpret_cast<uint4*>(dx + row * lddx + c * 8) = pack8(o);
+      }
+    }
+  }
+  // dw then db partials, each reduced across the 4 waves through LDS
+  for (int pass = 0; pass < 2; ++pass) {
+    float* dst = pass == 0 ? dw_part : db_part;
+    if (!dst) continue;
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[wid][c * 8 + e] = pass == 0 ? dwp[i][e] : dbp[i][e];
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < D; d += 256)
+      dst[(long)blockIdx.x * D + d] = red[0][d] + red[1][d] + red[2][d] + red[3][d];
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- GeGLU
+__device__ __forceinline__ float rbf(float v) { return bf2f(f2bf(v)); }
+__device__ __forceinline__ float gelu_erf(float g) { return 0.5f * g * (1.f + erff(g * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float g) {  // d/dg gelu = cdf + g * pdf (torch GeluBackward)
+  const float cdf = 0.5f * (1.f + erff(g * 0.70710678118654752f));
+  const float pdf = __expf(-0.5f * g * g) * 0.3989422804014327f;
+  return cdf + g * pdf;
+}
+
+// out[m][j] = h * gelu(gate), h = x12[m][j], gate = x12[m][F + j] (chunk(2, -1) order), bf16 tensors:
+// out = bf16(h * bf16(gelu(gate))).
+__global__ void geglu_fwd_kernel(const bf16_t* __restrict__ x12, long ldx, int F, long M, bf16_t* __restrict__ out) {
+  const int nch = F >> 3;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= M * nch) return;
+  const long m = gid / nch;
+  const int c = gid % nch;
+  float h[8], g[8], o[8];
+  unpack8(*reinterpret_cast<const uint4*>(x12 + m * ldx + c * 8), h);
+  unpack8(*reinterpret_cast<const uint4*>(x12 + m * ldx + F + c * 8), g);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = h[e] * rbf(gelu_erf(g[e]));
+  *reinterpret_cast<uint4*>(out + m * (long)F + c * 8) = pack8(o);
+}
+
+// Autograd of the bf16 graph: dh = bf16(dy * bf16(gelu(g))), dgate = bf16(bf16(dy * h) * gelu'(g)).
+__global__ void geglu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x12, long ldx, int F, long M,
+                                 bf16_t* __restrict__ dx12, long lddx) {
+  const int nch = F >> 3;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= M * nch) return;
+  const long m = gid / nch;
+  const int c = gid % nch;
+  float d[8], h[8], g[8], oh[8], og[8];
+  unpack8(*reinterpret_cast<const uint4*>(dy + m * (long)F + c * 8), d);
+  unpack8(*reinterpret_cast<const uint4*>(x12 + m * ldx + c * 8), h);
+  unpack8(*reinterpret_cast<const uint4*>(x12 + m * ldx + F + c * 8), g);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    oh[e] = d[e] * rbf(gelu_erf(g[e]));
+    og[e] = rbf(d[e] * h[e]) * gelu_erf_grad(g[e]);
+  }
+  *reinterpret_cast<uint4*>(dx12 + m * lddx + c * 8) = pack8(oh);
+  *reinterpret_cast<uint4*>(dx12 + m * lddx + F + c * 8) = pack8(og);
+}
+
+// ---------------------------------------------------------------- NF4
+__constant__ float kNF4[16] = {-1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f,
+                               -0.28444138169288635f, -0.18477343022823334f, -0.09105003625154495f, 0.0f,
+                               0.07958029955625534f, 0.16093020141124725f, 0.24611230194568634f,
+                               0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
+                               0.7229568362236023f, 1.0f};
+
+// W[i] = NF4[code_i] * absmax[i / 64], absmax[j] = code2[qabsmax[j]] * absmax2[j / 256] + offset; one
+// thread per packed byte (two weights, the first in the high nibble); bf16 output in the original
+// [out][in] layout, ready as the k-major B operand of the GEMM.
+__global__ void nf4_dequant_kernel(const uint8_t* __restrict__ packed, const uint8_t* __restrict__ qabsmax,
+                                   const float* __restrict__ absmax2, const float* __restrict__ code2,
+                                   const float* __restrict__ offset, long nbytes, bf16_t* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nbytes) return;
+  const long blk = (2 * i) / 64;
+  const float am = code2[qabsmax[blk]] * absmax2[blk / 256] + offset[0];
+  const uint8_t p = packed[i];
+  reinterpret_cast<uint32_t*>(out)[i] = pack_bf16x2(kNF4[p >> 4] * am, kNF4[p & 15] * am);
+}
+
+// Pass 1 of quantize_4bit: per 64-block absmax (one wave per block), nearest NF4 code of w / absmax
+// (first minimum of |v - code|, as argmin), packed pairs.
+__global__ __launch_bounds__(256) void nf4_quant_kernel(const bf16_t* __restrict__ w, long nblocks,
+                                                        uint8_t* __restrict__ packed, float* __restrict__ absmax) {
+  const int lane = threadIdx.x & 63;
+  const long blk = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blk >= nblocks) return;
+  const float v = bf2f(w[blk * 64 + lane]);
+  const float am = wave_max(fabsf(v));
+  const float sv = v / fmaxf(am, 1e-30f);
+  int best = 0;
+  float bd = fabsf(sv - kNF4[0]);
+#pragma unroll
+  for (int k = 1; k < 16; ++k) {
+    const float d = fabsf(sv - kNF4[k]);
+    if (d < bd) { bd = d; best = k; }
+  }
+  const int other = __shfl_xor(best, 1, 64);
+  if ((lane & 1) == 0) packed[blk * 32 + (lane >> 1)] = (uint8_t)((best << 4) | other);
+  if (lane == 0) absmax[blk] = am;
+}
+
+// Pass 2: offset = mean(absmax) (one block, fixed-order tree), then nested 8-bit blockwise
+// quantisation of absmax - offset over the dynamic map (blocksize 256; nearest code, first minimum).
+__global__ __launch_bounds__(256) void nf4_nested_kernel(const float* __restrict__ absmax, long nblocks,
+                                                         const float* __restrict__ code2, uint8_t* __restrict__ qabsmax,
+                                                         float* __restrict__ absmax2, float* __restrict__ offset) {
+  __shared__ float red[256];
+  __shared__ float code[256];
+  __shared__ float off_s;
+  const int tid = threadIdx.x;
+  code[tid] = code2[tid];
+  float s = 0.f;
+  for (long j = tid; j < nblocks; j += 256) s += absmax[j];
+  red[tid] = s;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (tid < h) red[tid] += red[tid + h];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    off_s = red[0] / (float)nblocks;
+    offset[0] = off_s;
+  }
+  __syncthreads();
+  const float off = off_s;
+  const long nb2 = (nblocks + 255) / 256;
+  for (long b2 = 0; b2 < nb2; ++b2) {
+    const long j = b2 * 256 + tid;
+    const float a = j < nblocks ? absmax[j] - off : 0.f;
+    red[tid] = fabsf(a);
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+      if (tid < h) red[tid] = fmaxf(red[tid], red[tid + h]);
+      __syncthreads();
+    }
+    const float am2 = red[0];
+    __syncthreads();
+    if (tid == 0) absmax2[b2] = am2;
+    if (j < nblocks) {
+      const float sv = a / fmaxf(am2, 1e-30f);
+      int best = 0;
+      float bd = fabsf(sv - code[0]);
+      for (int k = 1; k < 256; ++k) {
+        const float d = fabsf(sv - code[k]);
+        if (d < bd) { bd = d; best = k; }
+      }
+      qabsmax[j] = (uint8_t)best;
+    }
+  }
+}
+
+inline dim3 grid1(long n, int threads = 256) { return dim3((unsigned)((n + threads - 1) / threads)); }
+
+}  // namespace
+
+extern "C" int vpt_layernorm_fwd(const void* x, long ldx, const void* w, const void* b, void* y, long ldy, float* mean,
+                                 float* rstd, int M, int D, float eps, void* stream) {
+  VPT_CHECK_ARG(x && w && b && y && mean && rstd, "vpt_layernorm_fwd: null pointer");
+  VPT_CHECK_ARG(D % 8 == 0 && D <= 2048 && M >= 0, "vpt_layernorm_fwd: D must be a multiple of 8, <= 2048");
+  if (M == 0) return VPT_OK;
+  hipLaunchKernelGGL(layernorm_fwd_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                     ldx, (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y, ldy, mean, rstd, M, D, eps);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_layernorm_bwd_blocks(int M) {
+  const int b = (M + 3) / 4;
+  return b < 512 ? (b < 1 ? 1 : b) : 512;
+}
+
+extern "C" int vpt_layernorm_bwd(const void* dy, long lddy, const void* x, long ldx, const float* mean,
+                                 const float* rstd, const void* w, const void* dres, long ldr, void* dx, long lddx,
+                                 float* dw_part, float* db_part, int M, int D, void* stream) {
+  VPT_CHECK_ARG(dy && x && mean && rstd && w && dx, "vpt_layernorm_bwd: null pointer");
+  VPT_CHECK_ARG(D % 8 == 0 && D <= 2048, "vpt_layernorm_bwd: D must be a multiple of 8, <= 2048");
+  if (M == 0) return VPT_OK;
+  hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(vpt_layernorm_bwd_blocks(M)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, mean, rstd, (const bf16_t*)w,
+                     (const bf16_t*)dres, ldr, (bf16_t*)dx, lddx, dw_part, db_part, M, D);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_geglu_fwd(const void* x12, long ldx, int F, long M, void* out, void* stream) {
+  VPT_CHECK_ARG(x12 && out && F % 8 == 0 && ldx % 8 == 0, "vpt_geglu_fwd: bad args");
+  if (M == 0) return VPT_OK;
+  hipLaunchKernelGGL(geglu_fwd_kernel, grid1(M * (F / 8)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x12, ldx,
+                     F, M, (bf16_t*)out);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_geglu_bwd(const void* dy, const void* x12, long ldx, int F, long M, void* dx12, long lddx,
+                             void* stream) {
+  VPT_CHECK_ARG(dy && x12 && dx12 && F % 8 == 0 && ldx % 8 == 0 && lddx % 8 == 0, "vpt_geglu_bwd: bad args");
+  if (M == 0) return VPT_OK;
+  hipLaunchKernelGGL(geglu_bwd_kernel, grid1(M * (F / 8)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+                     (const bf16_t*)x12, ldx, F, M, (bf16_t*)dx12, lddx);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_nf4_dequant(const void* packed, const void* qabsmax, const float* absmax2, const float* code2,
+                               const float* offset, long n, void* out, void* stream) {
+  VPT_CHECK_ARG(packed && qabsmax && absmax2 && code2 && offset && out && n % 64 == 0 && n > 0,
+                "vpt_nf4_dequant: n must be a positive multiple of 64");
+  hipLaunchKernelGGL(nf4_dequant_kernel, grid1(n / 2), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)packed,
+                     (const uint8_t*)qabsmax, absmax2, code2, offset, n / 2, (bf16_t*)out);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_nf4_quantize(const void* w, long n, const float* code2, void* packed, void* qabsmax, float* absmax2,
+                                float* offset, float* absmax_scratch, void* stream) {
+  VPT_CHECK_ARG(w && code2 && packed && qabsmax && absmax2 && offset && absmax_scratch && n % 64 == 0 && n > 0,
+                "vpt_nf4_quantize: n must be a positive multiple of 64");
+  const long nb = n / 64;
+  hipLaunchKernelGGL(nf4_quant_kernel, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)w, nb, (uint8_t*)packed, absmax_scratch);
+  VPT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(nf4_nested_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, absmax_scratch, nb, code2,
+                     (uint8_t*)qabsmax, absmax2, offset);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}

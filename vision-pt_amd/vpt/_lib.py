@@ -21,13 +21,13 @@ LL = C.c_longlong
 
 # name -> argtypes; restype is c_int unless listed in _RESTYPES.
 SIGNATURES: dict[str, list] = {
-    "vpt_gemm_bf16": [P, L, I, P, L, I, P, L, I, I, I, P, P, L, I, I, I, P, P],
+    "vpt_gemm_bf16": [P, L, I, P, L, I, P, L, I, I, I, P, P, L, I, I, I, P, F, P],
     "vpt_gemm_workspace_bytes": [I, I, I, I],
     "vpt_gemm_set_geometry": [I],
     "vpt_gemm_set_debug": [P],
-    "vpt_attn_fwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, P, L, I, I, I, I, F, P],
+    "vpt_attn_fwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, P, L, I, I, I, I, I, F, P],
     "vpt_attn_bwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, P, L, L, P, L,
-                     P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, F, P],
+                     P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, I, F, P],
     "vpt_attn_set_rescale_threshold": [F],
     "vpt_attn_set_variant": [I],
     "vpt_rmsnorm_fwd": [P, L, P, P, L, P, I, I, F, P],
@@ -58,6 +58,15 @@ SIGNATURES: dict[str, list] = {
     "vpt_sf_init": [P, P, P, L, P],
     "vpt_copy_rows": [P, L, I, I, I, P, L, I, I, I, P],
     "vpt_silu": [P, P, P, L, I, P],
+    "vpt_layernorm_fwd": [P, L, P, P, P, L, P, P, I, I, F, P],
+    "vpt_layernorm_bwd_blocks": [I],
+    "vpt_layernorm_bwd": [P, L, P, L, P, P, P, P, L, P, L, P, P, I, I, P],
+    "vpt_geglu_fwd": [P, L, I, L, P, P],
+    "vpt_geglu_bwd": [P, P, L, I, L, P, L, P],
+    "vpt_nf4_dequant": [P, P, P, P, P, L, P, P],
+    "vpt_nf4_quantize": [P, L, P, P, P, P, P, P, P],
+    "vpt_add_bf16": [P, P, L, P, P],
+    "vpt_scale_bf16": [P, L, F, P, P],
     "vpt_last_error_string": [],
     "vpt_abi_version": [],
     "vpt_build_info": [],
@@ -68,7 +77,7 @@ _RESTYPES = {
     "vpt_build_info": C.c_char_p,
 }
 # Entry points that return a value (size / count / string) rather than a status code.
-_VALUE_FNS = {"vpt_gemm_workspace_bytes", "vpt_rmsnorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
+_VALUE_FNS = {"vpt_gemm_workspace_bytes", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
               "vpt_colsum_blocks", "vpt_last_error_string", "vpt_abi_version", "vpt_build_info"}
 
 

@@ -70,8 +70,8 @@ def _chk(t: torch.Tensor, dtype, name: str):
 
 # ----------------------------------------------------------------------------- GEMM
 def gemm(a, a_kmajor: bool, b, b_kmajor: bool, M: int, N: int, K: int, out, *, bias=None, resid=None,
-         out_mode=OUT_BF16, act=ACT_NONE, splits=1, workspace=None):
-    """out[M,N] (=|+=) sum_k A(m,k) B(n,k) (+bias[n]) (+resid[m,n]); see csrc/gemm.hip."""
+         out_mode=OUT_BF16, act=ACT_NONE, splits=1, workspace=None, alpha=1.0):
+    """out[M,N] (=|+=) alpha * sum_k A(m,k) B(n,k) (+bias[n]) (+resid[m,n]); see csrc/gemm.hip."""
     _chk(a, BF16, "a")
     _chk(b, BF16, "b")
     _chk(out, BF16 if out_mode == OUT_BF16 else F32, "out")
@@ -85,7 +85,7 @@ def gemm(a, a_kmajor: bool, b, b_kmajor: bool, M: int, N: int, K: int, out, *, b
     def run():
         call("vpt_gemm_bf16", a.data_ptr(), a.stride(0), int(a_kmajor), b.data_ptr(), b.stride(0), int(b_kmajor),
              out.data_ptr(), out.stride(0), M, N, K, _p(bias), _p(resid), 0 if resid is None else resid.stride(0),
-             out_mode, act, splits, _p(workspace), stream())
+             out_mode, act, splits, _p(workspace), float(alpha), stream())
     pr = PROBES.get("gemm")
     if pr is None:
         run()
@@ -103,13 +103,14 @@ def linear(x, w, bias=None, resid=None, out=None, act=ACT_NONE):
     return gemm(x, True, w, True, M, N, K, out, bias=bias, resid=resid, act=act)
 
 
-def linear_dgrad(dy, w, out=None):
-    """dx = dy @ w  (dy [M,N], w [N,K]) — nn.Linear input gradient."""
+def linear_dgrad(dy, w, out=None, resid=None):
+    """dx = dy @ w (+resid) (dy [M,N], w [N,K]) — nn.Linear input gradient (resid: a second bf16 gradient
+    of the same input, summed with the reference's bf16 rounding)."""
     M, N = dy.shape
     K = w.shape[1]
     if out is None:
         out = torch.empty(M, K, dtype=BF16, device=dy.device)
-    return gemm(dy, True, w, False, M, K, N, out)
+    return gemm(dy, True, w, False, M, K, N, out, resid=resid)
 
 
 def linear_wgrad(dy, x, out, accumulate=False, splits=1, workspace=None):
@@ -210,25 +211,31 @@ def _t4(t, B: int, rows: int, H: int, col0: int = 0):
     return t.data_ptr() + col0 * t.element_size(), rows * ld, 64, ld
 
 
-def attn_fwd(q, k, v, o, lse, kbias, B, H, rows, n, n_dense, scale=0.125):
-    """q/k/v/o as (ptr, sb, sh, sr) tuples (element strides); lse [B,H,rows] f32; kbias [B,rows] f32 or None."""
+def attn_fwd(q, k, v, o, lse, kbias, B, H, rows, n, n_dense, scale=0.125, nk=None):
+    """q/k/v/o as (ptr, sb, sh, sr) tuples (element strides); lse [B,H,rows] f32; kbias [B,keys] f32 or None;
+    n query rows, nk key rows (default n; cross-attention otherwise)."""
+    nk = n if nk is None else nk
+
     def run():
         call("vpt_attn_fwd", *q, *k, *v, *o, lse.data_ptr(), lse.stride(0), lse.stride(1),
-             _p(kbias), 0 if kbias is None else kbias.stride(0), B, H, n, n_dense, scale, stream())
+             _p(kbias), 0 if kbias is None else kbias.stride(0), B, H, n, nk, n_dense, scale, stream())
     pr = PROBES.get("attn_fwd")
     if pr is None:
         return run()
-    return pr.record(4.0 * B * H * n * n * 64, run)  # QK^T + PV over all (query, key) pairs
+    return pr.record(4.0 * B * H * n * nk * 64, run)  # QK^T + PV over all (query, key) pairs
 
 
-def attn_bwd(q, k, v, o, do, lse, delta, kbias, dq, dk, dv, B, H, rows, n, n_dense, scale=0.125):
+def attn_bwd(q, k, v, o, do, lse, delta, kbias, dq, dk, dv, B, H, rows, n, n_dense, scale=0.125, nk=None):
+    nk = n if nk is None else nk
+
     def run():
         call("vpt_attn_bwd", *q, *k, *v, *o, *do, lse.data_ptr(), delta.data_ptr(), lse.stride(0), lse.stride(1),
-             _p(kbias), 0 if kbias is None else kbias.stride(0), *dq, *dk, *dv, B, H, n, n_dense, scale, stream())
+             _p(kbias), 0 if kbias is None else kbias.stride(0), *dq, *dk, *dv, B, H, n, nk, n_dense, scale,
+             stream())
     pr = PROBES.get("attn_bwd")
     if pr is None:
         return run()
-    return pr.record(8.0 * B * H * n * n * 64, run)  # dV, dP, dK, dQ products (algorithmic 2x forward)
+    return pr.record(8.0 * B * H * n * nk * 64, run)  # dV, dP, dK, dQ products (algorithmic 2x forward)
 
 
 # ----------------------------------------------------------------------------- misc
@@ -356,3 +363,67 @@ def sf_lerp(y, z, w):
 
 def sf_init(y, z, v):
     call("vpt_sf_init", y.data_ptr(), z.data_ptr(), v.data_ptr(), y.numel(), stream())
+
+
+# ----------------------------------------------------------------------------- SDXL block (a29, a30)
+def layernorm_fwd(x, w, b, out=None, mean=None, rstd=None, eps=1e-5):
+    M, D = x.shape
+    out = torch.empty(M, D, dtype=BF16, device=x.device) if out is None else out
+    mean = torch.empty(M, dtype=F32, device=x.device) if mean is None else mean
+    rstd = torch.empty(M, dtype=F32, device=x.device) if rstd is None else rstd
+    call("vpt_layernorm_fwd", x.data_ptr(), x.stride(0), w.data_ptr(), b.data_ptr(), out.data_ptr(), out.stride(0),
+         mean.data_ptr(), rstd.data_ptr(), M, D, eps, stream())
+    return out, mean, rstd
+
+
+def layernorm_bwd(dy, x, mean, rstd, w, dres=None, dx=None, dw_part=None, db_part=None):
+    """dx = dres + LayerNorm'(dy); optional per-block dw/db partials [layernorm_bwd_blocks(M), D]."""
+    M, D = x.shape
+    dx = torch.empty(M, D, dtype=BF16, device=x.device) if dx is None else dx
+    call("vpt_layernorm_bwd", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), mean.data_ptr(), rstd.data_ptr(),
+         w.data_ptr(), _p(dres), 0 if dres is None else dres.stride(0), dx.data_ptr(), dx.stride(0), _p(dw_part),
+         _p(db_part), M, D, stream())
+    return dx
+
+
+def layernorm_bwd_blocks(M: int) -> int:
+    return lib.vpt_layernorm_bwd_blocks(M)
+
+
+def geglu_fwd(x12, out=None):
+    M, F2 = x12.shape
+    out = torch.empty(M, F2 // 2, dtype=BF16, device=x12.device) if out is None else out
+    call("vpt_geglu_fwd", x12.data_ptr(), x12.stride(0), F2 // 2, M, out.data_ptr(), stream())
+    return out
+
+
+def geglu_bwd(dy, x12, dx12=None):
+    M, F2 = x12.shape
+    dx12 = torch.empty_like(x12) if dx12 is None else dx12
+    call("vpt_geglu_bwd", dy.data_ptr(), x12.data_ptr(), x12.stride(0), F2 // 2, M, dx12.data_ptr(), dx12.stride(0),
+         stream())
+    return dx12
+
+
+def add_bf16(a, b, out=None):
+    out = torch.empty_like(a) if out is None else out
+    call("vpt_add_bf16", a.data_ptr(), b.data_ptr(), a.numel(), out.data_ptr(), stream())
+    return out
+
+
+def scale_bf16(a, s, out=None):
+    out = torch.empty_like(a) if out is None else out
+    call("vpt_scale_bf16", a.data_ptr(), a.numel(), float(s), out.data_ptr(), stream())
+    return out
+
+
+def nf4_dequant(packed, qabsmax, absmax2, code2, offset, n, out):
+    call("vpt_nf4_dequant", packed.data_ptr(), qabsmax.data_ptr(), absmax2.data_ptr(), code2.data_ptr(),
+         offset.data_ptr(), n, out.data_ptr(), stream())
+    return out
+
+
+def nf4_quantize(w, code2, packed, qabsmax, absmax2, offset, scratch):
+    call("vpt_nf4_quantize", w.data_ptr(), w.numel(), code2.data_ptr(), packed.data_ptr(), qabsmax.data_ptr(),
+         absmax2.data_ptr(), offset.data_ptr(), scratch.data_ptr(), stream())
+

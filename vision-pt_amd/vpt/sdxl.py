@@ -1,0 +1,204 @@
+"""SDXL QLoRA rows of SURVEY §8(a) on the HIP kernels:
+
+a29  LoRALinearNF4: LoRALinear (src/modules/peft/lora.py:92-104) over a bitsandbytes NF4 Linear4bit
+     (src/modules/quant/bnb.py:37-129): y = bf16(bf16(x W^T + b) + bf16(s * up(down(x)))), s = alpha/rank,
+     with W dequantised from the NF4 layout by `vpt_nf4_dequant` for the GEMM. Base weight frozen; the
+     adapters train (f32 gradients).
+a30  SDXLTransformerBlock: TransformerBlock.forward (src/models/sdxl/denoiser.py:258-280) --
+     LayerNorm -> self-attention -> LayerNorm -> cross-attention to the text context -> LayerNorm ->
+     GeGLU feed-forward, residuals -- with its 10 Linear layers as LoRALinearNF4 (the QLoRA targets),
+     forward with saved activations and the backward of the reference's bf16 autograd graph (grads of
+     the input, the context and every adapter).
+"""
+
+from __future__ import annotations
+
+import torch
+
+from . import ops
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+U8 = torch.uint8
+
+
+class NF4Weight:
+    """Device-resident NF4 tensor in the bitsandbytes layout (see include/vpt_hip.h)."""
+
+    def __init__(self, packed, qabsmax, absmax2, code2, offset, shape):
+        self.packed, self.qabsmax, self.absmax2, self.code2, self.offset = packed, qabsmax, absmax2, code2, offset
+        self.shape = tuple(int(s) for s in shape)
+        self.numel = 1
+        for s in self.shape:
+            self.numel *= s
+
+    @classmethod
+    def from_state(cls, st: dict[str, torch.Tensor], device="cuda"):
+        """From {packed, qabsmax, absmax2, code2, offset, shape} (the bnb quant_state fields)."""
+        d = {k: v.to(device) for k, v in st.items() if k != "shape"}
+        return cls(d["packed"].to(U8).contiguous(), d["qabsmax"].to(U8).contiguous(), d["absmax2"].float().contiguous(),
+                   d["code2"].float().contiguous(), d["offset"].float().reshape(1).contiguous(), st["shape"].tolist())
+
+    @classmethod
+    def quantize(cls, w: torch.Tensor, code2: torch.Tensor):
+        """quantize_4bit(w, blocksize=64, compress_statistics=True, quant_type="nf4") on the device."""
+        w = w.to(BF16).contiguous()
+        n = w.numel()
+        dev = w.device
+        packed = torch.empty(n // 2, dtype=U8, device=dev)
+        qabsmax = torch.empty(n // 64, dtype=U8, device=dev)
+        absmax2 = torch.empty((n // 64 + 255) // 256, dtype=F32, device=dev)
+        offset = torch.empty(1, dtype=F32, device=dev)
+        scratch = torch.empty(n // 64, dtype=F32, device=dev)
+        code2 = code2.to(dev, F32).contiguous()
+        ops.nf4_quantize(w, code2, packed, qabsmax, absmax2, offset, scratch)
+        return cls(packed, qabsmax, absmax2, code2, offset, w.shape)
+
+    def dequantize(self, out: torch.Tensor | None = None) -> torch.Tensor:
+        if out is None:
+            out = torch.empty(self.shape, dtype=BF16, device=self.packed.device)
+        return ops.nf4_dequant(self.packed, self.qabsmax, self.absmax2, self.code2, self.offset, self.numel,
+                               out.view(self.shape))
+
+
+class LoRALinearNF4:
+    """a29. `down` [r, in], `up` [out, r] bf16 trainable (grads `g_down`, `g_up` f32); `base` NF4 [out, in]."""
+
+    def __init__(self, base: NF4Weight, bias: torch.Tensor | None, down: torch.Tensor, up: torch.Tensor,
+                 alpha: float, rank: int):
+        self.base, self.bias = base, bias
+        self.down, self.up = down.to(BF16).contiguous(), up.to(BF16).contiguous()
+        self.scale = alpha / rank
+        self.g_down = torch.zeros(self.down.shape, dtype=F32, device=self.down.device)
+        self.g_up = torch.zeros(self.up.shape, dtype=F32, device=self.up.device)
+        self._w = None
+        self._saved = None
+
+    def weight(self) -> torch.Tensor:
+        """The dequantised base weight (bf16, one scratch per layer; re-dequantised every forward)."""
+        if self._w is None:
+            self._w = torch.empty(self.base.shape, dtype=BF16, device=self.down.device)
+        return self.base.dequantize(self._w)
+
+    def forward(self, x: torch.Tensor, save: bool = True) -> torch.Tensor:
+        W = self.weight()
+        d = ops.linear(x, self.down)                                         # lora_down(x)        [M, r]
+        lo = torch.empty(x.shape[0], self.up.shape[0], dtype=BF16, device=x.device)
+        ops.gemm(d, True, self.up, True, x.shape[0], self.up.shape[0], self.up.shape[1], lo, alpha=self.scale)
+        y = ops.linear(x, W, bias=self.bias, resid=lo)                      # bf16(bf16(xW^T+b) + lora)
+        self._saved = (x, d) if save else None
+        return y
+
+    def backward(self, dy: torch.Tensor) -> torch.Tensor:
+        """Accumulates g_up, g_down; returns dx (bf16) = dy W + bf16(s dy) up down."""
+        x, d = self._saved
+        g = ops.scale_bf16(dy, self.scale)                                   # grad of (up_out * s)
+        ops.linear_wgrad(g, d, self.g_up, accumulate=True, splits=ops.wgrad_splits(*self.up.shape, x.shape[0]))
+        dd = ops.linear_dgrad(g, self.up)                                    # [M, r]
+        ops.linear_wgrad(dd, x, self.g_down, accumulate=True,
+                         splits=ops.wgrad_splits(*self.down.shape, x.shape[0]))
+        dx_lora = ops.linear_dgrad(dd, self.down)
+        return ops.linear_dgrad(dy, self.weight(), resid=dx_lora)
+
+
+TARGETS = ["attn1.to_q", "attn1.to_k", "attn1.to_v", "attn1.to_out.0", "attn2.to_q", "attn2.to_k", "attn2.to_v",
+           "attn2.to_out.0", "ff.net.0.proj", "ff.net.2"]
+
+
+class SDXLTransformerBlock:
+    """a30. Weights from a reference-named state dict: `<target>.linear.weight` given either as an NF4
+    state ({packed, qabsmax, absmax2, code2, offset, shape}) or as a dense tensor (quantised on load),
+    `<target>.linear.bias`, `<target>.lora_down.weight`, `<target>.lora_up.weight`, `norm{1,2,3}.{weight,bias}`."""
+
+    def __init__(self, dim: int, heads: int, context_dim: int, rank: int, alpha: float, sd: dict, code2=None,
+                 device="cuda", head_dim: int = 64):
+        if head_dim != 64:
+            raise NotImplementedError("attention kernels are head_dim 64 (SDXL: 64)")
+        self.dim, self.heads, self.cdim, self.rank = dim, heads, context_dim, rank
+        self.inner = heads * 64
+        self.device = device
+        self.lin = {}
+        for t in TARGETS:
+            wt = sd[f"{t}.linear.weight"]
+            if isinstance(wt, dict):
+                base = NF4Weight.from_state(wt, device)
+            else:
+                if code2 is None:
+                    raise ValueError("dense base weights need the dynamic map `code2` to quantise")
+                base = NF4Weight.quantize(wt.to(device), code2)
+            b = sd.get(f"{t}.linear.bias")
+            self.lin[t] = LoRALinearNF4(base, None if b is None else b.to(device, BF16).contiguous(),
+                                        sd[f"{t}.lora_down.weight"].to(device), sd[f"{t}.lora_up.weight"].to(device),
+                                        alpha, rank)
+        self.norm = {k: (sd[f"{k}.weight"].to(device, BF16).contiguous(), sd[f"{k}.bias"].to(device, BF16).contiguous())
+                     for k in ("norm1", "norm2", "norm3")}
+        self._st = None
+
+    def _attn_fwd(self, q, k, v, B, n, nk):
+        o = torch.empty(B * n, self.inner, dtype=BF16, device=self.device)
+        lse = torch.empty(B, self.heads, n, dtype=F32, device=self.device)
+        H = self.heads
+        ops.attn_fwd(ops._t4(q, B, n, H), ops._t4(k, B, nk, H), ops._t4(v, B, nk, H), ops._t4(o, B, n, H), lse, None,
+                     B, H, n, n, nk, nk=nk)
+        return o, lse
+
+    def _attn_bwd(self, q, k, v, o, lse, do, B, n, nk):
+        H = self.heads
+        dq = torch.empty_like(q)
+        dk = torch.empty_like(k)
+        dv = torch.empty_like(v)
+        delta = torch.empty_like(lse)
+        ops.attn_bwd(ops._t4(q, B, n, H), ops._t4(k, B, nk, H), ops._t4(v, B, nk, H), ops._t4(o, B, n, H),
+                     ops._t4(do, B, n, H), lse, delta, None, ops._t4(dq, B, n, H), ops._t4(dk, B, nk, H),
+                     ops._t4(dv, B, nk, H), B, H, n, n, nk, nk=nk)
+        return dq, dk, dv
+
+    def forward(self, x: torch.Tensor, ctx: torch.Tensor, B: int, n: int, nc: int, save: bool = True) -> torch.Tensor:
+        """x [B*n, dim] bf16, ctx [B*nc, context_dim] bf16 -> [B*n, dim] bf16 (denoiser.py:258-280)."""
+        L = self.lin
+        h1, m1, r1 = ops.layernorm_fwd(x, *self.norm["norm1"])
+        q, k, v = (L[f"attn1.to_{c}"].forward(h1, save) for c in "qkv")
+        o1, lse1 = self._attn_fwd(q, k, v, B, n, n)
+        x1 = ops.add_bf16(x, L["attn1.to_out.0"].forward(o1, save))
+        h2, m2, r2 = ops.layernorm_fwd(x1, *self.norm["norm2"])
+        q2 = L["attn2.to_q"].forward(h2, save)
+        k2 = L["attn2.to_k"].forward(ctx, save)
+        v2 = L["attn2.to_v"].forward(ctx, save)
+        o2, lse2 = self._attn_fwd(q2, k2, v2, B, n, nc)
+        x2 = ops.add_bf16(x1, L["attn2.to_out.0"].forward(o2, save))
+        h3, m3, r3 = ops.layernorm_fwd(x2, *self.norm["norm3"])
+        x12 = L["ff.net.0.proj"].forward(h3, save)
+        gg = ops.geglu_fwd(x12)
+        y = ops.add_bf16(x2, L["ff.net.2"].forward(gg, save))
+        self._st = dict(B=B, n=n, nc=nc, x=x, x1=x1, x2=x2, m=(m1, m2, m3), r=(r1, r2, r3), q=q, k=k, v=v, o1=o1,
+                        lse1=lse1, q2=q2, k2=k2, v2=v2, o2=o2, lse2=lse2, x12=x12) if save else None
+        return y
+
+    def backward(self, dy: torch.Tensor):
+        """Returns (dx, dctx); accumulates every adapter's g_down / g_up (norms and NF4 bases frozen)."""
+        st, L = self._st, self.lin
+        B, n, nc = st["B"], st["n"], st["nc"]
+        m1, m2, m3 = st["m"]
+        r1, r2, r3 = st["r"]
+        dgg = L["ff.net.2"].backward(dy)
+        dx12 = ops.geglu_bwd(dgg, st["x12"])
+        dh3 = L["ff.net.0.proj"].backward(dx12)
+        dx2 = ops.layernorm_bwd(dh3, st["x2"], m3, r3, self.norm["norm3"][0], dres=dy)
+        do2 = L["attn2.to_out.0"].backward(dx2)
+        dq2, dk2, dv2 = self._attn_bwd(st["q2"], st["k2"], st["v2"], st["o2"], st["lse2"], do2, B, n, nc)
+        dh2 = L["attn2.to_q"].backward(dq2)
+        dctx = ops.add_bf16(L["attn2.to_k"].backward(dk2), L["attn2.to_v"].backward(dv2))
+        dx1 = ops.layernorm_bwd(dh2, st["x1"], m2, r2, self.norm["norm2"][0], dres=dx2)
+        do1 = L["attn1.to_out.0"].backward(dx1)
+        dq, dk, dv = self._attn_bwd(st["q"], st["k"], st["v"], st["o1"], st["lse1"], do1, B, n, n)
+        dh1 = ops.add_bf16(ops.add_bf16(L["attn1.to_q"].backward(dq), L["attn1.to_k"].backward(dk)),
+                           L["attn1.to_v"].backward(dv))
+        dx = ops.layernorm_bwd(dh1, st["x"], m1, r1, self.norm["norm1"][0], dres=dx1)
+        return dx, dctx
+
+    def lora_grads(self) -> dict[str, torch.Tensor]:
+        out = {}
+        for t, l in self.lin.items():
+            out[f"{t}.lora_down.weight"] = l.g_down
+            out[f"{t}.lora_up.weight"] = l.g_up
+        return out
