@@ -104,8 +104,10 @@ def test_nf4_quantize_matches_oracle(ops):
     assert ((SO.nf4_absmax(mine) - am_ref).abs() <= 1e-5 * am_ref.abs().max()).all()
     assert abs(q.offset.item() - ref["offset"].item()) < 1e-6 * abs(ref["offset"].item()) + 1e-9
     assert torch.allclose(q.absmax2.cpu(), ref["absmax2"], rtol=1e-5)
+    # dequantize() emits bf16 (what the GEMM consumes): compare with the oracle rounded the same way;
+    # the only remaining differences come from the ~1e-5 absmax deviations above flipping a rounding
     deq = q.dequantize().float().cpu()
-    assert rel(deq, SO.nf4_dequantize(ref)) < 1e-3
+    assert rel(deq, SO.nf4_dequantize(ref).bfloat16().float()) < 1e-3
 
 
 def _block_inputs():
