@@ -53,6 +53,11 @@ int vpt_gemm_set_debug(unsigned long long* buf);
  * Tensors addressed p[b*sb + h*sh + row*sr + d]; n query rows, nk key rows (nk = n for
  * self-attention; SDXL cross-attention nk = context length). Keys < n_dense always valid; keys in
  * [n_dense, nk) get kbias[b*kb_sb + key] (0 or -inf); keys >= nk masked. lse/delta [b*l_sb+h*l_sh+q].
+ * q must be PRE-SCALED by scale*log2(e) (vpt_qknorm_rope_fwd q_scale, or any bf16 scaling); k, v are
+ * raw. The forward writes lse = -log2(sum_k exp(scale*q.k)) (negated, log2 units) for the backward;
+ * delta is backward workspace. dq, dk, dv are gradients w.r.t. the UNSCALED q, k, v. */
+float vpt_attn_q_scale(float scale);
+/* Attention entry points:
  * Replaces src/modules/attention.py:98-159 scaled_dot_product_attention (eager SDPA with the
  * [B,H,N,N] bool mask of src/models/jit/denoiser.py:375-390) and its autograd backward. */
 int vpt_attn_fwd(const void* q, long q_sb, long q_sh, long q_sr, const void* k, long k_sb, long k_sh, long k_sr,
@@ -88,9 +93,11 @@ int vpt_rmsnorm_bwd(const void* dy, long lddy, const void* x, long ldx, const fl
  * Replaces Attention.q_norm/k_norm + apply_rope, src/models/jit/denoiser.py:307-316,369-373,98-111
  * (cos/sin tables [rows_per_seq][32] f32 replace the per-forward host RoPE gather 1013-1051). */
 int vpt_qknorm_rope_blocks(int M);
+/* q_scale multiplies the q half of the output before its bf16 rounding: the engine passes
+ * vpt_attn_q_scale(1/sqrt(64)) so the result feeds vpt_attn_fwd/bwd directly (k is unscaled). */
 int vpt_qknorm_rope_fwd(const void* qkv, long ldin, const void* wq, const void* wk, const float* cos_t,
                         const float* sin_t, void* out, long ldout, int M, int rows_per_seq, int D, float eps,
-                        void* stream);
+                        float q_scale, void* stream);
 int vpt_qknorm_rope_bwd(const void* dqk, long lddqk, const void* qkv, long ldin, const void* wq, const void* wk,
                         const float* cos_t, const float* sin_t, void* dqkv, long lddqkv, float* dw_part, int M,
                         int rows_per_seq, int D, float eps, void* stream);

@@ -179,6 +179,13 @@ def test_qknorm_rope_fwd_bwd(ops):
 
 
 # ------------------------------------------------------------------------------------ attention
+def prescale_q(ops, t, D, scale=0.125):
+    """Copy of t whose first D columns (q) carry the attention kernels' pre-scale (include/vpt_hip.h)."""
+    t = t.clone()
+    t[:, :D] = (t[:, :D].float() * ops.attn_q_scale(scale)).bfloat16()
+    return t
+
+
 def _attn_ref(q, k, v, bias, scale):
     # q,k,v [B,H,N,64] f32; bias [B,N] additive
     s = torch.einsum("bhqd,bhkd->bhqk", q, k) * scale + bias[:, None, None, :]
@@ -205,9 +212,10 @@ def test_attention_fwd_bwd(ops, attn_variant, n, n_dense, masked):
         kb[1, n_dense:] = 0.0  # second sequence: nothing masked
     o = torch.zeros(B * rows, D, dtype=torch.bfloat16, device=DEV)
     lse = torch.zeros(B, H, rows, device=DEV)
-    q4 = ops._t4(qkv, B, rows, H, 0)
-    k4 = ops._t4(qkv, B, rows, H, D)
-    v4 = ops._t4(qkv, B, rows, H, 2 * D)
+    qkv_s = prescale_q(ops, qkv, D)
+    q4 = ops._t4(qkv_s, B, rows, H, 0)
+    k4 = ops._t4(qkv_s, B, rows, H, D)
+    v4 = ops._t4(qkv_s, B, rows, H, 2 * D)
     o4 = ops._t4(o, B, rows, H, 0)
     ops.attn_fwd(q4, k4, v4, o4, lse, kb, B, H, rows, n, n_dense)
 
@@ -256,7 +264,8 @@ def test_cross_attention_fwd_bwd(ops, n, nk, masked):
         kb[0, nk - nk // 3:] = float("-inf")
     o = torch.zeros(B * n, D, dtype=torch.bfloat16, device=DEV)
     lse = torch.zeros(B, H, n, device=DEV)
-    q4 = ops._t4(q, B, n, H, 0)
+    q_s = prescale_q(ops, q, D)  # kept alive: _t4 holds a raw pointer
+    q4 = ops._t4(q_s, B, n, H, 0)
     k4 = ops._t4(kv, B, nk, H, 0)
     v4 = ops._t4(kv, B, nk, H, D)
     ops.attn_fwd(q4, k4, v4, ops._t4(o, B, n, H, 0), lse, kb, B, H, n, n, n_dense, nk=nk)
@@ -297,7 +306,8 @@ def test_attention_fwd_rescale_branch(ops, tau):
     qkv[130, D:D + 64] = (1.2 * u).bfloat16()    # ~+4.8 -> 7 log2 units
     o = torch.zeros(B * rows, D, dtype=torch.bfloat16, device=DEV)
     lse = torch.zeros(B, H, rows, device=DEV)
-    q4, k4, v4 = (ops._t4(qkv, B, rows, H, c) for c in (0, D, 2 * D))
+    qkv_s = prescale_q(ops, qkv, D)
+    q4, k4, v4 = (ops._t4(qkv_s, B, rows, H, c) for c in (0, D, 2 * D))
     ops.lib.vpt_attn_set_rescale_threshold(tau)
     try:
         ops.attn_fwd(q4, k4, v4, ops._t4(o, B, rows, H, 0), lse, None, B, H, rows, n, n)
@@ -305,15 +315,16 @@ def test_attention_fwd_rescale_branch(ops, tau):
         ops.lib.vpt_attn_set_rescale_threshold(8.0)
 
     def heads(c0):
-        return qkv[:, c0:c0 + D].double().view(B, rows, H, 64)[:, :n].permute(0, 2, 1, 3)
+        return qkv_s[:, c0:c0 + D].double().view(B, rows, H, 64)[:, :n].permute(0, 2, 1, 3)
 
-    s = torch.einsum("bhqd,bhkd->bhqk", heads(0), heads(D)) * 0.125
+    # reference on the kernel's own (pre-scaled, log2-unit) logits, so the lse bar checks arithmetic only
+    s = torch.einsum("bhqd,bhkd->bhqk", heads(0), heads(D)) * math.log(2.0)
     ref = torch.einsum("bhqk,bhkd->bhqd", torch.softmax(s, -1), heads(2 * D))
     got = o.view(B, rows, H, 64)[:, :n].permute(0, 2, 1, 3).double()
     assert rel(got, ref) < 1e-2
     assert (got[0, :, 5] - ref[0, :, 5]).abs().max() < 2e-2
     ref_lse = torch.logsumexp(s, -1) / math.log(2.0)
-    assert (lse[:, :, :n].double() - ref_lse).abs().max() < 1e-3
+    assert (-lse[:, :, :n].double() - ref_lse).abs().max() < 1e-3  # the kernel stores -LSE (log2)
 
 
 # ------------------------------------------------------------------------------------ misc

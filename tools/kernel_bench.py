@@ -34,6 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--M", type=int, default=8 * 4170)
+    ap.add_argument("--attn-only", action="store_true")
     args = ap.parse_args()
     dev = "cuda"
     M = args.M
@@ -41,7 +42,7 @@ def main():
     res = {}
     ws = torch.empty(64 * 4096 * 2048, dtype=torch.float32, device=dev)
     for r in range(args.rounds):
-        for name, (N, K) in shapes.items():
+        for name, (N, K) in ({} if args.attn_only else shapes).items():
             x = (torch.randn(M, K, device=dev) * 0.5).bfloat16()
             w = (torch.randn(N, K, device=dev) * 0.05).bfloat16()
             dy = (torch.randn(M, N, device=dev) * 0.5).bfloat16()

@@ -15,6 +15,12 @@
 //   dQ      : S^T = K.Q^T, dP^T = V.dO^T, dQ^T += K^T.dS^T
 // Row tiles [64][64] bf16 live in LDS with one XOR swizzle (sigma) that is conflict-free for both
 // ds_read_b128 row reads and ds_read_b64_tr_b16 transposed reads.
+//
+// VALU diet (the softmax, not the MFMA, bounds head_dim 64): the caller passes the query pre-scaled by
+// c = scale*log2(e) (vpt_qknorm_rope_fwd's q_scale), so every S product is in log2 units; the row
+// constants (-m in the forward, -LSE and -delta in the backward, stored negated) are the MFMA chains'
+// initial accumulators. Per score that leaves exp2 (+ row-sum add / max) in the forward and exp2 + one
+// multiply in the backward.
 #include "common.h"
 
 namespace {
@@ -145,6 +151,24 @@ __device__ __forceinline__ bf16x8 pack_acc(const floatx16& a, int s) {
 __device__ __forceinline__ floatx16 mfma32(bf16x8 a, bf16x8 b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ floatx16 splat16(float v) {
+  floatx16 r;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) r[i] = v;
+  return r;
+}
+// Accumulator-layout tile of 16 per-row constants from an LDS row vector: register 4*g4+e of lane
+// holds row 8*g4 + 4*(lane>>5) + e (v_mfma_f32_32x32x16 D layout), rows offset by r0.
+__device__ __forceinline__ floatx16 rows16(const float* v, int r0, int h) {
+  floatx16 r;
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const floatx4 x = *reinterpret_cast<const floatx4*>(v + r0 + 8 * g4 + 4 * h);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[4 * g4 + e] = x[e];
+  }
+  return r;
+}
 __device__ __forceinline__ float key_bias(const AttnArgs& g, int b, int key) {
   if (key >= g.nk) return kNegInf;
   if (key < g.n_dense || !g.kbias) return 0.f;
@@ -194,13 +218,14 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnArgs g) {
   const bf16_t* K = g.k.p + b * g.k.sb + hd * g.k.sh;
   const bf16_t* V = g.v.p + b * g.v.sb + hd * g.v.sh;
 
-  bf16x8 qf[4];
+  bf16x8 qf[4];  // pre-scaled query: K.Q^T is already in log2 units
   load_row_frags(qf, Q, g.q.sr, q0 + (lane & 31), g.n, lane);
 
   floatx16 oacc[2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) { oacc[0][i] = 0.f; oacc[1][i] = 0.f; }
-  float m_c = kNegInf, lsum = 0.f;  // running reference max (scaled log2 units), row sum
+  float m_c = 0.f, lsum = 0.f;  // running reference point (log2 units), row sum
+  floatx16 nm = splat16(0.f);   // -m_c: the S^T chain's initial accumulator, so it ends at S - m_c
 
   const int nt = (g.nk + 63) / 64;
   const void* Ku = uniform_ptr(K);
@@ -221,15 +246,14 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnArgs g) {
     }
     const char* lk = lds[cur][0];
     const char* lv = lds[cur][1];
-    floatx16 sacc[2];
+    floatx16 sacc[2];  // S^T - m_c (log2 units) straight out of the MFMA chain
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
-      sacc[kb] = mfma32(frag_rows(lk, 32 * kb, 0, lane), qf[0], floatx16{});
+      sacc[kb] = mfma32(frag_rows(lk, 32 * kb, 0, lane), qf[0], nm);
 #pragma unroll
       for (int s = 1; s < 4; ++s) sacc[kb] = mfma32(frag_rows(lk, 32 * kb, s, lane), qf[s], sacc[kb]);
     }
-    // Raw-score max (the scale is positive, so max(s)*c = max(s*c)); key bias is 0 / -inf.
-    if (kv0 + 64 > g.n_dense) {
+    if (kv0 + 64 > g.n_dense) {  // key bias 0 / -inf (context and padding tiles only)
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -244,24 +268,31 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnArgs g) {
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[kb][i]);
-    const float mx_c = pair_max(mx) * g.scale_log2;
-    // Lazy rescale: the reference point m_c only moves when this tile's max exceeds it by more
-    // than tau (p <= 2^tau otherwise); wave-uniform branch, taken on the first tile and rarely after.
-    const bool up = mx_c > m_c + g.tau;
+    mx = pair_max(mx);
+    // Lazy rescale: the reference point m_c moves only on the first tile and when a tile's max
+    // exceeds it by more than tau (p <= 2^tau otherwise); wave-uniform branch, rarely taken after t=0.
+    const bool up = t == 0 || mx > g.tau;
     if (__builtin_amdgcn_ballot_w64(up)) {
-      const float m_new = up ? mx_c : m_c;
-      const float alpha = up ? __builtin_amdgcn_exp2f(m_c - m_new) : 1.f;
-      lsum *= alpha;
+      const float sh = up && mx != kNegInf ? mx : 0.f;  // shift of the reference point
+      if (t > 0) {
+        const float alpha = __builtin_amdgcn_exp2f(-sh);
+        lsum *= alpha;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
-      m_c = m_new;
+        for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
+      }
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[kb][i] -= sh;
+      m_c += sh;
+      nm = splat16(-m_c);
     }
     float ps = 0.f;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kb][i], g.scale_log2, -m_c));
+        const float p = __builtin_amdgcn_exp2f(sacc[kb][i]);
         sacc[kb][i] = p;
         ps += p;
       }
@@ -282,11 +313,12 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnArgs g) {
   const float inv = 1.f / l;
   const int qrow = q0 + (lane & 31);
   store_T(g.o, (long)b * g.o.sb + hd * g.o.sh, oacc, inv, qrow, g.n, lane, false);
-  if (lane < 32 && qrow < g.n) g.lse[b * g.l_sb + hd * g.l_sh + qrow] = m_c + __log2f(l);
+  if (lane < 32 && qrow < g.n) g.lse[b * g.l_sb + hd * g.l_sh + qrow] = -(m_c + __log2f(l));  // -LSE, log2
 }
 
 // ------------------------------------------------------------------ backward preprocess
-// delta[b,h,q] = sum_d dO[q,d] * O[q,d]; 8 lanes per (b,h,q) row.
+// delta[b,h,q] = -sum_d dO[q,d] * O[q,d] (stored negated: it is the dP chains' initial accumulator);
+// 8 lanes per (b,h,q) row.
 __global__ void attn_bwd_pre_kernel(AttnArgs g, int H, long rows_total) {
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long row = gid >> 3;
@@ -305,7 +337,7 @@ __global__ void attn_bwd_pre_kernel(AttnArgs g, int H, long rows_total) {
   s += __shfl_xor(s, 1, 64);
   s += __shfl_xor(s, 2, 64);
   s += __shfl_xor(s, 4, 64);
-  if (row < rows_total && part == 0) g.delta_out[b * g.l_sb + hd * g.l_sh + q] = s;
+  if (row < rows_total && part == 0) g.delta_out[b * g.l_sb + hd * g.l_sh + q] = -s;
 }
 
 // ------------------------------------------------------------------ backward dK, dV
@@ -368,27 +400,21 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
     floatx16 P[2], dS[2];
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
-      floatx16 s, dp;
-      s = mfma32(frag_rows(lq, 32 * qb, 0, lane), kf[0], floatx16{});  // zero C: inline constant
-      dp = mfma32(frag_rows(ld, 32 * qb, 0, lane), vf[0], floatx16{});
+      // Row constants as the initial accumulators (guide App. B): S' = Q~.K^T - LSE (Q~ pre-scaled, so
+      // log2 units) and dP' = dO.V^T - delta leave the chains ready for p = exp2(S'), dS = p * dP'.
+      floatx16 s = rows16(lstat[cur][0], 32 * qb, h), dp = rows16(lstat[cur][1], 32 * qb, h);
 #pragma unroll
-      for (int ks = 1; ks < 4; ++ks) {
+      for (int ks = 0; ks < 4; ++ks) {
         s = mfma32(frag_rows(lq, 32 * qb, ks, lane), kf[ks], s);
         dp = mfma32(frag_rows(ld, 32 * qb, ks, lane), vf[ks], dp);
       }
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int qi = 32 * qb + 8 * g4 + 4 * h;
-        const floatx4 l4 = *reinterpret_cast<const floatx4*>(&lstat[cur][0][qi]);
-        const floatx4 d4 = *reinterpret_cast<const floatx4*>(&lstat[cur][1][qi]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          // No key bias here: a masked key (bias -inf) only feeds its own lane's dK/dV columns, which
-          // are stored as exact zeros below, so one FMA + exp2 per score.
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[4 * g4 + e], g.scale_log2, -l4[e]));
-          P[qb][4 * g4 + e] = p;
-          dS[qb][4 * g4 + e] = p * (dp[4 * g4 + e] - d4[e]);
-        }
+      for (int i = 0; i < 16; ++i) {
+        // No key bias here: a masked key (bias -inf) only feeds its own lane's dK/dV columns, which
+        // are stored as exact zeros below.
+        const float p = __builtin_amdgcn_exp2f(s[i]);
+        P[qb][i] = p;
+        dS[qb][i] = p * dp[i];
       }
     }
 #pragma unroll
@@ -412,7 +438,8 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
     if (ABL != 1) cur ^= 1;
   }
   store_T(g.dv, (long)b * g.dv.sb + hd * g.dv.sh, dvT, 1.f, key, g.nk, lane, kmasked);
-  store_T(g.dk, (long)b * g.dk.sb + hd * g.dk.sh, dkT, g.scale, key, g.nk, lane, kmasked);
+  // dK = scale * dS^T.Q = (scale / c) * dS^T.Q~ with Q~ = c*Q, c = scale*log2(e): the factor is ln 2
+  store_T(g.dk, (long)b * g.dk.sb + hd * g.dk.sh, dkT, 0.69314718055994531f, key, g.nk, lane, kmasked);
 }
 
 // ------------------------------------------------------------------ backward dQ
@@ -431,8 +458,9 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dq_kernel(AttnArgs g) {
   load_row_frags(qf, g.q.p + b * g.q.sb + hd * g.q.sh, g.q.sr, qrow, g.n, lane);
   load_row_frags(df, g.dO.p + b * g.dO.sb + hd * g.dO.sh, g.dO.sr, qrow, g.n, lane);
   const long lo = b * g.l_sb + hd * g.l_sh + qrow;
-  const float lse = qrow < g.n ? g.lse[lo] : __builtin_huge_valf();
-  const float del = qrow < g.n ? g.delta_in[lo] : 0.f;
+  // -LSE and -delta of the lane's query as the S^T / dP^T chains' initial accumulators
+  const floatx16 nlse = splat16(qrow < g.n ? g.lse[lo] : -__builtin_huge_valf());
+  const floatx16 ndel = splat16(qrow < g.n ? g.delta_in[lo] : 0.f);
 
   floatx16 dqT[2];
 #pragma unroll
@@ -461,16 +489,12 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dq_kernel(AttnArgs g) {
     floatx16 dS[2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
-      floatx16 s, dp;
-      s = mfma32(frag_rows(lk, 32 * kb, 0, lane), qf[0], floatx16{});
-      dp = mfma32(frag_rows(lv, 32 * kb, 0, lane), df[0], floatx16{});
+      floatx16 s = nlse, dp = ndel;
 #pragma unroll
-      for (int ks = 1; ks < 4; ++ks) {
+      for (int ks = 0; ks < 4; ++ks) {
         s = mfma32(frag_rows(lk, 32 * kb, ks, lane), qf[ks], s);
         dp = mfma32(frag_rows(lv, 32 * kb, ks, lane), df[ks], dp);
       }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) s[i] = __builtin_fmaf(s[i], g.scale_log2, -lse);
       if (!dense) {  // scalar branch: only the context / padding key tiles carry a bias
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
@@ -480,7 +504,7 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dq_kernel(AttnArgs g) {
         }
       }
 #pragma unroll
-      for (int i = 0; i < 16; ++i) dS[kb][i] = __builtin_amdgcn_exp2f(s[i]) * (dp[i] - del);
+      for (int i = 0; i < 16; ++i) dS[kb][i] = __builtin_amdgcn_exp2f(s[i]) * dp[i];
     }
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
@@ -509,6 +533,9 @@ int check_common(int B, int H, int n, int nk) {
 }
 
 }  // namespace
+
+// The factor the caller applies to q before vpt_attn_fwd / vpt_attn_bwd.
+extern "C" float vpt_attn_q_scale(float scale) { return scale * 1.4426950408889634f; }
 
 // Strides are in elements; every tensor is addressed as p[b*sb + h*sh + row*sr + d], d in [0,64).
 extern "C" int vpt_attn_fwd(const void* q, long q_sb, long q_sh, long q_sr,

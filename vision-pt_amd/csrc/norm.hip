@@ -162,10 +162,11 @@ __global__ __launch_bounds__(256) void qknorm_rope_fwd_kernel(const bf16_t* __re
                                                               const bf16_t* __restrict__ wq, const bf16_t* __restrict__ wk,
                                                               const float* __restrict__ cs, const float* __restrict__ sn,
                                                               bf16_t* __restrict__ out, long ldout, int M,
-                                                              int rows_per_seq, int D, float eps) {
+                                                              int rows_per_seq, int D, float eps, float q_scale) {
   const int sub = threadIdx.x, per = D >> 3;   // blockDim = 2 * D / 8
   const int which = sub / per, head = (sub % per) >> 3, part = sub & 7;
   const bf16_t* w = which ? wk : wq;
+  const float osc = which ? 1.f : q_scale;  // q leaves pre-multiplied (one rounding) for the attention kernels
   float wf[8];
   unpack8(*reinterpret_cast<const uint4*>(w + part * 8), wf);
   for (long row = blockIdx.x; row < M; row += gridDim.x) {
@@ -186,8 +187,8 @@ __global__ __launch_bounds__(256) void qknorm_rope_fwd_kernel(const bf16_t* __re
     for (int i = 0; i < 4; ++i) {
       const float a = bf2f(f2bf((f[2 * i] * r) * wf[2 * i]));
       const float b = bf2f(f2bf((f[2 * i + 1] * r) * wf[2 * i + 1]));
-      o[2 * i] = a * c[i] - b * s[i];
-      o[2 * i + 1] = a * s[i] + b * c[i];
+      o[2 * i] = (a * c[i] - b * s[i]) * osc;
+      o[2 * i + 1] = (a * s[i] + b * c[i]) * osc;
     }
     *reinterpret_cast<uint4*>(out + row * ldout + which * D + head * 64 + part * 8) = pack8(o);
   }
@@ -320,13 +321,13 @@ extern "C" int vpt_qknorm_rope_blocks(int M) { return M < 1024 ? (M < 1 ? 1 : M)
 
 extern "C" int vpt_qknorm_rope_fwd(const void* qkv, long ldin, const void* wq, const void* wk, const float* cos_t,
                                    const float* sin_t, void* out, long ldout, int M, int rows_per_seq, int D,
-                                   float eps, void* stream) {
+                                   float eps, float q_scale, void* stream) {
   VPT_CHECK_ARG(qkv && wq && wk && cos_t && sin_t && out, "vpt_qknorm_rope_fwd: null pointer");
   VPT_CHECK_ARG(D % 64 == 0 && D <= 1024, "vpt_qknorm_rope_fwd: heads x 64 with D <= 1024");
   if (M == 0) return VPT_OK;
   hipLaunchKernelGGL(qknorm_rope_fwd_kernel, dim3(M < 8192 ? M : 8192), dim3(D / 4), 0, (hipStream_t)stream,
                      (const bf16_t*)qkv, ldin, (const bf16_t*)wq, (const bf16_t*)wk, cos_t, sin_t, (bf16_t*)out, ldout,
-                     M, rows_per_seq, D, eps);
+                     M, rows_per_seq, D, eps, q_scale);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

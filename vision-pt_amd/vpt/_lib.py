@@ -30,11 +30,12 @@ SIGNATURES: dict[str, list] = {
                      P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, I, F, P],
     "vpt_attn_set_rescale_threshold": [F],
     "vpt_attn_set_variant": [I],
+    "vpt_attn_q_scale": [F],
     "vpt_rmsnorm_fwd": [P, L, P, P, L, P, I, I, F, P],
     "vpt_rmsnorm_bwd_blocks": [I],
     "vpt_rmsnorm_bwd": [P, L, P, L, P, P, P, L, P, L, P, I, I, P],
     "vpt_qknorm_rope_blocks": [I],
-    "vpt_qknorm_rope_fwd": [P, L, P, P, P, P, P, L, I, I, I, F, P],
+    "vpt_qknorm_rope_fwd": [P, L, P, P, P, P, P, L, I, I, I, F, F, P],
     "vpt_qknorm_rope_bwd": [P, L, P, L, P, P, P, P, P, L, P, I, I, I, F, P],
     "vpt_reduce_rows": [P, I, I, P, I, P],
     "vpt_patchify": [P, I, P, P, F, U64, I, I, I, P, P],
@@ -73,12 +74,13 @@ SIGNATURES: dict[str, list] = {
 }
 _RESTYPES = {
     "vpt_gemm_workspace_bytes": C.c_long,
+    "vpt_attn_q_scale": C.c_float,
     "vpt_last_error_string": C.c_char_p,
     "vpt_build_info": C.c_char_p,
 }
 # Entry points that return a value (size / count / string) rather than a status code.
 _VALUE_FNS = {"vpt_gemm_workspace_bytes", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
-              "vpt_colsum_blocks", "vpt_last_error_string", "vpt_abi_version", "vpt_build_info"}
+              "vpt_colsum_blocks", "vpt_attn_q_scale", "vpt_last_error_string", "vpt_abi_version", "vpt_build_info"}
 
 
 def _load(path: Path) -> C.CDLL:

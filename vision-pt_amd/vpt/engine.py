@@ -194,7 +194,8 @@ class JiTEngine:
             xn1, rstd1 = ops.rmsnorm_fwd(x, w["pn1"], pool.get(tag + "xn1", (M, D)), pool.get(tag + "rstd1", (M,), F32))
             qkv = ops.linear(xn1, w["pwqkv"], w["pbqkv"], out=pool.get(tag + "qkv", (M, 3 * D)))
             qk = ops.qknorm_rope_fwd(qkv, w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, rows,
-                                     out=pool.get(tag + "qk", (M, 2 * D)))
+                                     out=pool.get(tag + "qk", (M, 2 * D)),
+                                     q_scale=ops.attn_q_scale(1.0 / math.sqrt(cfg.head_dim)))
             o = pool.get(tag + "o", (M, D))
             lse = pool.get(tag + "lse", (B, Hh, lse_ld), F32)
             ops.attn_fwd(ops._t4(qk, B, rows, Hh, 0), ops._t4(qk, B, rows, Hh, D), ops._t4(qkv, B, rows, Hh, 2 * D),

@@ -177,14 +177,15 @@ def reduce_rows(part, out, accumulate=False):
     return out
 
 
-def qknorm_rope_fwd(qkv, wq, wk, cos_t, sin_t, rows_per_seq, out=None, eps=1e-6):
-    """qkv [M, 3D] -> out [M, 2D] = (rope(rms(q)), rope(rms(k)))."""
+def qknorm_rope_fwd(qkv, wq, wk, cos_t, sin_t, rows_per_seq, out=None, eps=1e-6, q_scale=1.0):
+    """qkv [M, 3D] -> out [M, 2D] = (rope(rms(q)) * q_scale, rope(rms(k))); q_scale = attn_q_scale() makes
+    the q half the pre-scaled query the attention kernels take."""
     M = qkv.shape[0]
     D = qkv.shape[1] // 3
     if out is None:
         out = torch.empty(M, 2 * D, dtype=BF16, device=qkv.device)
     call("vpt_qknorm_rope_fwd", qkv.data_ptr(), qkv.stride(0), wq.data_ptr(), wk.data_ptr(), cos_t.data_ptr(),
-         sin_t.data_ptr(), out.data_ptr(), out.stride(0), M, rows_per_seq, D, eps, stream())
+         sin_t.data_ptr(), out.data_ptr(), out.stride(0), M, rows_per_seq, D, eps, float(q_scale), stream())
     return out
 
 
@@ -211,9 +212,15 @@ def _t4(t, B: int, rows: int, H: int, col0: int = 0):
     return t.data_ptr() + col0 * t.element_size(), rows * ld, 64, ld
 
 
+def attn_q_scale(scale=0.125) -> float:
+    """Factor the attention kernels expect pre-applied to q (scale * log2 e; see include/vpt_hip.h)."""
+    return float(call("vpt_attn_q_scale", scale))
+
+
 def attn_fwd(q, k, v, o, lse, kbias, B, H, rows, n, n_dense, scale=0.125, nk=None):
-    """q/k/v/o as (ptr, sb, sh, sr) tuples (element strides); lse [B,H,rows] f32; kbias [B,keys] f32 or None;
-    n query rows, nk key rows (default n; cross-attention otherwise)."""
+    """q/k/v/o as (ptr, sb, sh, sr) tuples (element strides); q PRE-SCALED by attn_q_scale(scale);
+    lse [B,H,rows] f32 (receives -LSE in log2 units); kbias [B,keys] f32 or None; n query rows, nk key rows
+    (default n; cross-attention otherwise)."""
     nk = n if nk is None else nk
 
     def run():

@@ -135,12 +135,18 @@ class SDXLTransformerBlock:
         self._st = None
 
     def _attn_fwd(self, q, k, v, B, n, nk):
+        """q must already be pre-scaled (`_qs`); the backward returns the gradient of the raw q."""
         o = torch.empty(B * n, self.inner, dtype=BF16, device=self.device)
         lse = torch.empty(B, self.heads, n, dtype=F32, device=self.device)
         H = self.heads
         ops.attn_fwd(ops._t4(q, B, n, H), ops._t4(k, B, nk, H), ops._t4(v, B, nk, H), ops._t4(o, B, n, H), lse, None,
                      B, H, n, n, nk, nk=nk)
         return o, lse
+
+    @staticmethod
+    def _qs(q):
+        """The attention kernels take q pre-multiplied by scale*log2(e) (include/vpt_hip.h)."""
+        return ops.scale_bf16(q, ops.attn_q_scale(0.125))
 
     def _attn_bwd(self, q, k, v, o, lse, do, B, n, nk):
         H = self.heads
@@ -158,10 +164,11 @@ class SDXLTransformerBlock:
         L = self.lin
         h1, m1, r1 = ops.layernorm_fwd(x, *self.norm["norm1"])
         q, k, v = (L[f"attn1.to_{c}"].forward(h1, save) for c in "qkv")
+        q = self._qs(q)
         o1, lse1 = self._attn_fwd(q, k, v, B, n, n)
         x1 = ops.add_bf16(x, L["attn1.to_out.0"].forward(o1, save))
         h2, m2, r2 = ops.layernorm_fwd(x1, *self.norm["norm2"])
-        q2 = L["attn2.to_q"].forward(h2, save)
+        q2 = self._qs(L["attn2.to_q"].forward(h2, save))
         k2 = L["attn2.to_k"].forward(ctx, save)
         v2 = L["attn2.to_v"].forward(ctx, save)
         o2, lse2 = self._attn_fwd(q2, k2, v2, B, n, nc)
