@@ -48,6 +48,9 @@ int vpt_gemm_set_geometry(int geo);
 /* Diagnostic: u64 buffer [256][8][8] receiving per-wave K-step segment cycle sums from the stamped
  * ring build (geometry 2566, forward direction); nullptr disables. */
 int vpt_gemm_set_debug(unsigned long long* buf);
+/* The 256x256 ring kernel is persistent: min(work items, grid) blocks walk (tile, split-K slice)
+ * items. Benchmark/test hook for the grid size (0 = default, 256 = one block per CU). */
+int vpt_gemm_set_ring_grid(int blocks);
 
 /* ---- flash attention, head_dim 64 ---------------------------------------------------------
  * Tensors addressed p[b*sb + h*sh + row*sr + d]; n query rows, nk key rows (nk = n for

@@ -105,6 +105,29 @@ def test_gemm_geometries_all_directions(ops, geo, M, N, K):
         ops.lib.vpt_gemm_set_geometry(0)
 
 
+@pytest.mark.parametrize("grid", [1, 3, 8, 37])
+def test_gemm_ring_persistent_grid(ops, grid):
+    """The persistent 256x256 ring kernel with fewer blocks than work items: every block walks several
+    (tile, split-K slice) items (epilogue -> next item's DMA in one block), all three directions."""
+    M, N, K = 1100, 776, 200
+    ops.lib.vpt_gemm_set_geometry(256)
+    ops.lib.vpt_gemm_set_ring_grid(grid)
+    try:
+        x = rnd(M, K, seed=90)
+        w = rnd(N, K, scale=0.05, seed=91)
+        b = rnd(N, scale=0.1, seed=92)
+        dy = rnd(M, N, seed=93)
+        assert rel(ops.linear(x, w, bias=b), x.float() @ w.float().t() + b.float()) < 5e-3
+        assert rel(ops.linear_dgrad(dy, w), dy.float() @ w.float()) < 5e-3
+        out = torch.empty(N, K, dtype=torch.float32, device=DEV)
+        for splits in (1, 5):
+            ops.linear_wgrad(dy, x, out, splits=splits)
+            assert rel(out, dy.float().t() @ x.float()) < 1e-5
+    finally:
+        ops.lib.vpt_gemm_set_ring_grid(0)
+        ops.lib.vpt_gemm_set_geometry(0)
+
+
 def test_gemm_split_matches_unsplit(ops):
     M, N, K = 2048, 384, 256
     dy, x = rnd(M, N, seed=12), rnd(M, K, seed=13)

@@ -41,6 +41,7 @@ struct GemmArgs {
   int k_split;          // reduction length per split slice (multiple of BK)
   long split_stride;    // elements between partial slabs (f32 outputs)
   int out_mode, act;
+  int splits;               // split-K slices (ring kernel work items = tiles * splits)
   float alpha;              // output scale applied to the accumulator before bias (LoRA alpha / rank)
   unsigned long long* dbg;  // stamp-diagnostic output (geometry 2566 only)
 };
@@ -183,7 +184,7 @@ __device__ __forceinline__ void mma_tile(const char* la, floatx4 (&acc)[G::MI][G
 // then a vectorised row pass applies bias / SiLU / residual and stores 8-16 B per lane.
 template <typename G>
 __device__ __forceinline__ void epilogue(const GemmArgs& g, floatx4 (&acc)[G::MI][G::NI], char* smem, int wid, int lane,
-                                         int m0, int n0, int wm, int wn) {
+                                         int m0, int n0, int wm, int wn, int split) {
   float* st = reinterpret_cast<float*>(smem) + wid * 64 * EPI_LD;
   const int colw = (lane & 15) * 4;
 #pragma unroll
@@ -232,7 +233,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, floatx4 (&acc)[G::MI
           w.y = pack_bf16x2(o[2], o[3]);
           *reinterpret_cast<uint2*>(C + (long)row * g.ldc + col) = w;
         } else {
-          float* C = reinterpret_cast<float*>(g.C) + (long)blockIdx.y * g.split_stride;
+          float* C = reinterpret_cast<float*>(g.C) + (long)split * g.split_stride;
           floatx4* dst = reinterpret_cast<floatx4*>(C + (long)row * g.ldc + col);
           floatx4 ov = {o[0], o[1], o[2], o[3]};
           if (g.out_mode == OUT_F32_ACC) ov += *dst;
@@ -306,7 +307,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_bf16_kernel(GemmArgs g
     cur ^= 1;
   }
 
-  epilogue<G>(g, acc, smem, wid, lane, m0, n0, wm, wn);
+  epilogue<G>(g, acc, smem, wid, lane, m0, n0, wm, wn, blockIdx.y);
 }
 
 // ---- T256 ring kernel: 256x256 block tile, 8 waves (2x4) of 128x64, BK = 32 stages ------------
@@ -327,6 +328,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_bf16_kernel(GemmArgs g
 // (finite, in-bounds) addresses and its k >= K lanes of the A fragments are zeroed in registers.
 constexpr int RBK = 32;
 constexpr int RSTAGES = 4;
+int g_ring_grid = 256;  // persistent ring grid: one block per CU (vpt_gemm_set_ring_grid)
 
 __device__ __forceinline__ int kmaj32_off(int row, int chunk) {  // [R][32] bf16, 64-B rows
   return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4);
@@ -441,11 +443,165 @@ __device__ __forceinline__ unsigned long long stamp() {
   return t;
 }
 
+// Wait for a K tile with two younger tiles (8 pieces) and the previous item's S epilogue stores (issued
+// after the tile) still allowed in flight: S = 16 (bf16 output) or 32 (f32).
+__device__ __forceinline__ void wait_vm_pend(int S) {
+  if (S == 16) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+}
+
+// One work item (tile, split-K slice) of the ring kernel.
+struct RingItem {
+  int m0, n0, split, kbeg, kend, nk, klast;
+  uint32_t va0, va1, vb0, vb1;  // loop-invariant per-lane DMA piece offsets of full K tiles
+};
+
+template <bool AK, bool BK_>
+__device__ __forceinline__ RingItem ring_item(const GemmArgs& g, int item, int items, int tiles, int tiles_n, int wid,
+                                              int lane) {
+  const int q8 = items >> 3, r8 = items & 7, xcd = item & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (item >> 3);
+  RingItem it;
+  it.split = wgid / tiles;
+  const int tile = wgid - it.split * tiles;
+  it.m0 = tile / tiles_n * 256;
+  it.n0 = tile % tiles_n * 256;
+  it.kbeg = it.split * g.k_split;
+  it.kend = min(g.K, it.kbeg + g.k_split);
+  it.nk = (it.kend - it.kbeg + RBK - 1) / RBK;
+  it.klast = it.kend - it.kbeg - (it.nk - 1) * RBK;  // valid k of the last tile (1..32)
+  it.va0 = tile_voff<AK, 256>(g.lda, it.m0, g.M, RBK, wid, lane, 0);
+  it.va1 = tile_voff<AK, 256>(g.lda, it.m0, g.M, RBK, wid, lane, 1);
+  it.vb0 = tile_voff<BK_, 256>(g.ldb, it.n0, g.N, RBK, wid, lane, 0);
+  it.vb1 = tile_voff<BK_, 256>(g.ldb, it.n0, g.N, RBK, wid, lane, 1);
+  return it;
+}
+
+// K tile t of item `it` by LDS-DMA into ring stage t % 4: 4 pieces per wave (A: 2, B: 2).
+template <bool AK, bool BK_>
+__device__ __forceinline__ void ring_issue(const GemmArgs& g, const RingItem& it, int t, uint32_t lds0, int wid,
+                                           int lane) {
+  constexpr int A32 = 256 * RBK * 2, STAGE32 = 2 * A32;
+  const uint32_t la = __builtin_amdgcn_readfirstlane(lds0 + (t & (RSTAGES - 1)) * STAGE32);
+  const int k0 = it.kbeg + t * RBK;
+  const int kv = min(RBK, it.kend - k0);
+  const void* ab = uniform_ptr(tile_ptr<AK>(g.A, g.lda, it.m0, k0));
+  const void* bb = uniform_ptr(tile_ptr<BK_>(g.B, g.ldb, it.n0, k0));
+  if (kv == RBK) {
+    glds_step(ab, bb, it.va0, it.va1, it.vb0, it.vb1, la, la + 1024, la + A32, la + A32 + 1024);
+  } else {
+    glds_step(ab, bb, tile_voff<AK, 256>(g.lda, it.m0, g.M, kv, wid, lane, 0),
+              tile_voff<AK, 256>(g.lda, it.m0, g.M, kv, wid, lane, 1),
+              tile_voff<BK_, 256>(g.ldb, it.n0, g.N, kv, wid, lane, 0),
+              tile_voff<BK_, 256>(g.ldb, it.n0, g.N, kv, wid, lane, 1), la, la + 1024, la + A32, la + A32 + 1024);
+  }
+}
+
+// Ring epilogue. Per 16-row fragment of the wave's 128x64 sub-tile: stage the f32 accumulators in the
+// wave's 4 KB slice of ring stage 3 (16 rows x 64 floats, 16-B slot ^= row & 1: conflict-free b128
+// reads, 2-way b32 writes), read back 2 rows x 8 consecutive columns per lane, apply alpha / bias /
+// SiLU / residual / accumulate, and store with buffer stores. Rows past M fall outside the buffer's
+// num_records and columns past N carry an offset past it, so the hardware drops them without a
+// branch: every wave issues exactly ring_stores(out_mode) store instructions, which the next item's
+// counted vmcnt waits rely on (stores are younger than that item's first three K tiles).
+__device__ __forceinline__ int ring_stores(int out_mode) { return out_mode == OUT_BF16 ? 16 : 32; }
+__device__ __forceinline__ int stg_off(int row, int col) {
+  return row * 256 + (((col >> 2) ^ (row & 1)) << 4) + ((col & 3) << 2);
+}
+
+__device__ __forceinline__ void epilogue_ring(const GemmArgs& g, const floatx4 (&acc)[8][4], char* stg, int lane,
+                                              const RingItem& it, int wm, int wn, const float (&bias8)[8]) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const int es = g.out_mode == OUT_BF16 ? 2 : 4;
+  const int rows_here = min(256, g.M - it.m0);
+  char* cbase = (char*)g.C + ((long)it.split * g.split_stride + (long)it.m0 * g.ldc + it.n0) * es;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(cbase, (short)0, rows_here * (int)g.ldc * es,
+                                                                       0x00020000);
+  const int cw = lane & 7;
+  const int tcol = wn * 64 + cw * 8;  // column within the tile
+  const bool col_ok = it.n0 + tcol < g.N;
+  const int lrow = wm * 128 + (lane >> 3);  // tile row of (fragment 0, p = 0)
+  // lane part of the store offset; fragment i / half p add the wave-uniform soffset (i*16 + p*8) rows
+  const uint32_t voff = col_ok ? (uint32_t)((lrow * (int)g.ldc + tcol) * es) : 0x80000000u;
+  const int rstride = (int)g.ldc * es;  // bytes per row
+  // residual rows of this tile (bf16, leading dim ldr), addressed like C
+  const bf16_t* rbase = g.resid ? g.resid + (long)it.m0 * g.ldr + it.n0 : g.resid;
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)rbase, (short)0,
+                                                                       g.resid ? rows_here * (int)g.ldr * 2 : 0, 0x00020000);
+  const int rrstride = (int)g.ldr * 2;
+  const uint32_t rvoff = col_ok ? (uint32_t)((lrow * (int)g.ldr + tcol) * 2) : 0x80000000u;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        *reinterpret_cast<float*>(stg + stg_off((lane >> 4) * 4 + r, j * 16 + (lane & 15))) = acc[i][j][r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own-wave LDS writes retired
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int lr = p * 8 + (lane >> 3);
+      const floatx4 x0 = *reinterpret_cast<const floatx4*>(stg + stg_off(lr, cw * 8));
+      const floatx4 x1 = *reinterpret_cast<const floatx4*>(stg + stg_off(lr, cw * 8 + 4));
+      float o[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = o[e] * g.alpha + bias8[e];
+      if (g.act == ACT_SILU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = o[e] / (1.f + __expf(-o[e]));
+      }
+      const int soff = (i * 16 + p * 8) * rstride;
+      if (g.out_mode == OUT_BF16) {
+        if (g.resid) {
+          // reference semantics: residual + bf16(linear output), rounded again to bf16. Buffer load over
+          // the tile's residual rows: out-of-range rows / columns read 0 (their stores are dropped).
+          const u32x4 r4 = __builtin_amdgcn_raw_buffer_load_b128(rr, (int)rvoff, (i * 16 + p * 8) * rrstride, 0);
+          float rv[8];
+          unpack8(make_uint4(r4[0], r4[1], r4[2], r4[3]), rv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = bf2f(f2bf(o[e])) + rv[e];
+        }
+        const uint4 w = pack8(o);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{w.x, w.y, w.z, w.w}, rs, (int)voff, soff, 0);
+      } else {
+        if (g.out_mode == OUT_F32_ACC) {
+          const u32x4 a0 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)voff, soff, 0);
+          const u32x4 a1 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)voff, soff + 16, 0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { o[e] += __uint_as_float(a0[e]); o[4 + e] += __uint_as_float(a1[e]); }
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4{__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3])}, rs,
+            (int)voff, soff, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4{__float_as_uint(o[4]), __float_as_uint(o[5]), __float_as_uint(o[6]), __float_as_uint(o[7])}, rs,
+            (int)voff, soff + 16, 0);
+      }
+    }
+  }
+}
+
 // STAMP (diagnostic build, geometry 2566): per-wave cycle sums of the K-step segments (DMA issue,
 // ds_reads, vmcnt wait, barrier Y, MFMA issue, barrier X) to g.dbg[(block*8 + wave)*8 + seg]; read the
 // shares, not the length (the stamps' lgkmcnt(0) forbids overlaps the real kernel has).
-template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false, bool STAMP = false>
-__global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g) {
+//
+// PERSISTENT grid: min(items, 256) blocks walk work items (tile, split-K slice) with a stride of
+// gridDim.x; item -> tile uses the same bijective XCD remap as a one-tile-per-block launch of `items`
+// blocks (block b runs on XCD b % 8 and only sees items == b mod 8). Item seam: after the last K step
+// the block DMAs the NEXT item's K tiles 0-2 into ring stages 0-2, then runs this item's epilogue out of
+// stage 3, so the next item's operand latency and this item's store drain overlap the epilogue and
+// the next item's first K steps (its waits for tiles 0-2 count the epilogue stores as younger).
+// TL (diagnostic build, geometry 2567): wave 0 of each block writes s_memrealtime (100 MHz) stamps of its
+// first 4 items to g.dbg[(block*4 + k)*4 + phase]: phase 0 item start, 1 tile 0 ready (after X_0),
+// 2 K loop done, 3 epilogue issued.
+__device__ __forceinline__ void tl_stamp(const GemmArgs& g, int k, int phase, int wid, int lane) {
+  if (wid == 0 && lane == 0 && k < 4)
+    g.dbg[((long)blockIdx.x * 4 + k) * 4 + phase] = __builtin_amdgcn_s_memrealtime();
+}
+
+template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false, bool STAMP = false, bool TL = false>
+__global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
   using G = GR;
   constexpr int A32 = 256 * RBK * 2, STAGE32 = 2 * A32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -453,93 +609,109 @@ __global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmArgs g) {
   const int wm = wid / 4, wn = wid % 4;
 
   const int tiles_n = (g.N + 255) / 256;
-  const int nwg = gridDim.x;
-  const int orig = blockIdx.x;
-  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int tm = wgid / tiles_n, tn = wgid % tiles_n;
-  const int m0 = tm * 256, n0 = tn * 256;
-
-  const int kbeg = blockIdx.y * g.k_split;
-  const int kend = min(g.K, kbeg + g.k_split);
-  const int nk = (kend - kbeg + RBK - 1) / RBK;
-  const int klast = kend - kbeg - (nk - 1) * RBK;  // valid k of the last tile (1..32)
-
-  floatx4 acc[G::MI][G::NI];
-#pragma unroll
-  for (int i = 0; i < G::MI; ++i)
-#pragma unroll
-    for (int j = 0; j < G::NI; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  // Loop-invariant per-lane piece offsets (full tiles) and LDS piece addresses (stage 0).
-  const uint32_t va0 = tile_voff<AK, 256>(g.lda, m0, g.M, RBK, wid, lane, 0);
-  const uint32_t va1 = tile_voff<AK, 256>(g.lda, m0, g.M, RBK, wid, lane, 1);
-  const uint32_t vb0 = tile_voff<BK_, 256>(g.ldb, n0, g.N, RBK, wid, lane, 0);
-  const uint32_t vb1 = tile_voff<BK_, 256>(g.ldb, n0, g.N, RBK, wid, lane, 1);
+  const int tiles = ((g.M + 255) / 256) * tiles_n;
+  const int items = tiles * g.splits;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(VPT_LDS char*)smem + wid * 2048;
-  auto issue = [&](int t) {  // 4 pieces per wave: 2 of A, 2 of B
-    const uint32_t la = __builtin_amdgcn_readfirstlane(lds0 + (t & (RSTAGES - 1)) * STAGE32);
-    const int k0 = kbeg + t * RBK;
-    const int kv = min(RBK, kend - k0);
-    const void* ab = uniform_ptr(tile_ptr<AK>(g.A, g.lda, m0, k0));
-    const void* bb = uniform_ptr(tile_ptr<BK_>(g.B, g.ldb, n0, k0));
-    if (kv == RBK) {
-      glds_step(ab, bb, va0, va1, vb0, vb1, la, la + 1024, la + A32, la + A32 + 1024);
-    } else {
-      glds_step(ab, bb, tile_voff<AK, 256>(g.lda, m0, g.M, kv, wid, lane, 0),
-                tile_voff<AK, 256>(g.lda, m0, g.M, kv, wid, lane, 1), tile_voff<BK_, 256>(g.ldb, n0, g.N, kv, wid, lane, 0),
-                tile_voff<BK_, 256>(g.ldb, n0, g.N, kv, wid, lane, 1), la, la + 1024, la + A32, la + A32 + 1024);
-    }
-  };
-  issue(0);
-  if (nk > 1) issue(1);
-  if (nk > 2) issue(2);
-  wait_younger(min(2, nk - 1));  // tile 0
-  if (PP && wm == 1) raw_barrier();
-  raw_barrier();  // X_0
+  char* stg = smem + 3 * STAGE32 + wid * 4096;  // this wave's epilogue staging slice (ring stage 3)
+  const int S = ring_stores(g.out_mode);
 
-  unsigned long long seg[6] = {0, 0, 0, 0, 0, 0};
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* st = smem + (kt & (RSTAGES - 1)) * STAGE32;
-    unsigned long long t0 = 0, t1 = 0;
-    if (STAMP) t0 = stamp();
-    if (!DMAC && ABL != 1 && kt + 3 < nk) issue(kt + 3);
-    if (STAMP) { t1 = stamp(); seg[0] += t1 - t0; t0 = t1; }
-    bf16x8 bfr[G::NI], af[G::MI];
-#pragma unroll
-    for (int j = 0; j < G::NI; ++j) bfr[j] = read_frag32<BK_, 256>(st + A32, wn * G::WC + j * 16, lane);
-#pragma unroll
-    for (int i = 0; i < G::MI; ++i) af[i] = read_frag32<AK, 256>(st, wm * G::WR + i * 16, lane);
-    if (kt == nk - 1 && klast < RBK) {
-#pragma unroll
-      for (int i = 0; i < G::MI; ++i) af[i] = mask_k(af[i], 8 * (lane >> 4), klast);
-    }
-    if (STAMP) { t1 = stamp(); seg[1] += t1 - t0; t0 = t1; }
-    if (ABL != 2) wait_younger(min(DMAC ? 1 : 2, nk - 2 - kt));  // tile kt+1 (if any) landed for this wave
-    if (STAMP) { t1 = stamp(); seg[2] += t1 - t0; t0 = t1; }
-    if (DMAC) bare_barrier(); else raw_barrier();                // Y_kt
-    if (STAMP) { t1 = stamp(); seg[3] += t1 - t0; t0 = t1; }
-    if (DMAC && ABL != 1 && kt + 3 < nk) issue(kt + 3);
-    __builtin_amdgcn_s_setprio(1);
+  int item = blockIdx.x;
+  if (item >= items) return;
+  RingItem it = ring_item<AK, BK_>(g, item, items, tiles, tiles_n, wid, lane);
+  ring_issue<AK, BK_>(g, it, 0, lds0, wid, lane);
+  if (it.nk > 1) ring_issue<AK, BK_>(g, it, 1, lds0, wid, lane);
+  if (it.nk > 2) ring_issue<AK, BK_>(g, it, 2, lds0, wid, lane);
+  int pend = 0;  // epilogue stores younger than this item's pre-issued tiles 0-2 (0 on the first item)
+  int kth = 0;   // items done by this block (TL stamps)
+
+  for (;;) {
+    if (TL) tl_stamp(g, kth, 0, wid, lane);
+    const int nk = it.nk;
+    // bias of this item's 8 output columns (plain load; consumed after the K loop, when nothing is
+    // outstanding, so the compiler's wait for it costs nothing)
+    uint4 braw = make_uint4(0, 0, 0, 0);
+    const int bcol = it.n0 + wn * 64 + (lane & 7) * 8;
+    if (g.bias && bcol < g.N) braw = *reinterpret_cast<const uint4*>(g.bias + bcol);
+
+    floatx4 acc[G::MI][G::NI];
 #pragma unroll
     for (int i = 0; i < G::MI; ++i)
 #pragma unroll
-      for (int j = 0; j < G::NI; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    if (STAMP) { t1 = stamp(); seg[4] += t1 - t0; t0 = t1; }
-    if (DMAC) bare_barrier(); else raw_barrier();  // X_kt+1
-    if (STAMP) { t1 = stamp(); seg[5] += t1 - t0; }
-  }
-  if (STAMP && lane == 0 && blockIdx.x < 256 && blockIdx.y == 0) {
-    unsigned long long* o = g.dbg + ((long)blockIdx.x * 8 + wid) * 8;
+      for (int j = 0; j < G::NI; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    if (pend && nk >= 3) wait_vm_pend(pend);  // tile 0 landed: tiles 1, 2 and the stores are younger
+    else wait_younger(min(2, nk - 1));
+    if (PP && wm == 1) raw_barrier();
+    raw_barrier();  // X_0
+    if (TL) tl_stamp(g, kth, 1, wid, lane);
+
+    unsigned long long seg[6] = {0, 0, 0, 0, 0, 0};
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* st = smem + (kt & (RSTAGES - 1)) * STAGE32;
+      unsigned long long t0 = 0, t1 = 0;
+      if (STAMP) t0 = stamp();
+      if (!DMAC && ABL != 1 && kt + 3 < nk) ring_issue<AK, BK_>(g, it, kt + 3, lds0, wid, lane);
+      if (STAMP) { t1 = stamp(); seg[0] += t1 - t0; t0 = t1; }
+      bf16x8 bfr[G::NI], af[G::MI];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) o[i] = seg[i];
-    o[6] = nk;
+      for (int j = 0; j < G::NI; ++j) bfr[j] = read_frag32<BK_, 256>(st + A32, wn * G::WC + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < G::MI; ++i) af[i] = read_frag32<AK, 256>(st, wm * G::WR + i * 16, lane);
+      if (kt == nk - 1 && it.klast < RBK) {
+#pragma unroll
+        for (int i = 0; i < G::MI; ++i) af[i] = mask_k(af[i], 8 * (lane >> 4), it.klast);
+      }
+      if (STAMP) { t1 = stamp(); seg[1] += t1 - t0; t0 = t1; }
+      // tile kt+1 (if any) landed for this wave; the previous epilogue's stores are younger than tiles 0-2
+      if (ABL != 2) {
+        if (!DMAC && pend && kt < 2 && nk - 2 - kt >= 2) wait_vm_pend(pend);  // 8 + S younger
+        else wait_younger(min(DMAC ? 1 : 2, nk - 2 - kt));  // (over-waits for the stores when pend)
+      }
+      if (STAMP) { t1 = stamp(); seg[2] += t1 - t0; t0 = t1; }
+      if (DMAC) bare_barrier(); else raw_barrier();                // Y_kt
+      if (STAMP) { t1 = stamp(); seg[3] += t1 - t0; t0 = t1; }
+      if (DMAC && ABL != 1 && kt + 3 < nk) ring_issue<AK, BK_>(g, it, kt + 3, lds0, wid, lane);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < G::MI; ++i)
+#pragma unroll
+        for (int j = 0; j < G::NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (STAMP) { t1 = stamp(); seg[4] += t1 - t0; t0 = t1; }
+      if (DMAC) bare_barrier(); else raw_barrier();  // X_kt+1
+      if (STAMP) { t1 = stamp(); seg[5] += t1 - t0; }
+    }
+    if (STAMP && lane == 0 && item < 256 && it.split == 0) {
+      unsigned long long* o = g.dbg + ((long)item * 8 + wid) * 8;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) o[i] = seg[i];
+      o[6] = nk;
+    }
+    if (PP && wm == 0) raw_barrier();
+    if (TL) tl_stamp(g, kth, 2, wid, lane);
+    float bias8[8];
+    unpack8(braw, bias8);
+    // Every wave has passed its last K step (barrier X_nk), so ring stages 0-2 are free: DMA the next
+    // item's first tiles before this item's epilogue (which stages through stage 3 only).
+    const int next = item + gridDim.x;
+    RingItem nx;
+    if (next < items) {
+      nx = ring_item<AK, BK_>(g, next, items, tiles, tiles_n, wid, lane);
+      ring_issue<AK, BK_>(g, nx, 0, lds0, wid, lane);
+      if (nx.nk > 1) ring_issue<AK, BK_>(g, nx, 1, lds0, wid, lane);
+      if (nx.nk > 2) ring_issue<AK, BK_>(g, nx, 2, lds0, wid, lane);
+    }
+    epilogue_ring(g, acc, stg, lane, it, wm, wn, bias8);
+    if (TL) tl_stamp(g, kth, 3, wid, lane);
+    ++kth;
+    if (next >= items) break;
+    // The next item's first LDS-DMA into stage 3 (tile 3, issued at its K step 0) follows its barrier
+    // X_0, which every wave reaches only after its staging reads (raw_barrier: lgkmcnt(0) first).
+    item = next;
+    it = nx;
+    pend = S;
   }
-  if (PP && wm == 0) raw_barrier();
-  __syncthreads();  // the ring is reused as epilogue staging
-  epilogue<G>(g, acc, smem, wid, lane, m0, n0, wm, wn);
 }
 
 template <bool AK, bool BK_, int TM, int TN, int WGM, int WGN>
@@ -552,23 +724,26 @@ int launch(const GemmArgs& g, int splits, hipStream_t s) {
   return VPT_OK;
 }
 
-template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false, bool STAMP = false>
+template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false, bool STAMP = false, bool TL = false>
 int launch_ring(const GemmArgs& g, int splits, hipStream_t s) {
-  constexpr int LDS = RSTAGES * 2 * 256 * RBK * 2 > GR::EPI ? RSTAGES * 2 * 256 * RBK * 2 : GR::EPI;
-  const int tiles = ((g.M + 255) / 256) * ((g.N + 255) / 256);
-  hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP>), dim3(tiles, splits), dim3(512), LDS, s, g);
+  constexpr int LDS = RSTAGES * 2 * 256 * RBK * 2;  // the epilogue stages through ring stage 3
+  const int items = ((g.M + 255) / 256) * ((g.N + 255) / 256) * splits;
+  const int grid = items < g_ring_grid ? items : g_ring_grid;
+  hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL>), dim3(grid), dim3(512), LDS, s, g);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
 
 template <bool AK, bool BK_>
 int launch_geo(const GemmArgs& g, int splits, int geo, hipStream_t s) {
+  if (geo != 128 && geo != 2562 && g.N % 8 != 0) geo = 128;  // ring epilogue stores 8-column chunks
   if (geo == 256) return launch_ring<AK, BK_, true>(g, splits, s);
   if (geo == 2561) return launch_ring<AK, BK_, false>(g, splits, s);  // ring without the stagger (A/B only)
   if (AK && BK_ && geo == 2563) return launch_ring<AK, BK_, true, 1>(g, splits, s);  // ablation, wrong results
   if (AK && BK_ && geo == 2564) return launch_ring<AK, BK_, true, 2>(g, splits, s);  // ablation, wrong results
   if (geo == 2565) return launch_ring<AK, BK_, true, 0, true>(g, splits, s);  // DMA in the MFMA phase
   if (AK && BK_ && geo == 2566 && g.dbg) return launch_ring<AK, BK_, true, 0, false, true>(g, splits, s);  // stamps
+  if (AK && BK_ && geo == 2567 && g.dbg) return launch_ring<AK, BK_, true, 0, false, false, true>(g, splits, s);  // timeline
   if (geo == 2562) return launch<AK, BK_, 256, 256, 2, 4>(g, splits, s);  // 2-stage BK=64 T256 (A/B only)
   return launch<AK, BK_, 128, 128, 2, 2>(g, splits, s);
 }
@@ -636,11 +811,13 @@ extern "C" int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* 
     per = (per + BK - 1) / BK * BK;
     splits = (K + per - 1) / per;
     g.k_split = per;
+    g.splits = splits;
     g.C = workspace; g.ldc = N;
     g.split_stride = (long)M * N;
     g.out_mode = OUT_F32;
   } else {
     g.k_split = K;
+    g.splits = 1;
     g.C = C; g.ldc = ldc;
     g.split_stride = 0;
     g.out_mode = out_mode;
@@ -662,8 +839,8 @@ extern "C" int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* 
 }
 
 extern "C" int vpt_gemm_set_geometry(int geo) {
-  VPT_CHECK_ARG(geo == 0 || geo == 128 || geo == 256 || (geo >= 2561 && geo <= 2566),
-                "vpt_gemm_set_geometry: 0, 128, 256 or 2561-2566");
+  VPT_CHECK_ARG(geo == 0 || geo == 128 || geo == 256 || (geo >= 2561 && geo <= 2567),
+                "vpt_gemm_set_geometry: 0, 128, 256 or 2561-2567");
   g_geo_override = geo;
   return VPT_OK;
 }
@@ -672,6 +849,13 @@ extern "C" long vpt_gemm_workspace_bytes(int M, int N, int K, int splits) {
   (void)K;
   if (splits <= 1) return 0;
   return (long)splits * M * N * 4;
+}
+
+// Benchmark hook: persistent ring grid size (blocks); 0 restores one block per CU (256).
+extern "C" int vpt_gemm_set_ring_grid(int blocks) {
+  VPT_CHECK_ARG(blocks >= 0 && blocks <= 65536, "vpt_gemm_set_ring_grid: 0..65536");
+  g_ring_grid = blocks ? blocks : 256;
+  return VPT_OK;
 }
 
 // Diagnostic hook: output buffer for the stamped ring build (geometry 2566), [256 blocks][8 waves][8] u64.

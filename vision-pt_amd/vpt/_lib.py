@@ -25,6 +25,7 @@ SIGNATURES: dict[str, list] = {
     "vpt_gemm_workspace_bytes": [I, I, I, I],
     "vpt_gemm_set_geometry": [I],
     "vpt_gemm_set_debug": [P],
+    "vpt_gemm_set_ring_grid": [I],
     "vpt_attn_fwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, P, L, I, I, I, I, I, F, P],
     "vpt_attn_bwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, P, L, L, P, L,
                      P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, I, F, P],
