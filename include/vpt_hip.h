@@ -78,7 +78,9 @@ int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr, const void* k, 
 int vpt_attn_set_rescale_threshold(float tau);
 /* Benchmark hook: kernel variant (0 = production, 4-wave blocks; 1 / 2 = timing-only backward
  * ablations with wrong results: no in-loop tile staging / row reads in place of transposed reads;
- * 3 = 8-wave blocks, correct). Process-wide. */
+ * 3 = 8-wave blocks, correct; 4-7 = dK/dV-kernel timing ablations, wrong results: no exp2 / 4 of 16
+ * dV,dK MFMAs / no transposed LDS reads / no S,dP LDS reads; 8 = previous compiler-scheduled dK/dV
+ * body, correct). Process-wide. */
 int vpt_attn_set_variant(int v);
 
 /* ---- RMSNorm over the hidden dim -----------------------------------------------------------

@@ -216,7 +216,7 @@ def _attn_ref(q, k, v, bias, scale):
     return torch.einsum("bhqk,bhkd->bhqd", p, v)
 
 
-@pytest.fixture(params=[0, 3], ids=["4wave", "8wave"])
+@pytest.fixture(params=[0, 3, 8], ids=["4wave", "8wave", "unordered"])
 def attn_variant(ops, request):
     ops.lib.vpt_attn_set_variant(request.param)
     yield request.param

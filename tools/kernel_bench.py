@@ -82,13 +82,14 @@ def main():
         tb = timeit(lambda: ops.attn_bwd(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, None,
                                          ops._t4(dq, B, rows, H), ops._t4(dk, B, rows, H), ops._t4(dv, B, rows, H),
                                          B, H, rows, n, n))
-        for var in (1, 2):  # timing-only ablations of the backward (wrong results)
+        for var in (1, 2, 4, 5, 6, 7, 8):  # timing-only ablations of the backward (wrong results)
             ops.lib.vpt_attn_set_variant(var)
             tv = timeit(lambda: ops.attn_bwd(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, None,
                                              ops._t4(dq, B, rows, H), ops._t4(dk, B, rows, H),
                                              ops._t4(dv, B, rows, H), B, H, rows, n, n))
             ops.lib.vpt_attn_set_variant(0)
             res.setdefault(f"attn.bwd_alg_abl{var}", []).append(2 * fl / (tv * 1e-3) / 1e12)
+            res.setdefault(f"attn.bwd_ms_abl{var}", []).append(tv)
         ops.lib.vpt_attn_set_variant(3)  # 8-wave blocks (A/B)
         tf4 = timeit(lambda: ops.attn_fwd(q4, k4, v4, o4, lse, None, B, H, rows, n, n))
         tb4 = timeit(lambda: ops.attn_bwd(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, None,

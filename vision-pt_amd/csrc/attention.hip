@@ -397,6 +397,62 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
     if (more) stage(cur ^ 1, (t + 1) * 64);
     const char* lq = lds[cur][0];
     const char* ld = lds[cur][1];
+    if (ABL == 8) {
+      // Explicitly ordered body: the row fragments and row constants of query block qb+1 are read while
+      // block qb's S / dP chains run (s_setprio 1 around every MFMA group), P and dS are packed to bf16
+      // as soon as they exist, and sched_barriers keep hipcc from sinking the reads back to their uses.
+      floatx16 cs = rows16(lstat[cur][0], 0, h), cd = rows16(lstat[cur][1], 0, h);
+      bf16x8 qa[4], da[4], pp[2][2], pd[2][2];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) { qa[ks] = frag_rows(lq, 0, ks, lane); da[ks] = frag_rows(ld, 0, ks, lane); }
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        floatx16 s = cs, dp = cd;
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          s = mfma32(qa[ks], kf[ks], s);
+          dp = mfma32(da[ks], vf[ks], dp);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        if (qb == 0) {
+          cs = rows16(lstat[cur][0], 32, h);
+          cd = rows16(lstat[cur][1], 32, h);
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) { qa[ks] = frag_rows(lq, 32, ks, lane); da[ks] = frag_rows(ld, 32, ks, lane); }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        floatx16 P, dS;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = __builtin_amdgcn_exp2f(s[i]);
+          P[i] = p;
+          dS[i] = p * dp[i];
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) { pp[qb][s2] = pack_acc(P, s2); pd[qb][s2] = pack_acc(dS, s2); }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 tv[2], tq[2];
+#pragma unroll
+          for (int db = 0; db < 2; ++db) { tv[db] = frag_tr(ld, db, 2 * qb + s2, lane); tq[db] = frag_tr(lq, db, 2 * qb + s2, lane); }
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            dvT[db] = mfma32(tv[db], pp[qb][s2], dvT[db]);
+            dkT[db] = mfma32(tq[db], pd[qb][s2], dkT[db]);
+          }
+          __builtin_amdgcn_s_setprio(0);
+        }
+      if (more) settle(cur ^ 1, (t + 1) * 64);
+      cur ^= 1;
+      continue;
+    }
     floatx16 P[2], dS[2];
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
@@ -405,14 +461,14 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
       floatx16 s = rows16(lstat[cur][0], 32 * qb, h), dp = rows16(lstat[cur][1], 32 * qb, h);
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        s = mfma32(frag_rows(lq, 32 * qb, ks, lane), kf[ks], s);
-        dp = mfma32(frag_rows(ld, 32 * qb, ks, lane), vf[ks], dp);
+        s = mfma32(ABL == 6 ? vf[ks] : frag_rows(lq, 32 * qb, ks, lane), kf[ks], s);
+        dp = mfma32(ABL == 6 ? kf[ks] : frag_rows(ld, 32 * qb, ks, lane), vf[ks], dp);
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         // No key bias here: a masked key (bias -inf) only feeds its own lane's dK/dV columns, which
         // are stored as exact zeros below.
-        const float p = __builtin_amdgcn_exp2f(s[i]);
+        const float p = ABL == 3 ? s[i] : __builtin_amdgcn_exp2f(s[i]);
         P[qb][i] = p;
         dS[qb][i] = p * dp[i];
       }
@@ -423,9 +479,16 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
       for (int s2 = 0; s2 < 2; ++s2) {
         const bf16x8 pp = pack_acc(P[qb], s2);
         const bf16x8 pd = pack_acc(dS[qb], s2);
+        if (ABL == 4) {  // timing: one MFMA per (qb, s2) keeps P, dS alive in place of the 4 products
+          dvT[0] = mfma32(pp, pd, dvT[0]);
+          continue;
+        }
 #pragma unroll
         for (int db = 0; db < 2; ++db) {
-          if (ABL == 2) {
+          if (ABL == 5) {  // timing: register operands in place of the transposed LDS reads
+            dvT[db] = mfma32(kf[2 * db + s2], pp, dvT[db]);
+            dkT[db] = mfma32(vf[2 * db + s2], pd, dkT[db]);
+          } else if (ABL == 2) {
             dvT[db] = mfma32(frag_rows(ld, 32 * db, 2 * qb + s2, lane), pp, dvT[db]);
             dkT[db] = mfma32(frag_rows(lq, 32 * db, 2 * qb + s2, lane), pd, dkT[db]);
           } else {
@@ -610,8 +673,17 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
   } else if (g_variant == 2) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, 4>), k4, dim3(256), 0, s, g);
     hipLaunchKernelGGL((attn_bwd_dq_kernel<2, 4>), g4, dim3(256), kbl, s, g);
-  } else if (g_waves == 4) {
+  } else if (g_variant == 7) {  // the previous compiler-scheduled dK/dV body (correct results, A/B)
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 4>), k4, dim3(256), 0, s, g);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 4>), g4, dim3(256), kbl, s, g);
+  } else if (g_variant >= 3 && g_variant <= 6) {  // dK/dV-only timing ablations (dQ kernel unchanged)
+    if (g_variant == 3) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<3, 4>), k4, dim3(256), 0, s, g);
+    if (g_variant == 4) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<4, 4>), k4, dim3(256), 0, s, g);
+    if (g_variant == 5) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<5, 4>), k4, dim3(256), 0, s, g);
+    if (g_variant == 6) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<6, 4>), k4, dim3(256), 0, s, g);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 4>), g4, dim3(256), kbl, s, g);
+  } else if (g_waves == 4) {  // production: the explicitly ordered dK/dV body (ABL 8; +2 % measured)
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<8, 4>), k4, dim3(256), 0, s, g);
     VPT_LAUNCH_CHECK();
     hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 4>), g4, dim3(256), kbl, s, g);
   } else {
@@ -632,10 +704,12 @@ extern "C" int vpt_attn_set_rescale_threshold(float tau) {
 
 // Benchmark hook: kernel variant (0 = production: 4-wave blocks; 1, 2 = timing-only backward ablations
 // whose results are wrong: 1 = no in-loop tile staging, 2 = row reads in place of transposed reads;
-// 3 = 8-wave blocks, correct, A/B only).
+// 3 = 8-wave blocks, correct, A/B only; dK/dV-kernel-only ablations (wrong results): 4 = no exp2,
+// 5 = 4 of the 16 dV/dK MFMAs, 6 = no transposed LDS reads, 7 = no S/dP LDS reads; 8 = the
+// compiler-scheduled dK/dV body the production ordered body replaced, correct, A/B).
 extern "C" int vpt_attn_set_variant(int v) {
-  VPT_CHECK_ARG(v >= 0 && v <= 3, "vpt_attn_set_variant: 0..3");
-  g_variant = v == 3 ? 0 : v;
+  VPT_CHECK_ARG(v >= 0 && v <= 8, "vpt_attn_set_variant: 0..8");
+  g_variant = v == 3 ? 0 : (v >= 4 ? v - 1 : v);
   g_waves = v == 3 ? 8 : 4;
   return VPT_OK;
 }
