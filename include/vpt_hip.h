@@ -201,6 +201,16 @@ int vpt_scale_bf16(const void* a, long n, float s, void* out, void* stream);
 int vpt_nf4_quantize(const void* w, long n, const float* code2, void* packed, void* qabsmax, float* absmax2,
                      float* offset, float* absmax_scratch, void* stream);
 
+/* ---- bucketed batch preparation ---------------------------------------------
+ * One decoded uint8 RGB image [in_h][in_w][3] -> fp16 [3][out_h][out_w] batch slot: the reference's
+ * PILToTensor -> ToDtype(float16, scale=True) -> Normalize(0.5, 0.5) -> ObjectCoverResize (bicubic,
+ * antialias, to (scaled_h, scaled_w)) -> RandomCrop(top, left) chain, computed for the crop window only.
+ * Replaces src/dataset/text_to_image.py:145-158,164-177,199-213 and src/dataset/transform.py:11-55
+ * (torchvision / ATen antialiased bicubic on the CPU). workspace: *_workspace() bytes. */
+long vpt_cover_resize_crop_workspace(int in_h, int in_w, int scaled_h, int scaled_w, int top, int out_h, int out_w);
+int vpt_cover_resize_crop(const void* img, int in_h, int in_w, int scaled_h, int scaled_w, int top, int left,
+                          int out_h, int out_w, void* workspace, void* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

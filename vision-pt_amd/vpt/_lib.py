@@ -69,18 +69,21 @@ SIGNATURES: dict[str, list] = {
     "vpt_nf4_quantize": [P, L, P, P, P, P, P, P, P],
     "vpt_add_bf16": [P, P, L, P, P],
     "vpt_scale_bf16": [P, L, F, P, P],
+    "vpt_cover_resize_crop_workspace": [I, I, I, I, I, I, I],
+    "vpt_cover_resize_crop": [P, I, I, I, I, I, I, I, I, P, P, P],
     "vpt_last_error_string": [],
     "vpt_abi_version": [],
     "vpt_build_info": [],
 }
 _RESTYPES = {
     "vpt_gemm_workspace_bytes": C.c_long,
+    "vpt_cover_resize_crop_workspace": C.c_long,
     "vpt_attn_q_scale": C.c_float,
     "vpt_last_error_string": C.c_char_p,
     "vpt_build_info": C.c_char_p,
 }
 # Entry points that return a value (size / count / string) rather than a status code.
-_VALUE_FNS = {"vpt_gemm_workspace_bytes", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
+_VALUE_FNS = {"vpt_gemm_workspace_bytes", "vpt_cover_resize_crop_workspace", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
               "vpt_colsum_blocks", "vpt_attn_q_scale", "vpt_last_error_string", "vpt_abi_version", "vpt_build_info"}
 
 

@@ -434,3 +434,19 @@ def nf4_quantize(w, code2, packed, qabsmax, absmax2, offset, scratch):
     call("vpt_nf4_quantize", w.data_ptr(), w.numel(), code2.data_ptr(), packed.data_ptr(), qabsmax.data_ptr(),
          absmax2.data_ptr(), offset.data_ptr(), scratch.data_ptr(), stream())
 
+
+
+# ----------------------------------------------------------------------------- bucketed batch preparation
+def cover_resize_crop_workspace(in_h, in_w, scaled_h, scaled_w, top, out_h, out_w) -> int:
+    return int(call("vpt_cover_resize_crop_workspace", in_h, in_w, scaled_h, scaled_w, top, out_h, out_w))
+
+
+def cover_resize_crop(img_u8, in_h, in_w, scaled_h, scaled_w, top, left, out_h, out_w, workspace, out):
+    """uint8 [in_h, in_w, 3] -> fp16 [3, out_h, out_w] (see include/vpt_hip.h)."""
+    if img_u8.dtype != torch.uint8 or not img_u8.is_contiguous():
+        raise ValueError("img must be a contiguous uint8 [H, W, 3] GPU tensor")
+    if out.dtype != torch.float16 or not out.is_contiguous():
+        raise ValueError("out must be a contiguous fp16 [3, h, w] GPU tensor")
+    call("vpt_cover_resize_crop", img_u8.data_ptr(), in_h, in_w, scaled_h, scaled_w, top, left, out_h, out_w,
+         workspace.data_ptr(), out.data_ptr(), stream())
+    return out
