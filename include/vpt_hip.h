@@ -52,6 +52,18 @@ int vpt_gemm_set_debug(unsigned long long* buf);
  * items. Benchmark/test hook for the grid size (0 = default, 256 = one block per CU). */
 int vpt_gemm_set_ring_grid(int blocks);
 
+/* Fused SwiGLU MLP GEMMs (src/models/jit/denoiser.py:480-506 SwiGLU, :535-543 FinalLayer):
+ * forward: x12 [M][2F] = x.W12^T + b12 (W12 = w_1 | w_2 rows, [2F][K]) and h [M][F] =
+ * bf16(bf16(silu(x1)) * x2) from one GEMM (the epilogue pairs x1 / x2 columns);
+ * backward: dx12 [M][2F] from dh = dy.W3 (dy [M][D], W3 [D][F]) and x12, the SwiGLU derivative applied
+ * in the dgrad epilogue (dh never reaches memory). Small shapes run the plain GEMM + the elementwise
+ * kernel (backward: dh in `workspace`, vpt_gemm_swiglu_bwd_workspace bytes, 0 when not needed). */
+int vpt_gemm_swiglu_fwd(const void* x, long ldx, const void* w12, long ldw, const void* b12, void* x12, long ldx12,
+                        void* h, long ldh, int M, int F, int K, void* stream);
+long vpt_gemm_swiglu_bwd_workspace(int M, int F, int D);
+int vpt_gemm_swiglu_bwd(const void* dy, long lddy, const void* w3, long ldw3, const void* x12, long ldx12, void* dx12,
+                        long lddx12, int M, int F, int D, void* workspace, void* stream);
+
 /* ---- flash attention, head_dim 64 ---------------------------------------------------------
  * Tensors addressed p[b*sb + h*sh + row*sr + d]; n query rows, nk key rows (nk = n for
  * self-attention; SDXL cross-attention nk = context length). Keys < n_dense always valid; keys in

@@ -44,6 +44,11 @@ struct GemmArgs {
   int splits;               // split-K slices (ring kernel work items = tiles * splits)
   float alpha;              // output scale applied to the accumulator before bias (LoRA alpha / rank)
   unsigned long long* dbg;  // stamp-diagnostic output (geometry 2566 only)
+  // fused SwiGLU (ring kernel only): sw = 1 forward (C = x12 [M][2F], C2 = h [M][F]; N = 2F, B = W1|W2),
+  // sw = 2 backward of the W3 dgrad (C = dx12 [M][2F], aux = x12; N = F)
+  int sw;
+  bf16_t* C2; long ldc2;
+  const bf16_t* aux; long ldaux;
 };
 
 // ---- LDS images -----------------------------------------------------------------------------
@@ -447,6 +452,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 // after the tile) still allowed in flight: S = 16 (bf16 output) or 32 (f32).
 __device__ __forceinline__ void wait_vm_pend(int S) {
   if (S == 16) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if (S == 24) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
 }
 
@@ -456,7 +462,19 @@ struct RingItem {
   uint32_t va0, va1, vb0, vb1;  // loop-invariant per-lane DMA piece offsets of full K tiles
 };
 
-template <bool AK, bool BK_>
+// SW (fused SwiGLU forward): tile rows 0-127 of B are W1 rows c0.., rows 128-255 the matching W2 rows
+// F + c0.. (F = N / 2, c0 = 128 * tile column), so each wave's fragments j = 0, 1 and 2, 3 hold x1 and x2
+// of the same 32 output features; the staged output pairs them in the epilogue.
+__device__ __forceinline__ uint32_t tile_voff_sw(long ld, int c0, int F, int kvalid, int wid, int lane, int i) {
+  const int q = wid * 2 + i;
+  const int row = q * 16 + (lane >> 2);
+  int c = (lane & 3) ^ (((row >> 2) & 1) << 1);
+  c = c * 8 < kvalid ? c : 0;
+  const int srow = row < 128 ? c0 + row : F + c0 + row - 128;
+  return (uint32_t)(((long)srow * ld + c * 8) * 2);
+}
+
+template <bool AK, bool BK_, int SW = 0>
 __device__ __forceinline__ RingItem ring_item(const GemmArgs& g, int item, int items, int tiles, int tiles_n, int wid,
                                               int lane) {
   const int q8 = items >> 3, r8 = items & 7, xcd = item & 7;
@@ -465,20 +483,25 @@ __device__ __forceinline__ RingItem ring_item(const GemmArgs& g, int item, int i
   it.split = wgid / tiles;
   const int tile = wgid - it.split * tiles;
   it.m0 = tile / tiles_n * 256;
-  it.n0 = tile % tiles_n * 256;
+  it.n0 = tile % tiles_n * (SW ? 128 : 256);  // SW: first output feature of the tile
   it.kbeg = it.split * g.k_split;
   it.kend = min(g.K, it.kbeg + g.k_split);
   it.nk = (it.kend - it.kbeg + RBK - 1) / RBK;
   it.klast = it.kend - it.kbeg - (it.nk - 1) * RBK;  // valid k of the last tile (1..32)
   it.va0 = tile_voff<AK, 256>(g.lda, it.m0, g.M, RBK, wid, lane, 0);
   it.va1 = tile_voff<AK, 256>(g.lda, it.m0, g.M, RBK, wid, lane, 1);
-  it.vb0 = tile_voff<BK_, 256>(g.ldb, it.n0, g.N, RBK, wid, lane, 0);
-  it.vb1 = tile_voff<BK_, 256>(g.ldb, it.n0, g.N, RBK, wid, lane, 1);
+  if (SW) {
+    it.vb0 = tile_voff_sw(g.ldb, it.n0, g.N / 2, RBK, wid, lane, 0);
+    it.vb1 = tile_voff_sw(g.ldb, it.n0, g.N / 2, RBK, wid, lane, 1);
+  } else {
+    it.vb0 = tile_voff<BK_, 256>(g.ldb, it.n0, g.N, RBK, wid, lane, 0);
+    it.vb1 = tile_voff<BK_, 256>(g.ldb, it.n0, g.N, RBK, wid, lane, 1);
+  }
   return it;
 }
 
 // K tile t of item `it` by LDS-DMA into ring stage t % 4: 4 pieces per wave (A: 2, B: 2).
-template <bool AK, bool BK_>
+template <bool AK, bool BK_, int SW = 0>
 __device__ __forceinline__ void ring_issue(const GemmArgs& g, const RingItem& it, int t, uint32_t lds0, int wid,
                                            int lane) {
   constexpr int A32 = 256 * RBK * 2, STAGE32 = 2 * A32;
@@ -486,9 +509,13 @@ __device__ __forceinline__ void ring_issue(const GemmArgs& g, const RingItem& it
   const int k0 = it.kbeg + t * RBK;
   const int kv = min(RBK, it.kend - k0);
   const void* ab = uniform_ptr(tile_ptr<AK>(g.A, g.lda, it.m0, k0));
-  const void* bb = uniform_ptr(tile_ptr<BK_>(g.B, g.ldb, it.n0, k0));
+  const void* bb = uniform_ptr(tile_ptr<BK_>(g.B, g.ldb, SW ? 0 : it.n0, k0));
   if (kv == RBK) {
     glds_step(ab, bb, it.va0, it.va1, it.vb0, it.vb1, la, la + 1024, la + A32, la + A32 + 1024);
+  } else if (SW) {
+    glds_step(ab, bb, tile_voff<AK, 256>(g.lda, it.m0, g.M, kv, wid, lane, 0),
+              tile_voff<AK, 256>(g.lda, it.m0, g.M, kv, wid, lane, 1), tile_voff_sw(g.ldb, it.n0, g.N / 2, kv, wid, lane, 0),
+              tile_voff_sw(g.ldb, it.n0, g.N / 2, kv, wid, lane, 1), la, la + 1024, la + A32, la + A32 + 1024);
   } else {
     glds_step(ab, bb, tile_voff<AK, 256>(g.lda, it.m0, g.M, kv, wid, lane, 0),
               tile_voff<AK, 256>(g.lda, it.m0, g.M, kv, wid, lane, 1),
@@ -504,7 +531,12 @@ __device__ __forceinline__ void ring_issue(const GemmArgs& g, const RingItem& it
 // num_records and columns past N carry an offset past it, so the hardware drops them without a
 // branch: every wave issues exactly ring_stores(out_mode) store instructions, which the next item's
 // counted vmcnt waits rely on (stores are younger than that item's first three K tiles).
-__device__ __forceinline__ int ring_stores(int out_mode) { return out_mode == OUT_BF16 ? 16 : 32; }
+__device__ __forceinline__ int ring_stores(const GemmArgs& g) {
+  if (g.sw == 1) return 24;  // x1, x2, h per lane and fragment
+  if (g.sw == 2) return 32;  // dx1, dx2 per lane, fragment and half
+  return g.out_mode == OUT_BF16 ? 16 : 32;
+}
+__device__ __forceinline__ float silu_ref(float x) { return x / (1.f + expf(-x)); }
 __device__ __forceinline__ int stg_off(int row, int col) {
   return row * 256 + (((col >> 2) ^ (row & 1)) << 4) + ((col & 3) << 2);
 }
@@ -530,6 +562,12 @@ __device__ __forceinline__ void epilogue_ring(const GemmArgs& g, const floatx4 (
                                                                        g.resid ? rows_here * (int)g.ldr * 2 : 0, 0x00020000);
   const int rrstride = (int)g.ldr * 2;
   const uint32_t rvoff = col_ok ? (uint32_t)((lrow * (int)g.ldr + tcol) * 2) : 0x80000000u;
+  // fused SwiGLU backward: x12 rows of this tile (bf16, leading dim ldaux)
+  const bf16_t* abase = g.aux ? g.aux + (long)it.m0 * g.ldaux + it.n0 : g.aux;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)abase, (short)0,
+                                                                       g.aux ? rows_here * (int)g.ldaux * 2 : 0, 0x00020000);
+  const int rastride = (int)g.ldaux * 2;
+  const uint32_t avoff = col_ok ? (uint32_t)((lrow * (int)g.ldaux + tcol) * 2) : 0x80000000u;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
 #pragma unroll
@@ -552,7 +590,29 @@ __device__ __forceinline__ void epilogue_ring(const GemmArgs& g, const floatx4 (
         for (int e = 0; e < 8; ++e) o[e] = o[e] / (1.f + __expf(-o[e]));
       }
       const int soff = (i * 16 + p * 8) * rstride;
-      if (g.out_mode == OUT_BF16) {
+      if (g.sw == 2) {
+        // fused SwiGLU backward (the reference's SwiGLU autograd, denoiser.py:480-506, as swiglu_bwd_kernel):
+        // o = dh; x1, x2 from x12; dx1 -> column c, dx2 -> column F + c of dx12 (F = N)
+        const u32x4 a4 = __builtin_amdgcn_raw_buffer_load_b128(ra, (int)avoff, (i * 16 + p * 8) * rastride, 0);
+        const u32x4 b4 = __builtin_amdgcn_raw_buffer_load_b128(ra, (int)(col_ok ? avoff + g.N * 2 : avoff),
+                                                               (i * 16 + p * 8) * rastride, 0);
+        float a[8], b[8], d1[8], d2[8];
+        unpack8(make_uint4(a4[0], a4[1], a4[2], a4[3]), a);
+        unpack8(make_uint4(b4[0], b4[1], b4[2], b4[3]), b);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float gd = bf2f(f2bf(o[e]));  // dh is a bf16 tensor in the reference
+          const float sg = 1.f / (1.f + expf(-a[e]));
+          const float sv = bf2f(f2bf(a[e] * sg));
+          const float ds = bf2f(f2bf(gd * b[e]));
+          d2[e] = gd * sv;
+          d1[e] = ds * (sg * (1.f + a[e] * (1.f - sg)));
+        }
+        const uint4 w1 = pack8(d1), w2 = pack8(d2);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{w1.x, w1.y, w1.z, w1.w}, rs, (int)voff, soff, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{w2.x, w2.y, w2.z, w2.w}, rs, (int)(col_ok ? voff + g.N * 2 : voff),
+                                               soff, 0);
+      } else if (g.out_mode == OUT_BF16) {
         if (g.resid) {
           // reference semantics: residual + bf16(linear output), rounded again to bf16. Buffer load over
           // the tile's residual rows: out-of-range rows / columns read 0 (their stores are dropped).
@@ -582,6 +642,55 @@ __device__ __forceinline__ void epilogue_ring(const GemmArgs& g, const floatx4 (
   }
 }
 
+// Fused SwiGLU forward epilogue (SW): per 16-row fragment, stage as epilogue_ring (staged columns 0-31 =
+// x1, 32-63 = x2 of the same 32 features), then each lane takes one row and 8 features: x1, x2 = bf16(acc
+// + bias) stored to x12 (columns c and F + c) and h = bf16(bf16(silu(x1)) * x2) to C2 (column c) -- the
+// reference's SwiGLU (denoiser.py:480-506) with the same roundings as swiglu_fwd_kernel. 24 stores per wave.
+__device__ __forceinline__ void epilogue_ring_swf(const GemmArgs& g, const floatx4 (&acc)[8][4], char* stg, int lane,
+                                                  const RingItem& it, int wm, int wn, const float (&b1)[8],
+                                                  const float (&b2)[8]) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const int F = g.N / 2;
+  const int rows_here = min(256, g.M - it.m0);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (char*)g.C + (long)it.m0 * g.ldc * 2, (short)0, rows_here * (int)g.ldc * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
+      (char*)g.C2 + (long)it.m0 * g.ldc2 * 2, (short)0, rows_here * (int)g.ldc2 * 2, 0x00020000);
+  const int q = lane & 3, lr = lane >> 2;     // 8-feature chunk, fragment row
+  const int col = it.n0 + wn * 32 + q * 8;     // first output feature of the lane
+  const int lrow = wm * 128 + lr;
+  const uint32_t vx = (uint32_t)((lrow * (int)g.ldc + col) * 2);
+  const uint32_t vh = (uint32_t)((lrow * (int)g.ldc2 + col) * 2);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        *reinterpret_cast<float*>(stg + stg_off((lane >> 4) * 4 + r, j * 16 + (lane & 15))) = acc[i][j][r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own-wave LDS writes retired
+    __builtin_amdgcn_wave_barrier();
+    const floatx4 a0 = *reinterpret_cast<const floatx4*>(stg + stg_off(lr, q * 8));
+    const floatx4 a1 = *reinterpret_cast<const floatx4*>(stg + stg_off(lr, q * 8 + 4));
+    const floatx4 c0 = *reinterpret_cast<const floatx4*>(stg + stg_off(lr, 32 + q * 8));
+    const floatx4 c1 = *reinterpret_cast<const floatx4*>(stg + stg_off(lr, 32 + q * 8 + 4));
+    float x1[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    float x2[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+    float hv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      x1[e] = bf2f(f2bf(x1[e] * g.alpha + b1[e]));
+      x2[e] = bf2f(f2bf(x2[e] * g.alpha + b2[e]));
+      hv[e] = bf2f(f2bf(silu_ref(x1[e]))) * x2[e];
+    }
+    const int soff = i * 16 * (int)g.ldc * 2, soffh = i * 16 * (int)g.ldc2 * 2;
+    const uint4 w1 = pack8(x1), w2 = pack8(x2), wh = pack8(hv);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{w1.x, w1.y, w1.z, w1.w}, rs, (int)vx, soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{w2.x, w2.y, w2.z, w2.w}, rs, (int)(vx + F * 2), soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{wh.x, wh.y, wh.z, wh.w}, rh, (int)vh, soffh, 0);
+  }
+}
+
 // STAMP (diagnostic build, geometry 2566): per-wave cycle sums of the K-step segments (DMA issue,
 // ds_reads, vmcnt wait, barrier Y, MFMA issue, barrier X) to g.dbg[(block*8 + wave)*8 + seg]; read the
 // shares, not the length (the stamps' lgkmcnt(0) forbids overlaps the real kernel has).
@@ -600,7 +709,7 @@ __device__ __forceinline__ void tl_stamp(const GemmArgs& g, int k, int phase, in
     g.dbg[((long)blockIdx.x * 4 + k) * 4 + phase] = __builtin_amdgcn_s_memrealtime();
 }
 
-template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false, bool STAMP = false, bool TL = false>
+template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false, bool STAMP = false, bool TL = false, int SW = 0>
 __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
   using G = GR;
   constexpr int A32 = 256 * RBK * 2, STAGE32 = 2 * A32;
@@ -613,14 +722,14 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
   const int items = tiles * g.splits;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(VPT_LDS char*)smem + wid * 2048;
   char* stg = smem + 3 * STAGE32 + wid * 4096;  // this wave's epilogue staging slice (ring stage 3)
-  const int S = ring_stores(g.out_mode);
+  const int S = ring_stores(g);
 
   int item = blockIdx.x;
   if (item >= items) return;
-  RingItem it = ring_item<AK, BK_>(g, item, items, tiles, tiles_n, wid, lane);
-  ring_issue<AK, BK_>(g, it, 0, lds0, wid, lane);
-  if (it.nk > 1) ring_issue<AK, BK_>(g, it, 1, lds0, wid, lane);
-  if (it.nk > 2) ring_issue<AK, BK_>(g, it, 2, lds0, wid, lane);
+  RingItem it = ring_item<AK, BK_, SW>(g, item, items, tiles, tiles_n, wid, lane);
+  ring_issue<AK, BK_, SW>(g, it, 0, lds0, wid, lane);
+  if (it.nk > 1) ring_issue<AK, BK_, SW>(g, it, 1, lds0, wid, lane);
+  if (it.nk > 2) ring_issue<AK, BK_, SW>(g, it, 2, lds0, wid, lane);
   int pend = 0;  // epilogue stores younger than this item's pre-issued tiles 0-2 (0 on the first item)
   int kth = 0;   // items done by this block (TL stamps)
 
@@ -629,9 +738,17 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
     const int nk = it.nk;
     // bias of this item's 8 output columns (plain load; consumed after the K loop, when nothing is
     // outstanding, so the compiler's wait for it costs nothing)
-    uint4 braw = make_uint4(0, 0, 0, 0);
-    const int bcol = it.n0 + wn * 64 + (lane & 7) * 8;
-    if (g.bias && bcol < g.N) braw = *reinterpret_cast<const uint4*>(g.bias + bcol);
+    uint4 braw = make_uint4(0, 0, 0, 0), braw2 = make_uint4(0, 0, 0, 0);
+    if (SW) {  // bias of the lane's 8 features in both halves (W1 at c, W2 at F + c)
+      const int c = it.n0 + wn * 32 + (lane & 3) * 8;
+      if (g.bias) {
+        braw = *reinterpret_cast<const uint4*>(g.bias + c);
+        braw2 = *reinterpret_cast<const uint4*>(g.bias + g.N / 2 + c);
+      }
+    } else {
+      const int bcol = it.n0 + wn * 64 + (lane & 7) * 8;
+      if (g.bias && bcol < g.N) braw = *reinterpret_cast<const uint4*>(g.bias + bcol);
+    }
 
     floatx4 acc[G::MI][G::NI];
 #pragma unroll
@@ -650,11 +767,12 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
       const char* st = smem + (kt & (RSTAGES - 1)) * STAGE32;
       unsigned long long t0 = 0, t1 = 0;
       if (STAMP) t0 = stamp();
-      if (!DMAC && ABL != 1 && kt + 3 < nk) ring_issue<AK, BK_>(g, it, kt + 3, lds0, wid, lane);
+      if (!DMAC && ABL != 1 && kt + 3 < nk) ring_issue<AK, BK_, SW>(g, it, kt + 3, lds0, wid, lane);
       if (STAMP) { t1 = stamp(); seg[0] += t1 - t0; t0 = t1; }
       bf16x8 bfr[G::NI], af[G::MI];
 #pragma unroll
-      for (int j = 0; j < G::NI; ++j) bfr[j] = read_frag32<BK_, 256>(st + A32, wn * G::WC + j * 16, lane);
+      for (int j = 0; j < G::NI; ++j)
+        bfr[j] = read_frag32<BK_, 256>(st + A32, SW ? ((j & 2) << 6) + wn * 32 + (j & 1) * 16 : wn * G::WC + j * 16, lane);
 #pragma unroll
       for (int i = 0; i < G::MI; ++i) af[i] = read_frag32<AK, 256>(st, wm * G::WR + i * 16, lane);
       if (kt == nk - 1 && it.klast < RBK) {
@@ -670,7 +788,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
       if (STAMP) { t1 = stamp(); seg[2] += t1 - t0; t0 = t1; }
       if (DMAC) bare_barrier(); else raw_barrier();                // Y_kt
       if (STAMP) { t1 = stamp(); seg[3] += t1 - t0; t0 = t1; }
-      if (DMAC && ABL != 1 && kt + 3 < nk) ring_issue<AK, BK_>(g, it, kt + 3, lds0, wid, lane);
+      if (DMAC && ABL != 1 && kt + 3 < nk) ring_issue<AK, BK_, SW>(g, it, kt + 3, lds0, wid, lane);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < G::MI; ++i)
@@ -690,19 +808,21 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
     }
     if (PP && wm == 0) raw_barrier();
     if (TL) tl_stamp(g, kth, 2, wid, lane);
-    float bias8[8];
+    float bias8[8], bias8b[8];
     unpack8(braw, bias8);
+    unpack8(braw2, bias8b);
     // Every wave has passed its last K step (barrier X_nk), so ring stages 0-2 are free: DMA the next
     // item's first tiles before this item's epilogue (which stages through stage 3 only).
     const int next = item + gridDim.x;
     RingItem nx;
     if (next < items) {
-      nx = ring_item<AK, BK_>(g, next, items, tiles, tiles_n, wid, lane);
-      ring_issue<AK, BK_>(g, nx, 0, lds0, wid, lane);
-      if (nx.nk > 1) ring_issue<AK, BK_>(g, nx, 1, lds0, wid, lane);
-      if (nx.nk > 2) ring_issue<AK, BK_>(g, nx, 2, lds0, wid, lane);
+      nx = ring_item<AK, BK_, SW>(g, next, items, tiles, tiles_n, wid, lane);
+      ring_issue<AK, BK_, SW>(g, nx, 0, lds0, wid, lane);
+      if (nx.nk > 1) ring_issue<AK, BK_, SW>(g, nx, 1, lds0, wid, lane);
+      if (nx.nk > 2) ring_issue<AK, BK_, SW>(g, nx, 2, lds0, wid, lane);
     }
-    epilogue_ring(g, acc, stg, lane, it, wm, wn, bias8);
+    if (SW) epilogue_ring_swf(g, acc, stg, lane, it, wm, wn, bias8, bias8b);
+    else epilogue_ring(g, acc, stg, lane, it, wm, wn, bias8);
     if (TL) tl_stamp(g, kth, 3, wid, lane);
     ++kth;
     if (next >= items) break;
@@ -724,12 +844,12 @@ int launch(const GemmArgs& g, int splits, hipStream_t s) {
   return VPT_OK;
 }
 
-template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false, bool STAMP = false, bool TL = false>
+template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false, bool STAMP = false, bool TL = false, int SW = 0>
 int launch_ring(const GemmArgs& g, int splits, hipStream_t s) {
   constexpr int LDS = RSTAGES * 2 * 256 * RBK * 2;  // the epilogue stages through ring stage 3
   const int items = ((g.M + 255) / 256) * ((g.N + 255) / 256) * splits;
   const int grid = items < g_ring_grid ? items : g_ring_grid;
-  hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL>), dim3(grid), dim3(512), LDS, s, g);
+  hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, SW>), dim3(grid), dim3(512), LDS, s, g);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
@@ -792,7 +912,7 @@ extern "C" int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* 
   VPT_CHECK_ARG(out_mode >= 0 && out_mode <= 2, "vpt_gemm_bf16: bad out_mode");
   VPT_CHECK_ARG(!resid || out_mode == OUT_BF16, "vpt_gemm_bf16: residual only with bf16 output");
   if (splits < 1) splits = 1;
-  GemmArgs g;
+  GemmArgs g = {};
   g.A = (const bf16_t*)A; g.lda = lda;
   g.B = (const bf16_t*)B; g.ldb = ldb;
   g.bias = (const bf16_t*)bias;
@@ -862,4 +982,72 @@ extern "C" int vpt_gemm_set_ring_grid(int blocks) {
 extern "C" int vpt_gemm_set_debug(unsigned long long* buf) {
   g_dbg = buf;
   return VPT_OK;
+}
+
+// ---- fused SwiGLU GEMMs (the JiT MLP, denoiser.py:480-506; FinalLayer 535-543) ---------------------
+extern "C" int vpt_swiglu_fwd(const void* x12, long M, int F, void* h, void* stream);
+extern "C" int vpt_swiglu_bwd(const void* dh, const void* x12, long M, int F, void* dx12, void* stream);
+
+static bool swiglu_ring_ok(int M, int N) {
+  if (g_geo_override && g_geo_override != 256) return false;
+  return N % 256 == 0 && ((long)((M + 255) / 256) * (N / 256) >= 160 || g_geo_override == 256);
+}
+
+// x12 [M][2F] = x . W12^T + b12 (W12 = W1 | W2 [2F][K]) and h [M][F] = bf16(silu(x1)) * x2, from one ring
+// GEMM whose epilogue pairs x1 / x2 (small shapes: the plain GEMM + vpt_swiglu_fwd, same roundings).
+extern "C" int vpt_gemm_swiglu_fwd(const void* x, long ldx, const void* w12, long ldw, const void* b12, void* x12,
+                                   long ldx12, void* h, long ldh, int M, int F, int K, void* stream) {
+  VPT_CHECK_ARG(x && w12 && x12 && h, "vpt_gemm_swiglu_fwd: null pointer");
+  VPT_CHECK_ARG(M > 0 && F > 0 && K > 0 && F % 8 == 0 && K % 8 == 0, "vpt_gemm_swiglu_fwd: bad shape");
+  if (!swiglu_ring_ok(M, 2 * F) || ldx12 != 2 * F || ldh != F) {
+    int rc = vpt_gemm_bf16(x, ldx, 1, w12, ldw, 1, x12, ldx12, M, 2 * F, K, b12, nullptr, 0, OUT_BF16, ACT_NONE, 1,
+                           nullptr, 1.f, stream);
+    if (rc) return rc;
+    VPT_CHECK_ARG(ldx12 == 2 * F && ldh == F, "vpt_gemm_swiglu_fwd: dense x12 / h required");
+    return vpt_swiglu_fwd(x12, M, F, h, stream);
+  }
+  VPT_CHECK_ARG(ldx % 8 == 0 && ldw % 8 == 0, "vpt_gemm_swiglu_fwd: leading dims must be 16B multiples");
+  GemmArgs g = {};
+  g.A = (const bf16_t*)x; g.lda = ldx;
+  g.B = (const bf16_t*)w12; g.ldb = ldw;
+  g.C = x12; g.ldc = ldx12;
+  g.C2 = (bf16_t*)h; g.ldc2 = ldh;
+  g.bias = (const bf16_t*)b12;
+  g.M = M; g.N = 2 * F; g.K = K;
+  g.k_split = K; g.splits = 1;
+  g.out_mode = OUT_BF16; g.act = ACT_NONE; g.alpha = 1.f;
+  g.sw = 1;
+  return launch_ring<true, true, true, 0, false, false, false, 1>(g, 1, (hipStream_t)stream);
+}
+
+extern "C" long vpt_gemm_swiglu_bwd_workspace(int M, int F, int D) {
+  (void)D;
+  return swiglu_ring_ok(M, F) ? 0 : (long)M * F * 2;
+}
+
+// dx12 [M][2F] = SwiGLU backward of dh = dy . W3 (dy [M][D], W3 [D][F]) against x12, from one ring dgrad
+// whose epilogue applies the SwiGLU derivative (small shapes: dgrad into `workspace` + vpt_swiglu_bwd).
+extern "C" int vpt_gemm_swiglu_bwd(const void* dy, long lddy, const void* w3, long ldw3, const void* x12, long ldx12,
+                                   void* dx12, long lddx12, int M, int F, int D, void* workspace, void* stream) {
+  VPT_CHECK_ARG(dy && w3 && x12 && dx12, "vpt_gemm_swiglu_bwd: null pointer");
+  VPT_CHECK_ARG(M > 0 && F > 0 && D > 0 && F % 8 == 0 && D % 8 == 0, "vpt_gemm_swiglu_bwd: bad shape");
+  if (!swiglu_ring_ok(M, F) || ldx12 != 2 * F || lddx12 != 2 * F) {
+    VPT_CHECK_ARG(workspace != nullptr, "vpt_gemm_swiglu_bwd: workspace required (vpt_gemm_swiglu_bwd_workspace)");
+    VPT_CHECK_ARG(ldx12 == 2 * F && lddx12 == 2 * F, "vpt_gemm_swiglu_bwd: dense x12 / dx12 required");
+    int rc = vpt_gemm_bf16(dy, lddy, 1, w3, ldw3, 0, workspace, F, M, F, D, nullptr, nullptr, 0, OUT_BF16, ACT_NONE, 1,
+                           nullptr, 1.f, stream);
+    if (rc) return rc;
+    return vpt_swiglu_bwd(workspace, x12, M, F, dx12, stream);
+  }
+  VPT_CHECK_ARG(lddy % 8 == 0 && ldw3 % 8 == 0, "vpt_gemm_swiglu_bwd: leading dims must be 16B multiples");
+  GemmArgs g = {};
+  g.A = (const bf16_t*)dy; g.lda = lddy;
+  g.B = (const bf16_t*)w3; g.ldb = ldw3;
+  g.C = dx12; g.ldc = lddx12;
+  g.aux = (const bf16_t*)x12; g.ldaux = ldx12;
+  g.M = M; g.N = F; g.K = D;
+  g.k_split = D; g.splits = 1;
+  g.out_mode = OUT_BF16; g.act = ACT_NONE; g.alpha = 1.f;
+  g.sw = 2;
+  return launch_ring<true, false, true>(g, 1, (hipStream_t)stream);
 }

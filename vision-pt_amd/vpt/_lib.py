@@ -26,6 +26,9 @@ SIGNATURES: dict[str, list] = {
     "vpt_gemm_set_geometry": [I],
     "vpt_gemm_set_debug": [P],
     "vpt_gemm_set_ring_grid": [I],
+    "vpt_gemm_swiglu_fwd": [P, L, P, L, P, P, L, P, L, I, I, I, P],
+    "vpt_gemm_swiglu_bwd_workspace": [I, I, I],
+    "vpt_gemm_swiglu_bwd": [P, L, P, L, P, L, P, L, I, I, I, P, P],
     "vpt_attn_fwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, P, L, I, I, I, I, I, F, P],
     "vpt_attn_bwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, P, L, L, P, L,
                      P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, I, F, P],
@@ -78,12 +81,13 @@ SIGNATURES: dict[str, list] = {
 _RESTYPES = {
     "vpt_gemm_workspace_bytes": C.c_long,
     "vpt_cover_resize_crop_workspace": C.c_long,
+    "vpt_gemm_swiglu_bwd_workspace": C.c_long,
     "vpt_attn_q_scale": C.c_float,
     "vpt_last_error_string": C.c_char_p,
     "vpt_build_info": C.c_char_p,
 }
 # Entry points that return a value (size / count / string) rather than a status code.
-_VALUE_FNS = {"vpt_gemm_workspace_bytes", "vpt_cover_resize_crop_workspace", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
+_VALUE_FNS = {"vpt_gemm_workspace_bytes", "vpt_cover_resize_crop_workspace", "vpt_gemm_swiglu_bwd_workspace", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
               "vpt_colsum_blocks", "vpt_attn_q_scale", "vpt_last_error_string", "vpt_abi_version", "vpt_build_info"}
 
 

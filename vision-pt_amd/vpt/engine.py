@@ -202,8 +202,8 @@ class JiTEngine:
                          ops._t4(o, B, rows, Hh, 0), lse, kbias, B, Hh, rows, n_i, n_pre, 1.0 / math.sqrt(cfg.head_dim))
             xm = ops.linear(o, w["pwo"], w["pbo"], resid=x, out=pool.get(tag + "xm", (M, D)))
             xn2, rstd2 = ops.rmsnorm_fwd(xm, w["pn2"], pool.get(tag + "xn2", (M, D)), pool.get(tag + "rstd2", (M,), F32))
-            x12 = ops.linear(xn2, w["pw12"], w["pb12"], out=pool.get(tag + "x12", (M, 2 * F)))
-            h = ops.swiglu_fwd(x12, pool.get(tag + "h", (M, F)))
+            x12, h = ops.linear_swiglu(xn2, w["pw12"], w["pb12"], pool.get(tag + "x12", (M, 2 * F)),
+                                       pool.get(tag + "h", (M, F)))
             x_next = pool.get(f"x{i + 1}" if save else ("xa" if i % 2 == 0 else "xb"), (M, D))
             ops.linear(h, w["pw3"], w["pb3"], resid=xm, out=x_next)
             x = x_next
@@ -212,8 +212,7 @@ class JiTEngine:
         M2 = B * np_
         xf = ops.copy_rows(x, rows, 0, np_, pool.get("xf", (M2, D)), B)
         xnf, rstdf = ops.rmsnorm_fwd(xf, f["pn"], pool.get("xnf", (M2, D)), pool.get("rstdf", (M2,), F32))
-        f12 = ops.linear(xnf, f["pw12"], f["pb12"], out=pool.get("f12", (M2, 2 * F)))
-        fh = ops.swiglu_fwd(f12, pool.get("fh", (M2, F)))
+        f12, fh = ops.linear_swiglu(xnf, f["pw12"], f["pb12"], pool.get("f12", (M2, 2 * F)), pool.get("fh", (M2, F)))
         f3 = ops.linear(fh, f["pw3"], f["pb3"], out=pool.get("f3", (M2, D)))
         out = ops.linear(f3, f["pwl"], f["pbl"], out=pool.get("out", (M2, f["pwl"].shape[0])))
         self._state = dict(B=B, H=H, W=W, np_=np_, rows=rows, n_ctx=n_ctx, n_pre=n_pre, M=M, kbias=kbias,
@@ -264,8 +263,8 @@ class JiTEngine:
         df3 = ops.linear_dgrad(dout, f["pwl"], out=pool.get("d_a", (M2, D)))
         wgrad(df3, fh, f["gw3"])
         bgrad(df3, f["gb3"])
-        dfh = ops.linear_dgrad(df3, f["pw3"], out=pool.get("d_h", (M2, F)))
-        df12 = ops.swiglu_bwd(dfh, f12, pool.get("d_x12", (M2, 2 * F)))
+        df12 = ops.linear_dgrad_swiglu(df3, f["pw3"], f12, pool.get("d_x12", (M2, 2 * F)),
+                                       workspace=pool.get("d_h", (M2, F)))
         wgrad(df12, xnf, f["gw12"])
         bgrad(df12, f["gb12"])
         dxnf = ops.linear_dgrad(df12, f["pw12"], out=pool.get("d_b", (M2, D)))
@@ -301,8 +300,8 @@ class JiTEngine:
             # MLP
             wgrad(dx, h, w["gw3"])
             bgrad(dx, w["gb3"])
-            dh = ops.linear_dgrad(dx, w["pw3"], out=pool.get("d_h", (M, F)))
-            dx12 = ops.swiglu_bwd(dh, x12, pool.get("d_x12", (M, 2 * F)))
+            dx12 = ops.linear_dgrad_swiglu(dx, w["pw3"], x12, pool.get("d_x12", (M, 2 * F)),
+                                           workspace=pool.get("d_h", (M, F)))
             wgrad(dx12, xn2, w["gw12"])
             bgrad(dx12, w["gb12"])
             dxn2 = ops.linear_dgrad(dx12, w["pw12"], out=pool.get("d_b", (M, D)))

@@ -121,6 +121,45 @@ def linear_wgrad(dy, x, out, accumulate=False, splits=1, workspace=None):
                 splits=splits, workspace=workspace)
 
 
+def linear_swiglu(x, w12, b12, x12, h):
+    """x12 = x @ w12.T + b12 and h = bf16(silu(x1)) * x2 (SwiGLU, denoiser.py:480-506) in one GEMM."""
+    M, K = x.shape
+    F = w12.shape[0] // 2
+    for t, n in ((x, "x"), (w12, "w12"), (x12, "x12"), (h, "h")):
+        _chk(t, BF16, n)
+
+    def run():
+        call("vpt_gemm_swiglu_fwd", x.data_ptr(), x.stride(0), w12.data_ptr(), w12.stride(0), _p(b12), x12.data_ptr(),
+             x12.stride(0), h.data_ptr(), h.stride(0), M, F, K, stream())
+    pr = PROBES.get("gemm")
+    if pr is None:
+        run()
+    else:
+        pr.record(2.0 * M * 2 * F * K, run)
+    return x12, h
+
+
+def linear_dgrad_swiglu(dy, w3, x12, dx12, workspace=None):
+    """dx12 = SwiGLU backward of (dy @ w3) against x12 (dh stays in registers on the fused path)."""
+    M, D = dy.shape
+    F = w3.shape[1]
+    for t, n in ((dy, "dy"), (w3, "w3"), (x12, "x12"), (dx12, "dx12")):
+        _chk(t, BF16, n)
+    need = int(call("vpt_gemm_swiglu_bwd_workspace", M, F, D))
+    if need and (workspace is None or workspace.numel() * workspace.element_size() < need):
+        workspace = torch.empty(M * F, dtype=BF16, device=dy.device)
+
+    def run():
+        call("vpt_gemm_swiglu_bwd", dy.data_ptr(), dy.stride(0), w3.data_ptr(), w3.stride(0), x12.data_ptr(),
+             x12.stride(0), dx12.data_ptr(), dx12.stride(0), M, F, D, _p(workspace) if need else None, stream())
+    pr = PROBES.get("gemm")
+    if pr is None:
+        run()
+    else:
+        pr.record(2.0 * M * F * D, run)
+    return dx12
+
+
 def wgrad_splits(N: int, K: int, M: int) -> int:
     """Split-K factor for a weight gradient dW[N,K] = dy[M,N]^T x[M,K] (reduction over M tokens).
 
