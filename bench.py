@@ -98,7 +98,7 @@ def cpu_baseline(budget_s: float = 20.0):
         opt.step()
         opt.zero_grad()
 
-    one(256, 256)  # warm-up (allocator, threads)
+    one(*BUCKETS[0])  # warm-up at the sample's own size (allocator, threads)
     n, t0 = 0, time.perf_counter()
     while True:
         W, H = BUCKETS[n % len(BUCKETS)]
@@ -131,7 +131,7 @@ def main():
 
     from vpt import ops
     from vpt.config import JiT_B_16_Config, JiTTrainingConfig
-    from vpt.ddp import GradSync, grad_buckets
+    from vpt.ddp import GradSync, LossLog, grad_buckets
     from vpt.jit_train import JiTTrainer
     from vpt.optim import RAdamScheduleFreeFlat
 
@@ -140,7 +140,9 @@ def main():
     trainer.engine.init_weights(seed=0)  # identical on every rank (replaces DDP's broadcast)
     opt = RAdamScheduleFreeFlat(trainer.engine.params, trainer.engine.grads, lr=1e-4)
     opt.train()
-    sync = GradSync(trainer.engine.grads, grad_buckets(trainer.engine.layout, cfg.depth))
+    # bf16 wire: the reference's DDP all-reduces the bf16 .grad tensors of its bf16 parameters
+    sync = GradSync(trainer.engine.grads, grad_buckets(trainer.engine.layout, cfg.depth), wire="bf16")
+    losslog = LossLog(device)
     batches = make_batches(args.batch, device, seed=100 + rank)
     order = torch.randperm(len(BUCKETS), generator=torch.Generator().manual_seed(7)).tolist()
 
@@ -151,17 +153,15 @@ def main():
         s = opt.begin_step()
         if world > 1:
             sync.launch_rest()
-            sync.finish(lambda lo, hi, sc: opt.apply_range(s, lo, hi, sc))
+            sync.finish(lambda lo, hi, sc, g: opt.apply_range(s, lo, hi, sc, g))
         else:
             opt.apply_range(s, 0, opt.params.numel())
         opt.end_step(s)
+        losslog.push(trainer._loss)  # the reference's per-step loss gather (2-float all-reduce, read later)
 
     for i in range(args.warmup):
         step(i)
-    probes = {k: ops.KernelProbe(k) for k in ("attn_fwd", "attn_bwd", "gemm")}
-    ops.PROBES.update(probes)
-    for p in probes.values():
-        p.active = True
+    # ---- timed region: exactly K steps, no instrumentation
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -172,22 +172,44 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    for p in probes.values():
-        p.active = False
     if world > 1:
         t = torch.tensor([dt], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
-    loss = trainer._loss.item()
+    loss = None
+    while losslog.pending:
+        loss = losslog.pop()  # the last timed step's loss, averaged over ranks
+
+    # ---- probe pass (after the timed region): one round of the 5 buckets with HIP events around every
+    # launch of the MFMA ops (algorithmic FLOPs) and the memory-bound ops (algorithmic HBM bytes)
+    mfma_ops = ("attn_fwd", "attn_bwd", "gemm")
+    hbm_ops = ("rmsnorm_fwd", "rmsnorm_bwd", "qknorm_rope_fwd", "qknorm_rope_bwd", "bias_grad", "patchify",
+               "flow_loss", "radam_sf_step")
+    probes = {k: ops.KernelProbe(k) for k in mfma_ops + hbm_ops}
+    ops.PROBES.update(probes)
+    for p in probes.values():
+        p.active = True
+    n_probe = len(BUCKETS)
+    for i in range(args.warmup + args.steps, args.warmup + args.steps + n_probe):
+        step(i)
+    torch.cuda.synchronize()
+    for p in probes.values():
+        p.active = False
+    ops.PROBES.clear()
 
     imgs = args.batch * args.steps * world
     value = imgs / dt
     # dominant kernel = the probed op with the largest total time inside the timed region
-    stats = {}
-    for k, p in probes.items():
-        n, ms, fl = p.summary()
+    stats, hbm = {}, {}
+    for k in mfma_ops:
+        n, ms, fl = probes[k].summary()
         stats[k] = dict(launches=n, mean_ms=ms, total_ms=n * ms, tflops=(fl / (ms * 1e-3) / 1e12) if ms else 0.0,
                         mean_gflop=fl / 1e9)
+    for k in hbm_ops:
+        n, ms, nb = probes[k].summary()
+        gbs = nb / (ms * 1e-3) / 1e9 if ms else 0.0
+        hbm[k] = dict(launches=n, mean_ms=round(ms, 4), mean_mb=round(nb / 1e6, 3), gb_s=round(gbs, 1),
+                      frac=round(gbs / PEAK_HBM_GBS, 3))
     dom = max(stats, key=lambda k: stats[k]["total_ms"])
     ach = stats[dom]["tflops"]
     traffic, traffic_src = measured_traffic(dom)
@@ -200,13 +222,16 @@ def main():
         "config": {"workload": "JiT-B/16 (JiT_B_16_Config) training step, 1024^2 area, 5 aspect-ratio buckets round-robin",
                    "model": "JiT-B/16", "per_gpu_batch": args.batch, "global_batch": args.batch * world,
                    "seq_len": "4042-4170 tokens", "buckets_wh": BUCKETS, "parallelism": f"dp{world}",
-                   "loss_target": "image", "optimizer": "RAdamScheduleFree (fused HIP)", "grad_checkpointing": False},
+                   "loss_target": "image", "optimizer": "RAdamScheduleFree (fused HIP)",
+                   "grad_allreduce": "bf16 wire, per-block buckets overlapped with backward" if world > 1 else None, "grad_checkpointing": False},
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                      "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
                      "algorithmic_gflop_per_launch": round(stats[dom]["mean_gflop"], 3),
                      "mean_launch_ms": round(stats[dom]["mean_ms"], 4)},
         "kernels": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in stats.items()},
+        "hbm_kernels": hbm,
+        "probe_pass": f"{n_probe} steps after the timed region, HIP events on the launching stream",
         "model_tflops_per_gpu": round(step_tflop * args.steps / (dt) , 2),
         "mfu": round(step_tflop * args.steps / dt / PEAK_BF16_TFLOPS, 4),
         "final_loss": round(loss, 5),

@@ -41,16 +41,14 @@ int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* B, long ldb
                   long ldc, int M, int N, int K, const void* bias, const void* resid, long ldr, int out_mode,
                   int act, int splits, void* workspace, float alpha, void* stream);
 long vpt_gemm_workspace_bytes(int M, int N, int K, int splits);
-/* Tile geometry: 0 = automatic (default); 128 = 128x128 2-stage, 256 = 256x256 ping-pong ring,
- * 2561 = ring unstaggered, 2562 = 256x256 2-stage (benchmarking); 2563/2564 = timing-only ablations
- * of the ring (forward direction only; results are wrong). */
-int vpt_gemm_set_geometry(int geo);
-/* Diagnostic: u64 buffer [256][8][8] receiving per-wave K-step segment cycle sums from the stamped
- * ring build (geometry 2566, forward direction); nullptr disables. */
-int vpt_gemm_set_debug(unsigned long long* buf);
-/* The 256x256 ring kernel is persistent: min(work items, grid) blocks walk (tile, split-K slice)
- * items. Benchmark/test hook for the grid size (0 = default, 256 = one block per CU). */
-int vpt_gemm_set_ring_grid(int blocks);
+/* vpt_gemm_bf16 with an explicit tile geometry (stateless; same results contract): geometry 0 =
+ * automatic, 128 = 128x128 2-stage, 256 = the persistent 256x256 ping-pong ring, whose
+ * min(work items, ring_grid) blocks walk (tile, split-K slice) items (ring_grid 0 = one block per CU).
+ * Used by tests to cover both geometries and multi-item ring walks at small shapes. */
+int vpt_gemm_bf16_tiled(const void* A, long lda, int a_kmajor, const void* B, long ldb, int b_kmajor, void* C,
+                        long ldc, int M, int N, int K, const void* bias, const void* resid, long ldr, int out_mode,
+                        int act, int splits, void* workspace, float alpha, int geometry, int ring_grid,
+                        void* stream);
 
 /* Fused SwiGLU MLP GEMMs (src/models/jit/denoiser.py:480-506 SwiGLU, :535-543 FinalLayer):
  * forward: x12 [M][2F] = x.W12^T + b12 (W12 = w_1 | w_2 rows, [2F][K]) and h [M][F] =
@@ -85,16 +83,6 @@ int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr, const void* k, 
                  long l_sh, const float* kbias, long kb_sb, void* dq, long dq_sb, long dq_sh, long dq_sr,
                  void* dk, long dk_sb, long dk_sh, long dk_sr, void* dv, long dv_sb, long dv_sh, long dv_sr,
                  int B, int H, int n, int nk, int n_dense, float scale, void* stream);
-/* Forward lazy-rescale threshold in log2 units (default 8; 0 = rescale whenever the row max grows).
- * Test hook for the online-softmax rescale branch; process-wide. */
-int vpt_attn_set_rescale_threshold(float tau);
-/* Benchmark hook: kernel variant (0 = production, 4-wave blocks; 1 / 2 = timing-only backward
- * ablations with wrong results: no in-loop tile staging / row reads in place of transposed reads;
- * 3 = 8-wave blocks, correct; 4-7 = dK/dV-kernel timing ablations, wrong results: no exp2 / 4 of 16
- * dV,dK MFMAs / no transposed LDS reads / no S,dP LDS reads; 8 = previous compiler-scheduled dK/dV
- * body, correct). Process-wide. */
-int vpt_attn_set_variant(int v);
-
 /* ---- RMSNorm over the hidden dim -----------------------------------------------------------
  * Replaces FP32RMSNorm.forward src/modules/norm.py:20-27 (norm1/norm2/norm_final,
  * src/models/jit/denoiser.py:521,600,625) and its backward (dx = dres + RMSNorm'(dy);
@@ -176,13 +164,14 @@ int vpt_bias_grad(const void* in, long ld, long M, int N, float* part, float* ou
 int vpt_cast_f32_bf16(const float* in, long n, void* out, void* stream);
 
 /* ---- optimizer -------------------------------------------------------------------------------
- * RAdamScheduleFree step over flat buffers (bf16 y, f32 grad / z / v); sf_lerp implements the
+ * RAdamScheduleFree step over flat buffers (bf16 y, f32 z / v; grad f32, or bf16 when grad_bf16 = 1:
+ * the all-reduced bf16 wire buffer of the data-parallel path); sf_lerp implements the
  * train()/eval() y<->x swap; sf_init lazily creates z = y, v = 0. Replaces schedulefree 1.4.1
  * RAdamScheduleFree (configs/jit/x-loss/config.yml:74-78, src/optimizer/util.py:5-31,
  * src/trainer/common.py:276-285,382-388). */
-int vpt_radam_sf_step(void* y, const float* grad, float* z, float* v, long n, float beta2, float bias_correction2,
-                      float eps, float ckp1, float adaptive_y_lr, float lr, float decay, float grad_scale, int adam,
-                      void* stream);
+int vpt_radam_sf_step(void* y, const void* grad, int grad_bf16, float* z, float* v, long n, float beta2,
+                      float bias_correction2, float eps, float ckp1, float adaptive_y_lr, float lr, float decay,
+                      float grad_scale, int adam, void* stream);
 int vpt_sf_lerp(void* y, const float* z, long n, float w, void* stream);
 int vpt_sf_init(const void* y, float* z, float* v, long n, void* stream);
 

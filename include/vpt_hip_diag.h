@@ -1,0 +1,38 @@
+/*
+ * vpt_hip_diag.h — diagnostic-only entry points of libvpt_hip_diag.so.
+ *
+ * The diagnostic library is built from the same sources with -DVPT_DIAG (vpt/_build.py
+ * build(diag=True)); it is used by tools/ for A/B timing, ablations and cycle stamps and is never
+ * loaded by the product path (vpt/_lib.py loads it only when VPT_DIAG=1). These switches are
+ * PROCESS-WIDE and some of them make results WRONG (timing-only ablations), which is why the
+ * production library libvpt_hip.so does not export them (it is stateless and reentrant).
+ * It exports everything vpt_hip.h declares, plus the functions below.
+ */
+#ifndef VPT_HIP_DIAG_H
+#define VPT_HIP_DIAG_H
+#include "vpt_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* GEMM tile geometry override: 0 = automatic; 128, 256; 2561 = ring unstaggered, 2562 = 256x256
+ * 2-stage (A/B); 2563/2564 = timing-only ablations of the ring (WRONG results); 2565 = DMA in the
+ * MFMA phase; 2566 / 2567 = stamped / timeline ring builds (need vpt_gemm_set_debug). */
+int vpt_gemm_set_geometry(int geo);
+/* u64 buffer receiving per-wave K-step segment cycle sums (2566: [256][8][8]) or realtime stamps
+ * (2567: [grid][4][4]); nullptr disables. */
+int vpt_gemm_set_debug(unsigned long long* buf);
+/* Persistent ring grid override (0 = per-call / default). */
+int vpt_gemm_set_ring_grid(int blocks);
+/* Forward lazy-rescale threshold in log2 units (default 8; 0 = rescale whenever the row max grows). */
+int vpt_attn_set_rescale_threshold(float tau);
+/* Attention kernel variant: 0 = production; 1 / 2 = timing-only backward ablations (WRONG results);
+ * 3 = 8-wave blocks (correct); 4-7 = dK/dV timing ablations (WRONG results); 8 = the previous
+ * compiler-scheduled dK/dV body (correct). */
+int vpt_attn_set_variant(int v);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -86,3 +86,41 @@ def test_oracle_transform_chain_shapes():
     assert (sh, sw) == (399, 512)
     assert out.shape == (3, 384, 512) and out.dtype == torch.float16
     assert out.abs().max() <= 1.3  # bicubic ringing overshoots [-1, 1] on noise
+
+
+def test_bucket_loader_drops_buckets_beyond_rope_range():
+    """SURVEY gotcha #8: generate_buckets() yields sides up to 16384 px; JiT's RoPE covers 2048 px
+    per side (rope_axes_lens 128 x patch 16), so the loader keeps only buckets within it."""
+    full = D.generate_buckets()
+    assert full.max() > 2048
+    ld = D.BucketLoader([], [], None, batch_size=1, device="cpu")
+    assert ld.buckets.max() <= 2048 and len(ld.buckets) == int((full <= 2048).all(1).sum())
+    # an extreme panorama lands in the widest bucket the model can embed
+    sizes = [(9000, 600)]
+    ld = D.BucketLoader([None], sizes, None, batch_size=1, device="cpu")
+    b, _ = ld.batches[0]
+    assert ld.buckets[b][0] <= 2048
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_bucket_loader_rank_sharding(world):
+    """accelerate prepare_data_loader semantics (src/trainer/common.py:130): one shared shuffled order,
+    padded by cycling to a multiple of world_size, rank r takes r::world; every batch is seen, ranks
+    are disjoint up to the padding, lengths are equal."""
+    rng = random.Random(7)
+    sizes = [(rng.randint(1100, 2500), rng.randint(1100, 2500)) for _ in range(61)]
+    n = len(D.BucketLoader([None] * 61, sizes, None, batch_size=4, device="cpu", seed=3).batches)
+    ref = torch.randperm(n, generator=torch.Generator().manual_seed(3)).tolist()
+    padded = ref + [ref[i % n] for i in range(-n % world)]
+    orders = []
+    for r in range(world):
+        ld = D.BucketLoader([None] * 61, sizes, None, batch_size=4, device="cpu", seed=3, rank=r, world_size=world)
+        o = ld.order()
+        assert len(o) == len(ld) == -(-n // world)
+        assert o == padded[r::world]
+        orders.append(o)
+    allx = [i for o in orders for i in o]
+    assert sorted(set(allx)) == list(range(n))
+    assert len(allx) - n == -n % world  # only the padding repeats
+    with pytest.raises(ValueError):
+        D.BucketLoader([], [], None, batch_size=1, device="cpu", rank=2, world_size=2)

@@ -48,11 +48,11 @@ def test_buckets_tile_flat_buffer():
             assert len(inside) == 1, s.name
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, wire="f32"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(0)
-    from vpt.ddp import GradSync, grad_buckets
+    from vpt.ddp import GradSync, LossLog, grad_buckets
     from vpt.params import ParamLayout
     oc = GC.micro_config()
     cfg = _vcfg(oc)
@@ -71,23 +71,30 @@ def _worker(rank, world, port, q):
         grads[s.offset:s.offset + s.numel] = p.grad.reshape(-1)
     s = lay.by_name["class_encoder.embedding.weight"]
     grads[s.offset:s.offset + s.numel] = emb.grad.reshape(-1)
-    sync = GradSync(grads, grad_buckets(lay, cfg.depth))
+    sync = GradSync(grads, grad_buckets(lay, cfg.depth), wire=wire)
     for name, _, _ in sync.buckets[:-2]:   # launched from the backward hook, in completion order
         sync.launch(name)
     sync.launch_rest()
     applied = []
-    sync.finish(lambda lo, hi, sc: (applied.append((lo, hi)), grads[lo:hi].mul_(sc)))
-    q.put((rank, grads.clone(), applied))
+    out = torch.zeros_like(grads)
+    sync.finish(lambda lo, hi, sc, g: (applied.append((lo, hi)), out[lo:hi].copy_(g.float() * sc)))
+    # per-step loss logging: accelerator.gather(loss).mean() as one 2-float all-reduce, read later
+    log = LossLog("cpu", depth=2)
+    first = log.push(loss.detach())
+    second = log.push(loss.detach() * 3)
+    third = log.pop()
+    q.put((rank, out.clone(), applied, (first, second, third, loss.item())))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_rank_gradient_mean_equals_single_rank_big_batch():
+@pytest.mark.parametrize("wire", ["f32", "bf16"])
+def test_two_rank_gradient_mean_equals_single_rank_big_batch(wire):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, wire)) for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=300) for _ in range(world)]
@@ -113,6 +120,15 @@ def test_two_rank_gradient_mean_equals_single_rank_big_batch():
         ref[s.offset:s.offset + s.numel] = p.grad.reshape(-1)
     s = lay.by_name["class_encoder.embedding.weight"]
     ref[s.offset:s.offset + s.numel] = emb.grad.reshape(-1)
-    assert ((g0 - ref).norm() / ref.norm()).item() < 1e-5
+    # f32 wire: exact up to summation order; bf16 wire (the reference DDP's bf16 .grad reduction):
+    # two bf16 roundings of each rank's gradient and of the sum
+    assert ((g0 - ref).norm() / ref.norm()).item() < (1e-5 if wire == "f32" else 8e-3)
     applied = out[0][2]
     assert sum(hi - lo for lo, hi in applied) == lay.total
+    # loss log: mean over ranks of each pushed loss, returned one push later (depth 2)
+    l0, l1 = out[0][3][3], out[1][3][3]
+    for r in range(world):
+        first, second, third, _ = out[r][3]
+        assert first is None
+        assert abs(second - (l0 + l1) / 2) < 1e-6 * abs(l0 + l1)
+        assert abs(third - 3 * (l0 + l1) / 2) < 1e-6 * abs(l0 + l1)

@@ -81,40 +81,46 @@ def test_tokenizer_matches_oracle():
     assert torch.equal(ids, rid) and torch.equal(mask, rmask)
 
 
-def _sf_reference_schedule(lr, betas, steps, p=2.0):
-    """Scalar schedule of schedulefree RAdamScheduleFree.step, restated independently."""
-    beta1, beta2 = betas
-    out, lr_max, wsum = [], -1.0, 0.0
-    for k in range(steps):
-        step = k + 1
-        b2t = beta2 ** step
-        rho_inf = 2 / (1 - beta2) - 1
-        rho_t = rho_inf - 2 * step * b2t / (1 - b2t)
-        rect = math.sqrt((rho_t - 4) * (rho_t - 2) * rho_inf / ((rho_inf - 4) * (rho_inf - 2) * rho_t)) if rho_t > 4 else 0.0
-        lr_t = lr * rect
-        lr_max = max(lr_t, lr_max)
-        w = step ** p * lr_max ** p
-        wsum += w
-        ckp1 = w / wsum if wsum else 0.0
-        out.append((lr_t, ckp1, rho_t > 4))
-    return out
-
-
 def test_radam_sf_scalar_schedule():
+    """vpt.optim's host schedule == the published schedulefree step (tests/sf_reference.py), incl.
+    weight = step**r * lr_max**weight_lr_power with r = 0 (1/k-like averaging, not 3/k)."""
     import vpt.optim as vo
-    opt = vo.RAdamScheduleFreeFlat.__new__(vo.RAdamScheduleFreeFlat)
-    opt.param_groups = [dict(lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, r=0.0, k=0, train_mode=True,
-                             weight_sum=0.0, lr_max=-1.0, scheduled_lr=0.0, weight_lr_power=2.0,
-                             silent_sgd_phase=True)]
-    ref = _sf_reference_schedule(1e-4, (0.9, 0.999), 12)
-    for k in range(12):
-        s = opt.scalars()
-        g = opt.param_groups[0]
-        assert math.isclose(s["lr"], ref[k][0], rel_tol=1e-12, abs_tol=1e-20)
-        assert math.isclose(s["ckp1"], ref[k][1], rel_tol=1e-12, abs_tol=1e-20)
-        assert s["adam"] == ref[k][2]
-        g["lr_max"], g["weight_sum"], g["k"] = s["lr_max"], s["weight_sum"], g["k"] + 1
-    assert ref[0][0] == 0.0 and ref[-1][0] > 0  # silent SGD warm-up, then rectified Adam
+    from tests.sf_reference import reference_schedule
+    for r, wlp, silent in ((0.0, 2.0, True), (0.5, 1.0, False)):
+        opt = vo.RAdamScheduleFreeFlat.__new__(vo.RAdamScheduleFreeFlat)
+        opt.param_groups = [dict(lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, r=r, k=0, train_mode=True,
+                                 weight_sum=0.0, lr_max=-1.0, scheduled_lr=0.0, weight_lr_power=wlp,
+                                 silent_sgd_phase=silent)]
+        ref = reference_schedule(1e-4, (0.9, 0.999), 40, r=r, weight_lr_power=wlp, silent_sgd_phase=silent)
+        for k in range(40):
+            s = opt.scalars()
+            g = opt.param_groups[0]
+            assert math.isclose(s["lr"], ref[k][0], rel_tol=1e-12, abs_tol=1e-20)
+            assert math.isclose(s["ckp1"], ref[k][1], rel_tol=1e-12, abs_tol=1e-20)
+            assert s["adam"] == ref[k][2]
+            g["lr_max"], g["weight_sum"], g["k"] = s["lr_max"], s["weight_sum"], g["k"] + 1
+        if silent:
+            assert ref[0][0] == 0.0 and ref[0][1] == 0.0 and ref[-1][0] > 0  # silent SGD warm-up, then RAdam
+        else:
+            assert ref[0][0] == 1e-4  # plain SGD at the full lr during the warm-up
+    # r = 0: averaging weight -> 1/k once the rectified lr has settled (the r1 build's step**p gave ~3/k)
+    sch = reference_schedule(1e-3, (0.9, 0.999), 20000)
+    assert 0.9 < sch[-1][1] * 20000 < 1.2
+
+
+def test_radam_sf_restatement_matches_closed_form():
+    """The CPU restatement used as the GPU kernel's checker reproduces the closed form of one
+    Adam-phase step on a scalar (guards the checker itself)."""
+    from tests.sf_reference import SFRef
+    y = torch.tensor([0.5], dtype=torch.float32)
+    opt = SFRef([y], lr=1e-2, weight_decay=0.1, silent_sgd_phase=False)
+    opt.train()
+    g = torch.tensor([0.2])
+    s = opt.step([g])  # step 1: rho_t <= 4, silent_sgd_phase False -> plain SGD at lr
+    assert s["rho_t"] <= 4 and s["ckp1"] == 1.0
+    gd = 0.2 + 0.1 * 0.5
+    assert math.isclose(opt.z[0].item(), 0.5 - 1e-2 * gd, rel_tol=1e-6)
+    assert math.isclose(y.item(), 0.5 + (1e-2 * (0.9 * 0 - 1)) * gd, rel_tol=1e-6)
 
 
 def test_capi_exports_every_declared_symbol():
@@ -127,6 +133,12 @@ def test_capi_exports_every_declared_symbol():
     missing = [s for s in declared if not hasattr(lib, s)]
     assert not missing, missing
     assert declared == set(_lib.SIGNATURES), (declared ^ set(_lib.SIGNATURES))
+    # the production library is stateless: no process-wide A/B or ablation switch is exported
+    # (those live only in libvpt_hip_diag.so, include/vpt_hip_diag.h)
+    diag = set(re.findall(r"\b(vpt_[a-z0-9_]+)\s*\(", open(os.path.join(ROOT, "include", "vpt_hip_diag.h")).read()))
+    assert diag == set(_lib.DIAG_SIGNATURES)
+    leaked = [s for s in diag if hasattr(ctypes.CDLL(str(_lib.LIB)), s)]
+    assert not leaked, leaked
 
 
 def test_capi_reports_errors_without_gpu_work():

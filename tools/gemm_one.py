@@ -2,6 +2,8 @@
 
   python tools/gemm_one.py M N K GEO [ITERS]
 """
+import os
+os.environ.setdefault("VPT_DIAG", "1")  # A/B switches live in libvpt_hip_diag.so only
 
 import os
 import sys

@@ -4,6 +4,8 @@ Uniform [-1, 1) operands (guide §5.4 rule 25), interleaved rounds in one proces
 
   python tools/gemm_square.py [--rounds 3]
 """
+import os
+os.environ.setdefault("VPT_DIAG", "1")  # A/B switches live in libvpt_hip_diag.so only
 
 import argparse
 import json

@@ -3,6 +3,8 @@ Shares only -- the stamps' lgkmcnt(0) waits forbid overlaps of the real kernel (
 
   python tools/gemm_stamp.py
 """
+import os
+os.environ.setdefault("VPT_DIAG", "1")  # A/B switches live in libvpt_hip_diag.so only
 
 import json
 import os

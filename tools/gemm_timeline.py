@@ -4,6 +4,8 @@ the phases and the dispatch skew, in microseconds, per shape, plus the kernel's 
 
   python tools/gemm_timeline.py
 """
+import os
+os.environ.setdefault("VPT_DIAG", "1")  # A/B switches live in libvpt_hip_diag.so only
 
 import json
 import os

@@ -4,6 +4,8 @@ known-good reference bar. Interleaved rounds in one process (guide §5.4 rule 24
 
   python tools/kernel_bench.py [--rounds 5]
 """
+import os
+os.environ.setdefault("VPT_DIAG", "1")  # A/B switches live in libvpt_hip_diag.so only
 
 import argparse
 import json

@@ -48,8 +48,26 @@ def _counter(dirname, counter):
     return tot, launches
 
 
+def _counters(dirname, names):
+    """{op: {counter: sum over the op's dispatches}}, dispatches per op (counted once per launch kernel)."""
+    path = glob.glob(f"{dirname}/**/*counter_collection.csv", recursive=True)[0]
+    tot = collections.defaultdict(lambda: collections.defaultdict(float))
+    seen = collections.defaultdict(set)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] not in names:
+            continue
+        op = _op_of(r["Kernel_Name"])
+        if op is None:
+            continue
+        tot[op][r["Counter_Name"]] += float(r["Counter_Value"])
+        if any(m in r["Kernel_Name"] for m in OPS[op][1]):
+            seen[op].add(r.get("Dispatch_Id", r.get("Correlation_Id", len(seen[op]))))
+    return tot, {op: len(v) for op, v in seen.items()}
+
+
 def main():
     fdir, wdir, kdir, out = sys.argv[1:5]
+    mdir = sys.argv[5] if len(sys.argv) > 5 else None
     fetch, nf = _counter(fdir, "FETCH_SIZE")
     write, nw = _counter(wdir, "WRITE_SIZE")
     stats = glob.glob(f"{kdir}/**/*kernel_stats.csv", recursive=True)[0]
@@ -79,6 +97,25 @@ def main():
     res["_method"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of the same "
                       "command; read bytes = 2 x FETCH_SIZE x 1024 (gfx950 half-count of 16-B/lane reads), "
                       "write bytes = WRITE_SIZE x 1024; per launch of the op")
+    if mdir:
+        # MFMA pipe utilisation: SQ_VALU_MFMA_BUSY_CYCLES counts MFMA-busy cycles summed over SIMDs
+        # (MI355X_MICROARCH.md: 32 x N for 32x32x16 bf16); GRBM_GUI_ACTIVE is summed over the 8 XCDs, so
+        # the kernel's cycles = GUI_ACTIVE / 8 and the chip's SIMD-cycles = that x 1024 SIMDs.
+        names = ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE")
+        tot, n = _counters(mdir, names)
+        for op, c in tot.items():
+            if op not in res or not n.get(op):
+                continue
+            gui = c.get("GRBM_GUI_ACTIVE", 0.0)
+            busy = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+            d = res[op]
+            d["mfma_busy_cycles_per_launch"] = round(busy / n[op])
+            d["gui_active_per_launch"] = round(gui / n[op])
+            d["sq_busy_cycles_per_launch"] = round(c.get("SQ_BUSY_CYCLES", 0.0) / n[op])
+            if gui:
+                d["mfma_util"] = round(busy * 8 / (gui * 1024), 4)
+        res["_mfma_method"] = ("rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE (one pass); "
+                               "mfma_util = MFMA_BUSY x 8 / (GRBM_GUI_ACTIVE x 1024 SIMDs)")
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 

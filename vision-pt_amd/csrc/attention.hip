@@ -44,9 +44,16 @@ struct AttnArgs {
 };
 
 constexpr float kNegInf = -__builtin_huge_valf();
+constexpr float kTau = 8.f;  // forward lazy-rescale threshold, log2 units
+#ifdef VPT_DIAG
+// diagnostic build only (libvpt_hip_diag.so): process-wide A/B switches
 int g_variant = 0;  // backward kernel variant (vpt_attn_set_variant; 1, 2 = timing-only ablations)
 int g_waves = 4;    // waves per block (vpt_attn_set_variant 3 -> 8-wave blocks, A/B only)
-float g_tau = 8.f;  // forward lazy-rescale threshold, log2 units (vpt_attn_set_rescale_threshold)
+float g_tau = kTau; // forward lazy-rescale threshold (vpt_attn_set_rescale_threshold)
+#else
+constexpr int g_variant = 0, g_waves = 4;
+constexpr float g_tau = kTau;
+#endif
 
 // Reductions over the lane pair (l, l^32) with v_permlane32_swap (VALU, no LDS round trip): the two
 // results together hold both halves' values in every lane, whichever half the swap moves.
@@ -622,7 +629,7 @@ extern "C" int vpt_attn_fwd(const void* q, long q_sb, long q_sh, long q_sr,
   g.scale = scale; g.scale_log2 = scale * 1.4426950408889634f;
   g.tau = g_tau;
   g.kb0 = g.n_dense / 64 * 64;
-  if (g_waves == 4)
+  if (g_waves != 8)
     hipLaunchKernelGGL(attn_fwd_kernel<4>, dim3((n + 127) / 128, H, B), dim3(256), key_bias_lds_bytes(g),
                        (hipStream_t)stream, g);
   else
@@ -667,6 +674,7 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
   const size_t kbl = key_bias_lds_bytes(g);
   const dim3 g4((n + 127) / 128, H, B), g8((n + 255) / 256, H, B);  // dQ: over queries
   const dim3 k4((nk + 127) / 128, H, B), k8((nk + 255) / 256, H, B);  // dK/dV: over keys
+#ifdef VPT_DIAG
   if (g_variant == 1) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 4>), k4, dim3(256), 0, s, g);
     hipLaunchKernelGGL((attn_bwd_dq_kernel<1, 4>), g4, dim3(256), kbl, s, g);
@@ -682,19 +690,23 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
     if (g_variant == 5) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<5, 4>), k4, dim3(256), 0, s, g);
     if (g_variant == 6) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<6, 4>), k4, dim3(256), 0, s, g);
     hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 4>), g4, dim3(256), kbl, s, g);
-  } else if (g_waves == 4) {  // production: the explicitly ordered dK/dV body (ABL 8; +2 % measured)
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<8, 4>), k4, dim3(256), 0, s, g);
-    VPT_LAUNCH_CHECK();
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 4>), g4, dim3(256), kbl, s, g);
-  } else {
+  } else if (g_waves == 8) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 8>), k8, dim3(512), 0, s, g);
     VPT_LAUNCH_CHECK();
     hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 8>), g8, dim3(512), kbl, s, g);
+  } else
+#endif
+  {  // production: the explicitly ordered dK/dV body (ABL 8; +2 % measured)
+    (void)g8; (void)k8;
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<8, 4>), k4, dim3(256), 0, s, g);
+    VPT_LAUNCH_CHECK();
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 4>), g4, dim3(256), kbl, s, g);
   }
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
 
+#ifdef VPT_DIAG
 // Test hook: the forward lazy-rescale threshold (log2 units; 0 = rescale whenever the max grows).
 extern "C" int vpt_attn_set_rescale_threshold(float tau) {
   VPT_CHECK_ARG(tau >= 0.f && tau <= 64.f, "vpt_attn_set_rescale_threshold: tau in [0, 64]");
@@ -713,3 +725,4 @@ extern "C" int vpt_attn_set_variant(int v) {
   g_waves = v == 3 ? 8 : 4;
   return VPT_OK;
 }
+#endif  // VPT_DIAG

@@ -43,7 +43,8 @@ struct GemmArgs {
   int out_mode, act;
   int splits;               // split-K slices (ring kernel work items = tiles * splits)
   float alpha;              // output scale applied to the accumulator before bias (LoRA alpha / rank)
-  unsigned long long* dbg;  // stamp-diagnostic output (geometry 2566 only)
+  int ring_grid;            // persistent ring grid (0 = one block per CU)
+  unsigned long long* dbg;  // stamp-diagnostic output (diagnostic build only)
   // fused SwiGLU (ring kernel only): sw = 1 forward (C = x12 [M][2F], C2 = h [M][F]; N = 2F, B = W1|W2),
   // sw = 2 backward of the W3 dgrad (C = dx12 [M][2F], aux = x12; N = F)
   int sw;
@@ -333,7 +334,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_bf16_kernel(GemmArgs g
 // (finite, in-bounds) addresses and its k >= K lanes of the A fragments are zeroed in registers.
 constexpr int RBK = 32;
 constexpr int RSTAGES = 4;
-int g_ring_grid = 256;  // persistent ring grid: one block per CU (vpt_gemm_set_ring_grid)
+constexpr int kRingGrid = 256;  // persistent ring grid: one block per CU (GemmArgs::ring_grid overrides)
 
 __device__ __forceinline__ int kmaj32_off(int row, int chunk) {  // [R][32] bf16, 64-B rows
   return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4);
@@ -848,7 +849,8 @@ template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false, bool STAMP
 int launch_ring(const GemmArgs& g, int splits, hipStream_t s) {
   constexpr int LDS = RSTAGES * 2 * 256 * RBK * 2;  // the epilogue stages through ring stage 3
   const int items = ((g.M + 255) / 256) * ((g.N + 255) / 256) * splits;
-  const int grid = items < g_ring_grid ? items : g_ring_grid;
+  const int rg = g.ring_grid > 0 ? g.ring_grid : kRingGrid;
+  const int grid = items < rg ? items : rg;
   hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, SW>), dim3(grid), dim3(512), LDS, s, g);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
@@ -858,13 +860,17 @@ template <bool AK, bool BK_>
 int launch_geo(const GemmArgs& g, int splits, int geo, hipStream_t s) {
   if (geo != 128 && geo != 2562 && g.N % 8 != 0) geo = 128;  // ring epilogue stores 8-column chunks
   if (geo == 256) return launch_ring<AK, BK_, true>(g, splits, s);
+#ifdef VPT_DIAG
+  // diagnostic build only (libvpt_hip_diag.so): A/B geometries, timing ablations with WRONG results
+  // (2563, 2564), stamped / timeline builds
   if (geo == 2561) return launch_ring<AK, BK_, false>(g, splits, s);  // ring without the stagger (A/B only)
   if (AK && BK_ && geo == 2563) return launch_ring<AK, BK_, true, 1>(g, splits, s);  // ablation, wrong results
   if (AK && BK_ && geo == 2564) return launch_ring<AK, BK_, true, 2>(g, splits, s);  // ablation, wrong results
   if (geo == 2565) return launch_ring<AK, BK_, true, 0, true>(g, splits, s);  // DMA in the MFMA phase
   if (AK && BK_ && geo == 2566 && g.dbg) return launch_ring<AK, BK_, true, 0, false, true>(g, splits, s);  // stamps
-  if (AK && BK_ && geo == 2567 && g.dbg) return launch_ring<AK, BK_, true, 0, false, false, true>(g, splits, s);  // timeline
+  if (AK && BK_ && geo == 2567 && g.dbg) return launch_ring<AK, BK_, true, 0, false, false, true>(g, splits, s);
   if (geo == 2562) return launch<AK, BK_, 256, 256, 2, 4>(g, splits, s);  // 2-stage BK=64 T256 (A/B only)
+#endif
   return launch<AK, BK_, 128, 128, 2, 2>(g, splits, s);
 }
 
@@ -887,14 +893,24 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ part, long n, int
 }
 
 // Geometry choice: the 256x256 ring when its grid (x split-K slices) fills most of the 256 CUs,
-// otherwise 128x128 (2 blocks/CU, 4x the tiles).
+// otherwise 128x128 (2 blocks/CU, 4x the tiles). `req` (128 / 256) forces one (vpt_gemm_bf16_tiled).
+#ifdef VPT_DIAG
 unsigned long long* g_dbg = nullptr;  // vpt_gemm_set_debug
-int g_geo_override = 0;  // 0 = heuristic; 128 / 256 / 2561 / 2562 force a geometry (benchmarking)
-int pick_geo(int M, int N, int splits) {
+int g_geo_override = 0;               // vpt_gemm_set_geometry
+int g_ring_grid_override = 0;         // vpt_gemm_set_ring_grid
+#endif
+int pick_geo(int M, int N, int splits, int req) {
+#ifdef VPT_DIAG
   if (g_geo_override) return g_geo_override;
+#endif
+  if (req) return req;
   const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256) * splits;
   return t256 >= 160 ? 256 : 128;
 }
+
+int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, int b_kmajor, void* C, long ldc, int M,
+              int N, int K, const void* bias, const void* resid, long ldr, int out_mode, int act, int splits,
+              void* workspace, float alpha, int geo_req, int ring_grid, void* stream);
 
 }  // namespace
 
@@ -902,6 +918,24 @@ extern "C" int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* 
                              int b_kmajor, void* C, long ldc, int M, int N, int K,
                              const void* bias, const void* resid, long ldr, int out_mode, int act,
                              int splits, void* workspace, float alpha, void* stream) {
+  return gemm_impl(A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, M, N, K, bias, resid, ldr, out_mode, act, splits,
+                   workspace, alpha, 0, 0, stream);
+}
+
+extern "C" int vpt_gemm_bf16_tiled(const void* A, long lda, int a_kmajor, const void* B, long ldb, int b_kmajor,
+                                   void* C, long ldc, int M, int N, int K, const void* bias, const void* resid,
+                                   long ldr, int out_mode, int act, int splits, void* workspace, float alpha,
+                                   int geometry, int ring_grid, void* stream) {
+  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256, "vpt_gemm_bf16_tiled: geometry 0, 128 or 256");
+  VPT_CHECK_ARG(ring_grid >= 0 && ring_grid <= 65536, "vpt_gemm_bf16_tiled: ring_grid 0..65536");
+  return gemm_impl(A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, M, N, K, bias, resid, ldr, out_mode, act, splits,
+                   workspace, alpha, geometry, ring_grid, stream);
+}
+
+namespace {
+int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, int b_kmajor, void* C, long ldc, int M,
+              int N, int K, const void* bias, const void* resid, long ldr, int out_mode, int act, int splits,
+              void* workspace, float alpha, int geo_req, int ring_grid, void* stream) {
   VPT_CHECK_ARG(A && B && C, "vpt_gemm_bf16: null operand");
   VPT_CHECK_ARG(M > 0 && N > 0 && K > 0, "vpt_gemm_bf16: empty shape");
   VPT_CHECK_ARG(N % 4 == 0, "vpt_gemm_bf16: N%4 required");
@@ -920,7 +954,11 @@ extern "C" int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* 
   g.M = M; g.N = N; g.K = K;
   g.act = act;
   g.alpha = alpha;
+  g.ring_grid = ring_grid;
+#ifdef VPT_DIAG
   g.dbg = g_dbg;
+  if (g_ring_grid_override) g.ring_grid = g_ring_grid_override;
+#endif
   hipStream_t s = (hipStream_t)stream;
   int final_mode = out_mode;
   if (splits > 1) {
@@ -942,7 +980,7 @@ extern "C" int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* 
     g.split_stride = 0;
     g.out_mode = out_mode;
   }
-  const int geo = pick_geo(M, N, splits);
+  const int geo = pick_geo(M, N, splits, geo_req);
   int rc;
   if (a_kmajor && b_kmajor) rc = launch_geo<true, true>(g, splits, geo, s);
   else if (a_kmajor && !b_kmajor) rc = launch_geo<true, false>(g, splits, geo, s);
@@ -957,7 +995,10 @@ extern "C" int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* 
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
+}  // namespace
 
+#ifdef VPT_DIAG
+// ---- diagnostic build only (libvpt_hip_diag.so, include/vpt_hip_diag.h): process-wide switches ----
 extern "C" int vpt_gemm_set_geometry(int geo) {
   VPT_CHECK_ARG(geo == 0 || geo == 128 || geo == 256 || (geo >= 2561 && geo <= 2567),
                 "vpt_gemm_set_geometry: 0, 128, 256 or 2561-2567");
@@ -965,23 +1006,24 @@ extern "C" int vpt_gemm_set_geometry(int geo) {
   return VPT_OK;
 }
 
+// Persistent ring grid size (blocks); 0 restores one block per CU (256).
+extern "C" int vpt_gemm_set_ring_grid(int blocks) {
+  VPT_CHECK_ARG(blocks >= 0 && blocks <= 65536, "vpt_gemm_set_ring_grid: 0..65536");
+  g_ring_grid_override = blocks;
+  return VPT_OK;
+}
+
+// Output buffer for the stamped ring build (geometry 2566), [256 blocks][8 waves][8] u64.
+extern "C" int vpt_gemm_set_debug(unsigned long long* buf) {
+  g_dbg = buf;
+  return VPT_OK;
+}
+#endif  // VPT_DIAG
+
 extern "C" long vpt_gemm_workspace_bytes(int M, int N, int K, int splits) {
   (void)K;
   if (splits <= 1) return 0;
   return (long)splits * M * N * 4;
-}
-
-// Benchmark hook: persistent ring grid size (blocks); 0 restores one block per CU (256).
-extern "C" int vpt_gemm_set_ring_grid(int blocks) {
-  VPT_CHECK_ARG(blocks >= 0 && blocks <= 65536, "vpt_gemm_set_ring_grid: 0..65536");
-  g_ring_grid = blocks ? blocks : 256;
-  return VPT_OK;
-}
-
-// Diagnostic hook: output buffer for the stamped ring build (geometry 2566), [256 blocks][8 waves][8] u64.
-extern "C" int vpt_gemm_set_debug(unsigned long long* buf) {
-  g_dbg = buf;
-  return VPT_OK;
 }
 
 // ---- fused SwiGLU GEMMs (the JiT MLP, denoiser.py:480-506; FinalLayer 535-543) ---------------------
@@ -989,8 +1031,11 @@ extern "C" int vpt_swiglu_fwd(const void* x12, long M, int F, void* h, void* str
 extern "C" int vpt_swiglu_bwd(const void* dh, const void* x12, long M, int F, void* dx12, void* stream);
 
 static bool swiglu_ring_ok(int M, int N) {
+#ifdef VPT_DIAG
   if (g_geo_override && g_geo_override != 256) return false;
-  return N % 256 == 0 && ((long)((M + 255) / 256) * (N / 256) >= 160 || g_geo_override == 256);
+  if (g_geo_override == 256) return N % 256 == 0;
+#endif
+  return N % 256 == 0 && (long)((M + 255) / 256) * (N / 256) >= 160;
 }
 
 // x12 [M][2F] = x . W12^T + b12 (W12 = W1 | W2 [2F][K]) and h [M][F] = bf16(silu(x1)) * x2, from one ring

@@ -438,18 +438,21 @@ struct SfScalars {
   float beta2, bias_correction2, eps, ckp1, adaptive_y_lr, lr, decay, grad_scale;
   int adam;
 };
-__global__ void radam_sf_step_kernel(bf16_t* __restrict__ y, const float* __restrict__ grad, float* __restrict__ z,
+// GB: the gradient arrives as bf16 (the all-reduced bf16 wire buffer, vpt.ddp.GradSync wire="bf16").
+template <bool GB>
+__global__ void radam_sf_step_kernel(bf16_t* __restrict__ y, const void* __restrict__ grad, float* __restrict__ z,
                                      float* __restrict__ v, long n, SfScalars s) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  float g = grad[i] * s.grad_scale;
+  float g = (GB ? bf2f(reinterpret_cast<const bf16_t*>(grad)[i]) : reinterpret_cast<const float*>(grad)[i]) *
+            s.grad_scale;
   float vv = v[i] * s.beta2 + (1.f - s.beta2) * g * g;
   v[i] = vv;
   if (s.adam) g = g / (sqrtf(vv / s.bias_correction2) + s.eps);
   float yy = bf2f(y[i]);
   if (s.decay != 0.f) g += s.decay * yy;
   float zz = z[i];
-  yy = yy + s.ckp1 * (zz - yy);
+  yy = bf2f(f2bf(yy + s.ckp1 * (zz - yy)));  // y.lerp_(z, ckp1) on the bf16 parameter
   yy = yy + s.adaptive_y_lr * g;
   z[i] = zz - s.lr * g;
   y[i] = f2bf(yy);
@@ -693,13 +696,18 @@ extern "C" int vpt_cast_f32_bf16(const float* in, long n, void* out, void* strea
   return VPT_OK;
 }
 
-extern "C" int vpt_radam_sf_step(void* y, const float* grad, float* z, float* v, long n, float beta2,
+extern "C" int vpt_radam_sf_step(void* y, const void* grad, int grad_bf16, float* z, float* v, long n, float beta2,
                                  float bias_correction2, float eps, float ckp1, float adaptive_y_lr, float lr,
                                  float decay, float grad_scale, int adam, void* stream) {
   VPT_CHECK_ARG(y && grad && z && v && n >= 0, "vpt_radam_sf_step: bad args");
   if (n == 0) return VPT_OK;
   SfScalars s{beta2, bias_correction2, eps, ckp1, adaptive_y_lr, lr, decay, grad_scale, adam};
-  hipLaunchKernelGGL(radam_sf_step_kernel, grid1(n), dim3(256), 0, (hipStream_t)stream, (bf16_t*)y, grad, z, v, n, s);
+  if (grad_bf16)
+    hipLaunchKernelGGL(radam_sf_step_kernel<true>, grid1(n), dim3(256), 0, (hipStream_t)stream, (bf16_t*)y, grad, z, v,
+                       n, s);
+  else
+    hipLaunchKernelGGL(radam_sf_step_kernel<false>, grid1(n), dim3(256), 0, (hipStream_t)stream, (bf16_t*)y, grad, z,
+                       v, n, s);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

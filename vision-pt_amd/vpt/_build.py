@@ -15,6 +15,9 @@ PKG_ROOT = Path(__file__).resolve().parent.parent  # vision-pt_amd/
 CSRC = PKG_ROOT / "csrc"
 BUILD = PKG_ROOT / "build"
 LIB = PKG_ROOT / "lib" / "libvpt_hip.so"
+# diagnostic twin (-DVPT_DIAG): process-wide A/B switches and timing ablations for tools/ only
+BUILD_DIAG = PKG_ROOT / "build_diag"
+LIB_DIAG = PKG_ROOT / "lib" / "libvpt_hip_diag.so"
 ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
@@ -27,33 +30,36 @@ def _needs(obj: Path, deps: list[Path]) -> bool:
     return any(d.stat().st_mtime > t for d in deps)
 
 
-def _compile(src: Path) -> Path:
-    obj = BUILD / (src.stem + ".o")
+def _compile(src: Path, diag: bool = False) -> Path:
+    obj = (BUILD_DIAG if diag else BUILD) / (src.stem + ".o")
     deps = [src] + sorted(CSRC.glob("*.h"))
     if _needs(obj, deps):
-        cmd = [HIPCC, *CFLAGS, "-c", str(src), "-o", str(obj)]
+        cmd = [HIPCC, *CFLAGS, *(["-DVPT_DIAG"] if diag else []), "-c", str(src), "-o", str(obj)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr[-4000:]}")
     return obj
 
 
-def build(verbose: bool = False) -> Path:
-    BUILD.mkdir(exist_ok=True)
-    LIB.parent.mkdir(exist_ok=True)
+def build(verbose: bool = False, diag: bool = False) -> Path:
+    """Production library (default) or its diagnostic twin (diag=True, -DVPT_DIAG)."""
+    bdir, lib = (BUILD_DIAG, LIB_DIAG) if diag else (BUILD, LIB)
+    bdir.mkdir(exist_ok=True)
+    lib.parent.mkdir(exist_ok=True)
     srcs = sorted(CSRC.glob("*.hip"))
     workers = min(len(srcs), max(1, min(8, os.cpu_count() or 1)))
     with cf.ThreadPoolExecutor(workers) as ex:
-        objs = list(ex.map(_compile, srcs))
-    if _needs(LIB, objs):
-        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(LIB)]
+        objs = list(ex.map(lambda s: _compile(s, diag), srcs))
+    if _needs(lib, objs):
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(lib)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
     if verbose:
-        print(f"built {LIB}")
-    return LIB
+        print(f"built {lib}")
+    return lib
 
 
 if __name__ == "__main__":
-    build(verbose=True)
+    import sys
+    build(verbose=True, diag="--diag" in sys.argv)

@@ -8,9 +8,10 @@ this module raises. Every entry point returns an int status; nonzero raises Runt
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
-from ._build import LIB
+from ._build import LIB, LIB_DIAG
 
 P = C.c_void_p
 L = C.c_long
@@ -23,17 +24,13 @@ LL = C.c_longlong
 SIGNATURES: dict[str, list] = {
     "vpt_gemm_bf16": [P, L, I, P, L, I, P, L, I, I, I, P, P, L, I, I, I, P, F, P],
     "vpt_gemm_workspace_bytes": [I, I, I, I],
-    "vpt_gemm_set_geometry": [I],
-    "vpt_gemm_set_debug": [P],
-    "vpt_gemm_set_ring_grid": [I],
+    "vpt_gemm_bf16_tiled": [P, L, I, P, L, I, P, L, I, I, I, P, P, L, I, I, I, P, F, I, I, P],
     "vpt_gemm_swiglu_fwd": [P, L, P, L, P, P, L, P, L, I, I, I, P],
     "vpt_gemm_swiglu_bwd_workspace": [I, I, I],
     "vpt_gemm_swiglu_bwd": [P, L, P, L, P, L, P, L, I, I, I, P, P],
     "vpt_attn_fwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, P, L, I, I, I, I, I, F, P],
     "vpt_attn_bwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, P, L, L, P, L,
                      P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, I, F, P],
-    "vpt_attn_set_rescale_threshold": [F],
-    "vpt_attn_set_variant": [I],
     "vpt_attn_q_scale": [F],
     "vpt_rmsnorm_fwd": [P, L, P, P, L, P, I, I, F, P],
     "vpt_rmsnorm_bwd_blocks": [I],
@@ -58,7 +55,7 @@ SIGNATURES: dict[str, list] = {
     "vpt_embed_gather": [P, P, L, I, P, P],
     "vpt_embed_scatter_add": [P, P, L, I, LL, P, P],
     "vpt_cast_f32_bf16": [P, L, P, P],
-    "vpt_radam_sf_step": [P, P, P, P, L, F, F, F, F, F, F, F, F, I, P],
+    "vpt_radam_sf_step": [P, P, I, P, P, L, F, F, F, F, F, F, F, F, I, P],
     "vpt_sf_lerp": [P, P, L, F, P],
     "vpt_sf_init": [P, P, P, L, P],
     "vpt_copy_rows": [P, L, I, I, I, P, L, I, I, I, P],
@@ -78,6 +75,15 @@ SIGNATURES: dict[str, list] = {
     "vpt_abi_version": [],
     "vpt_build_info": [],
 }
+# Diagnostic-only entry points (include/vpt_hip_diag.h): exported by libvpt_hip_diag.so, loaded only
+# when VPT_DIAG=1 (tools/), never by the product path.
+DIAG_SIGNATURES: dict[str, list] = {
+    "vpt_gemm_set_geometry": [I],
+    "vpt_gemm_set_debug": [P],
+    "vpt_gemm_set_ring_grid": [I],
+    "vpt_attn_set_rescale_threshold": [F],
+    "vpt_attn_set_variant": [I],
+}
 _RESTYPES = {
     "vpt_gemm_workspace_bytes": C.c_long,
     "vpt_cover_resize_crop_workspace": C.c_long,
@@ -91,20 +97,22 @@ _VALUE_FNS = {"vpt_gemm_workspace_bytes", "vpt_cover_resize_crop_workspace", "vp
               "vpt_colsum_blocks", "vpt_attn_q_scale", "vpt_last_error_string", "vpt_abi_version", "vpt_build_info"}
 
 
-def _load(path: Path) -> C.CDLL:
+def _load(path: Path, diag: bool = False) -> C.CDLL:
     if not path.exists():
         raise ImportError(
             f"{path} not found: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()')")
     lib = C.CDLL(str(path))
-    for name, args in SIGNATURES.items():
+    sigs = {**SIGNATURES, **DIAG_SIGNATURES} if diag else SIGNATURES
+    for name, args in sigs.items():
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = _RESTYPES.get(name, C.c_int)
     return lib
 
 
-lib = _load(LIB)
-LIB_PATH = LIB
+DIAG = os.environ.get("VPT_DIAG", "0") == "1"
+LIB_PATH = LIB_DIAG if DIAG else LIB
+lib = _load(LIB_PATH, DIAG)
 
 
 def call(name: str, *args):

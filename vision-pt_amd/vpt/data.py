@@ -159,14 +159,32 @@ class BucketLoader:
     int64 [B,2] (device; (h, w) of the resized image, of the crop, and (top, left)), and caption list.
 
     `images[i]` is anything `decode(images[i])` turns into a uint8 [H,W,3] array (default: a PIL path /
-    array passthrough); `sizes[i]` = (width, height) as the reference's imagesize scan records."""
+    array passthrough); `sizes[i]` = (width, height) as the reference's imagesize scan records.
+
+    Buckets with a side longer than `max_side` px are dropped before images are assigned (SURVEY gotcha
+    #8: JiT's RoPE covers rope_axes_lens[1..2] * patch_size = 128 * 16 = 2048 px per side, while
+    generate_buckets() also yields e.g. 64 x 16384; the reference would fail in its RoPE gather).
+
+    Data-parallel sharding (`rank`, `world_size`) follows accelerate's prepare_data_loader over the
+    reference's DataLoader(batch_size=1, shuffle=True) (src/trainer/common.py:130, src/dataloader.py:68-87):
+    every rank draws the SAME shuffled order of bucket batches (same seed), pads it by cycling from its
+    start to a multiple of world_size (even_batches), and rank r takes entries r, r + W, r + 2W, ..."""
 
     def __init__(self, images: Sequence, sizes: Sequence[tuple[int, int]], captions: Sequence[str] | None,
                  batch_size: int, buckets: np.ndarray | None = None, num_repeats: int = 1, shuffle: bool = True,
-                 seed: int = 0, device="cuda", decode: Callable | None = None, do_upscale: bool = False):
+                 seed: int = 0, device="cuda", decode: Callable | None = None, do_upscale: bool = False,
+                 rank: int = 0, world_size: int = 1, max_side: int | None = 2048):
+        if not 0 <= rank < world_size:
+            raise ValueError(f"rank {rank} outside world_size {world_size}")
         self.images, self.sizes = images, list(sizes)
         self.captions = list(captions) if captions is not None else None
-        self.buckets = buckets if buckets is not None else generate_buckets()
+        buckets = buckets if buckets is not None else generate_buckets()
+        if max_side is not None:
+            buckets = buckets[(buckets <= max_side).all(axis=1)]
+        if len(buckets) == 0:
+            raise ValueError(f"no bucket with both sides <= {max_side}")
+        self.buckets = buckets
+        self.rank, self.world_size = rank, world_size
         self.batches = BucketBatches(assign_buckets(self.sizes, self.buckets), batch_size, num_repeats)
         self.batch_size, self.shuffle, self.device = batch_size, shuffle, torch.device(device)
         self.gen = torch.Generator().manual_seed(seed)
@@ -175,12 +193,20 @@ class BucketLoader:
         self._ws = None
 
     def __len__(self) -> int:
-        return len(self.batches)
+        return -(-len(self.batches) // self.world_size)
+
+    def order(self) -> list[int]:
+        """This rank's bucket-batch indices for one epoch (advances the shared shuffle generator)."""
+        n = len(self.batches)
+        order = torch.randperm(n, generator=self.gen).tolist() if self.shuffle else list(range(n))
+        if self.world_size > 1:
+            pad = -n % self.world_size
+            order = order + [order[i % n] for i in range(pad)]
+            order = order[self.rank::self.world_size]
+        return order
 
     def __iter__(self):
-        order = torch.randperm(len(self.batches), generator=self.gen).tolist() if self.shuffle else \
-            range(len(self.batches))
-        for idx in order:
+        for idx in self.order():
             yield self.batch(idx)
 
     def batch(self, idx: int) -> dict:

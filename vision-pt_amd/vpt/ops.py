@@ -55,6 +55,15 @@ class KernelProbe:
 PROBES: dict[str, KernelProbe] = {}
 
 
+def _launch(op: str, work: float, run):
+    """Runs `run`; when a probe for `op` is active, brackets it with HIP events and records `work`
+    (algorithmic FLOPs for MFMA ops, algorithmic HBM bytes for the memory-bound ones)."""
+    pr = PROBES.get(op)
+    if pr is None:
+        return run()
+    return pr.record(work, run)
+
+
 def _p(t: torch.Tensor | None):
     return None if t is None else t.data_ptr()
 
@@ -70,8 +79,9 @@ def _chk(t: torch.Tensor, dtype, name: str):
 
 # ----------------------------------------------------------------------------- GEMM
 def gemm(a, a_kmajor: bool, b, b_kmajor: bool, M: int, N: int, K: int, out, *, bias=None, resid=None,
-         out_mode=OUT_BF16, act=ACT_NONE, splits=1, workspace=None, alpha=1.0):
-    """out[M,N] (=|+=) alpha * sum_k A(m,k) B(n,k) (+bias[n]) (+resid[m,n]); see csrc/gemm.hip."""
+         out_mode=OUT_BF16, act=ACT_NONE, splits=1, workspace=None, alpha=1.0, geometry=0, ring_grid=0):
+    """out[M,N] (=|+=) alpha * sum_k A(m,k) B(n,k) (+bias[n]) (+resid[m,n]); see csrc/gemm.hip.
+    geometry / ring_grid (0 = automatic) force a tile geometry per call (vpt_gemm_bf16_tiled)."""
     _chk(a, BF16, "a")
     _chk(b, BF16, "b")
     _chk(out, BF16 if out_mode == OUT_BF16 else F32, "out")
@@ -82,10 +92,15 @@ def gemm(a, a_kmajor: bool, b, b_kmajor: bool, M: int, N: int, K: int, out, *, b
     if splits > 1 and workspace is None:
         workspace = torch.empty(splits * M * N, dtype=F32, device=out.device)
 
+    args = (a.data_ptr(), a.stride(0), int(a_kmajor), b.data_ptr(), b.stride(0), int(b_kmajor), out.data_ptr(),
+            out.stride(0), M, N, K, _p(bias), _p(resid), 0 if resid is None else resid.stride(0), out_mode, act, splits,
+            _p(workspace), float(alpha))
+
     def run():
-        call("vpt_gemm_bf16", a.data_ptr(), a.stride(0), int(a_kmajor), b.data_ptr(), b.stride(0), int(b_kmajor),
-             out.data_ptr(), out.stride(0), M, N, K, _p(bias), _p(resid), 0 if resid is None else resid.stride(0),
-             out_mode, act, splits, _p(workspace), float(alpha), stream())
+        if geometry or ring_grid:
+            call("vpt_gemm_bf16_tiled", *args, int(geometry), int(ring_grid), stream())
+        else:
+            call("vpt_gemm_bf16", *args, stream())
     pr = PROBES.get("gemm")
     if pr is None:
         run()
@@ -94,31 +109,31 @@ def gemm(a, a_kmajor: bool, b, b_kmajor: bool, M: int, N: int, K: int, out, *, b
     return out
 
 
-def linear(x, w, bias=None, resid=None, out=None, act=ACT_NONE):
+def linear(x, w, bias=None, resid=None, out=None, act=ACT_NONE, **tile):
     """y = x @ w.T (+bias) (+resid) in bf16 — nn.Linear forward."""
     M, K = x.shape
     N = w.shape[0]
     if out is None:
         out = torch.empty(M, N, dtype=BF16, device=x.device)
-    return gemm(x, True, w, True, M, N, K, out, bias=bias, resid=resid, act=act)
+    return gemm(x, True, w, True, M, N, K, out, bias=bias, resid=resid, act=act, **tile)
 
 
-def linear_dgrad(dy, w, out=None, resid=None):
+def linear_dgrad(dy, w, out=None, resid=None, **tile):
     """dx = dy @ w (+resid) (dy [M,N], w [N,K]) — nn.Linear input gradient (resid: a second bf16 gradient
     of the same input, summed with the reference's bf16 rounding)."""
     M, N = dy.shape
     K = w.shape[1]
     if out is None:
         out = torch.empty(M, K, dtype=BF16, device=dy.device)
-    return gemm(dy, True, w, False, M, K, N, out, resid=resid)
+    return gemm(dy, True, w, False, M, K, N, out, resid=resid, **tile)
 
 
-def linear_wgrad(dy, x, out, accumulate=False, splits=1, workspace=None):
+def linear_wgrad(dy, x, out, accumulate=False, splits=1, workspace=None, **tile):
     """dW (=|+=) dy.T @ x in f32 (dy [M,N], x [M,K], out [N,K]) — nn.Linear weight gradient."""
     M, N = dy.shape
     K = x.shape[1]
     return gemm(dy, False, x, False, N, K, M, out, out_mode=OUT_F32_ACC if accumulate else OUT_F32,
-                splits=splits, workspace=workspace)
+                splits=splits, workspace=workspace, **tile)
 
 
 def linear_swiglu(x, w12, b12, x12, h):
@@ -188,8 +203,9 @@ def rmsnorm_fwd(x, w, out=None, rstd=None, eps=1e-6):
         out = torch.empty(M, D, dtype=BF16, device=x.device)
     if rstd is None:
         rstd = torch.empty(M, dtype=F32, device=x.device)
-    call("vpt_rmsnorm_fwd", x.data_ptr(), x.stride(0), w.data_ptr(), out.data_ptr(), out.stride(0), rstd.data_ptr(),
-         M, D, eps, stream())
+    _launch("rmsnorm_fwd", M * D * 4 + M * 4,  # bf16 x in, bf16 y out, f32 rstd
+            lambda: call("vpt_rmsnorm_fwd", x.data_ptr(), x.stride(0), w.data_ptr(), out.data_ptr(), out.stride(0),
+                         rstd.data_ptr(), M, D, eps, stream()))
     return out, rstd
 
 
@@ -204,9 +220,11 @@ def rmsnorm_bwd(dy, x, rstd, w, dres=None, dx=None, dw_part=None):
         dx = torch.empty(M, D, dtype=BF16, device=x.device)
     if dw_part is None:
         dw_part = torch.empty(rmsnorm_bwd_blocks(M), D, dtype=F32, device=x.device)
-    call("vpt_rmsnorm_bwd", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), rstd.data_ptr(), w.data_ptr(),
-         _p(dres), 0 if dres is None else dres.stride(0), dx.data_ptr(), dx.stride(0), dw_part.data_ptr(), M, D,
-         stream())
+    nbytes = M * D * (6 + (2 if dres is not None else 0)) + M * 4 + dw_part.numel() * 4  # dy, x, (dres) in; dx out
+    _launch("rmsnorm_bwd", nbytes,
+            lambda: call("vpt_rmsnorm_bwd", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), rstd.data_ptr(),
+                         w.data_ptr(), _p(dres), 0 if dres is None else dres.stride(0), dx.data_ptr(), dx.stride(0),
+                         dw_part.data_ptr(), M, D, stream()))
     return dx, dw_part
 
 
@@ -223,8 +241,10 @@ def qknorm_rope_fwd(qkv, wq, wk, cos_t, sin_t, rows_per_seq, out=None, eps=1e-6,
     D = qkv.shape[1] // 3
     if out is None:
         out = torch.empty(M, 2 * D, dtype=BF16, device=qkv.device)
-    call("vpt_qknorm_rope_fwd", qkv.data_ptr(), qkv.stride(0), wq.data_ptr(), wk.data_ptr(), cos_t.data_ptr(),
-         sin_t.data_ptr(), out.data_ptr(), out.stride(0), M, rows_per_seq, D, eps, float(q_scale), stream())
+    _launch("qknorm_rope_fwd", M * 2 * D * 4,  # q, k bf16 in and out (the RoPE table is L2-resident)
+            lambda: call("vpt_qknorm_rope_fwd", qkv.data_ptr(), qkv.stride(0), wq.data_ptr(), wk.data_ptr(),
+                         cos_t.data_ptr(), sin_t.data_ptr(), out.data_ptr(), out.stride(0), M, rows_per_seq, D, eps,
+                         float(q_scale), stream()))
     return out
 
 
@@ -238,9 +258,10 @@ def qknorm_rope_bwd(dqk, qkv, wq, wk, cos_t, sin_t, rows_per_seq, dqkv, dw_part=
     D = qkv.shape[1] // 3
     if dw_part is None:
         dw_part = torch.empty(qknorm_rope_blocks(M), 128, dtype=F32, device=qkv.device)
-    call("vpt_qknorm_rope_bwd", dqk.data_ptr(), dqk.stride(0), qkv.data_ptr(), qkv.stride(0), wq.data_ptr(),
-         wk.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(), dqkv.data_ptr(), dqkv.stride(0), dw_part.data_ptr(), M,
-         rows_per_seq, D, eps, stream())
+    _launch("qknorm_rope_bwd", M * 2 * D * 6,  # dq, dk and q, k in; dq, dk out (bf16)
+            lambda: call("vpt_qknorm_rope_bwd", dqk.data_ptr(), dqk.stride(0), qkv.data_ptr(), qkv.stride(0),
+                         wq.data_ptr(), wk.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(), dqkv.data_ptr(),
+                         dqkv.stride(0), dw_part.data_ptr(), M, rows_per_seq, D, eps, stream()))
     return dw_part
 
 
@@ -286,8 +307,9 @@ def attn_bwd(q, k, v, o, do, lse, delta, kbias, dq, dk, dv, B, H, rows, n, n_den
 
 # ----------------------------------------------------------------------------- misc
 def patchify(img, B, H, W, out, t=None, noise=None, noise_scale=1.0, seed=0, noising=True):
-    call("vpt_patchify", img.data_ptr(), 0 if noising else 1, _p(noise), _p(t), noise_scale, seed, B, H, W,
-         out.data_ptr(), stream())
+    _launch("patchify", B * 3 * H * W * (4 + (2 if noise is not None else 0)),  # fp16 pixel in, bf16 out
+            lambda: call("vpt_patchify", img.data_ptr(), 0 if noising else 1, _p(noise), _p(t), noise_scale, seed, B,
+                         H, W, out.data_ptr(), stream()))
     return out
 
 
@@ -309,8 +331,9 @@ def loss_blocks() -> int:
 
 def flow_loss(pred, img, t, B, H, W, dpred, part, loss, target=0, t_eps=0.05, noise=None, noise_scale=1.0,
               seed=0):
-    call("vpt_flow_loss", pred.data_ptr(), img.data_ptr(), _p(noise), t.data_ptr(), noise_scale, seed, target,
-         t_eps, B, H, W, dpred.data_ptr(), part.data_ptr(), loss.data_ptr(), stream())
+    _launch("flow_loss", B * 3 * H * W * (6 + (2 if noise is not None else 0)),  # pred, image in; dpred out
+            lambda: call("vpt_flow_loss", pred.data_ptr(), img.data_ptr(), _p(noise), t.data_ptr(), noise_scale, seed,
+                         target, t_eps, B, H, W, dpred.data_ptr(), part.data_ptr(), loss.data_ptr(), stream()))
     return loss
 
 
@@ -357,8 +380,9 @@ def bias_grad(dy, out, part=None, accumulate=False):
     if part is None:
         part = torch.empty(nb, N, dtype=F32, device=dy.device)
     part = part.view(-1)[: nb * N]
-    call("vpt_bias_grad", dy.data_ptr(), dy.stride(0), M, N, part.data_ptr(), out.data_ptr(), int(accumulate),
-         stream())
+    _launch("bias_grad", M * N * 2 + nb * N * 8,  # dy read once; partials written and read back
+            lambda: call("vpt_bias_grad", dy.data_ptr(), dy.stride(0), M, N, part.data_ptr(), out.data_ptr(),
+                         int(accumulate), stream()))
     return out
 
 
@@ -399,8 +423,15 @@ def cast_f32_bf16(x, out):
 
 def radam_sf_step(y, grad, z, v, *, beta2, bias_correction2, eps, ckp1, adaptive_y_lr, lr, decay, grad_scale,
                   adam):
-    call("vpt_radam_sf_step", y.data_ptr(), grad.data_ptr(), z.data_ptr(), v.data_ptr(), y.numel(), beta2,
-         bias_correction2, eps, ckp1, adaptive_y_lr, lr, decay, grad_scale, int(adam), stream())
+    """grad f32, or bf16 (the all-reduced bf16 wire buffer of vpt.ddp.GradSync)."""
+    if grad.dtype not in (F32, BF16) or grad.numel() != y.numel():
+        raise ValueError("grad must be f32 or bf16 with y's size")
+    gb = grad.dtype == BF16
+    _launch("radam_sf_step", y.numel() * (22 if gb else 24),  # y bf16, grad, z / v f32 in; y, z, v out
+            lambda: call("vpt_radam_sf_step", y.data_ptr(), grad.data_ptr(), int(gb), z.data_ptr(), v.data_ptr(),
+                         y.numel(),
+                         beta2, bias_correction2, eps, ckp1, adaptive_y_lr, lr, decay, grad_scale, int(adam),
+                         stream()))
 
 
 def sf_lerp(y, z, w):

@@ -9,9 +9,11 @@ parity is unpinned — the update below follows the published algorithm):
   rect = sqrt((rho_t-4)(rho_t-2) rho_inf / ((rho_inf-4)(rho_inf-2) rho_t)) if rho_t > 4
          else (0 if silent_sgd_phase else 1)
   lr_t = lr * rect ; scheduled_lr = lr_t ; lr_max = max(lr_max, lr_t)
-  weight = (k+1)^p * lr_max^p ; weight_sum += weight ; ckp1 = weight / weight_sum (0 if 0/0)
+  weight = (k+1)^r * lr_max^weight_lr_power ; weight_sum += weight ; ckp1 = weight / weight_sum (0 if 0/0)
   v = beta2 v + (1-beta2) g^2 ; g <- g / (sqrt(v / bc2) + eps)  (only when rho_t > 4)
-  g += wd * y ; y <- lerp(y, z, ckp1) + lr_t (beta1 (1-ckp1) - 1) g ; z <- z - lr_t g
+  g += wd * y ; y <- lerp(y, z, ckp1) ; y <- y + lr_t (beta1 (1-ckp1) - 1) g ; z <- z - lr_t g
+  (y is the bf16 parameter: rounded after the lerp and after the add, as the reference's two
+  in-place foreach ops on a bf16 tensor round it)
 and train()/eval() swap y <-> x via p.lerp_(z, 1-beta1) / p.lerp_(z, 1-1/beta1).
 
 Differences from the reference by design: z and v are kept in f32 (the reference keeps them in the
@@ -74,8 +76,7 @@ class RAdamScheduleFreeFlat:
             rect = float(not g["silent_sgd_phase"])
         lr = g["lr"] * rect
         lr_max = max(lr, g["lr_max"])
-        p = g["weight_lr_power"]
-        weight = (step ** p) * (lr_max ** p)
+        weight = (step ** g["r"]) * (lr_max ** g["weight_lr_power"])
         weight_sum = g["weight_sum"] + weight
         ckp1 = weight / weight_sum if weight_sum != 0 else 0.0
         return dict(step=step, bc2=bc2, adam=rho_t > 4.0, lr=lr, lr_max=lr_max, weight_sum=weight_sum, ckp1=ckp1,
@@ -95,11 +96,14 @@ class RAdamScheduleFreeFlat:
         return self.scalars()
 
     @torch.no_grad()
-    def apply_range(self, s: dict, lo: int, hi: int, grad_scale: float = 1.0):
+    def apply_range(self, s: dict, lo: int, hi: int, grad_scale: float = 1.0, grad: torch.Tensor | None = None):
+        """Steps parameters [lo, hi) from self.grads[lo:hi], or from `grad` (f32 or bf16, the range's
+        all-reduced wire buffer) when given."""
         g = self.param_groups[0]
         if hi <= lo:
             return
-        ops.radam_sf_step(self.params[lo:hi], self.grads[lo:hi], self.z[lo:hi], self.v[lo:hi], beta2=s["beta2"],
+        src = self.grads[lo:hi] if grad is None else grad
+        ops.radam_sf_step(self.params[lo:hi], src, self.z[lo:hi], self.v[lo:hi], beta2=s["beta2"],
                           bias_correction2=s["bc2"], eps=g["eps"], ckp1=s["ckp1"], adaptive_y_lr=s["adaptive_y_lr"],
                           lr=s["lr"], decay=g["weight_decay"], grad_scale=grad_scale, adam=s["adam"])
 
