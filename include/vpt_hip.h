@@ -83,6 +83,7 @@ int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr, const void* k, 
                  long l_sh, const float* kbias, long kb_sb, void* dq, long dq_sb, long dq_sh, long dq_sr,
                  void* dk, long dk_sb, long dk_sh, long dk_sr, void* dv, long dv_sb, long dv_sh, long dv_sr,
                  int B, int H, int n, int nk, int n_dense, float scale, void* stream);
+
 /* ---- RMSNorm over the hidden dim -----------------------------------------------------------
  * Replaces FP32RMSNorm.forward src/modules/norm.py:20-27 (norm1/norm2/norm_final,
  * src/models/jit/denoiser.py:521,600,625) and its backward (dx = dres + RMSNorm'(dy);

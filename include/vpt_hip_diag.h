@@ -27,10 +27,15 @@ int vpt_gemm_set_debug(unsigned long long* buf);
 int vpt_gemm_set_ring_grid(int blocks);
 /* Forward lazy-rescale threshold in log2 units (default 8; 0 = rescale whenever the row max grows). */
 int vpt_attn_set_rescale_threshold(float tau);
-/* Attention kernel variant: 0 = production; 1 / 2 = timing-only backward ablations (WRONG results);
+/* Attention kernel variant: 0 = production (split dK/dV + dQ kernels); 13 = fused single-pass backward
+ * with f32 dQ atomics (correct); 10-12 = its timing ablations (WRONG results: no atomics / plain stores /
+ * no dQ product); 1 / 2 = timing-only backward ablations (WRONG results);
  * 3 = 8-wave blocks (correct); 4-7 = dK/dV timing ablations (WRONG results); 8 = the previous
  * compiler-scheduled dK/dV body (correct). */
 int vpt_attn_set_variant(int v);
+/* f32 dQ accumulator of the fused backward variants 10-13: [B*H][round_up(n, 64)][64]. */
+long vpt_attn_fused_workspace_bytes(int B, int H, int n);
+int vpt_attn_set_fused_workspace(void* ws);
 
 #ifdef __cplusplus
 }

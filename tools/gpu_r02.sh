@@ -7,7 +7,7 @@ TAG=${1:-r02a}
 O=gpurun_out/$TAG
 mkdir -p $O
 if [ "$2" != "skip_tests" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "TESTS FAILED"; tail -60 $O/gpu_tests.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=5 -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "TESTS FAILED"; tail -60 $O/gpu_tests.log; exit 1; }
   tail -3 $O/gpu_tests.log
   timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && cat $O/smoke.log || exit 1
 fi

@@ -83,9 +83,12 @@ DIAG_SIGNATURES: dict[str, list] = {
     "vpt_gemm_set_ring_grid": [I],
     "vpt_attn_set_rescale_threshold": [F],
     "vpt_attn_set_variant": [I],
+    "vpt_attn_fused_workspace_bytes": [I, I, I],
+    "vpt_attn_set_fused_workspace": [P],
 }
 _RESTYPES = {
     "vpt_gemm_workspace_bytes": C.c_long,
+    "vpt_attn_fused_workspace_bytes": C.c_long,
     "vpt_cover_resize_crop_workspace": C.c_long,
     "vpt_gemm_swiglu_bwd_workspace": C.c_long,
     "vpt_attn_q_scale": C.c_float,
@@ -93,7 +96,7 @@ _RESTYPES = {
     "vpt_build_info": C.c_char_p,
 }
 # Entry points that return a value (size / count / string) rather than a status code.
-_VALUE_FNS = {"vpt_gemm_workspace_bytes", "vpt_cover_resize_crop_workspace", "vpt_gemm_swiglu_bwd_workspace", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
+_VALUE_FNS = {"vpt_gemm_workspace_bytes", "vpt_attn_fused_workspace_bytes", "vpt_cover_resize_crop_workspace", "vpt_gemm_swiglu_bwd_workspace", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
               "vpt_colsum_blocks", "vpt_attn_q_scale", "vpt_last_error_string", "vpt_abi_version", "vpt_build_info"}
 
 

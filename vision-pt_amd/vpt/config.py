@@ -58,6 +58,11 @@ class DenoiserConfig(BaseModel):
         # SwiGLU(dim, hidden_dim=int(D*mlp_ratio)) uses int(hidden_dim * 2 / 3) (denoiser.py:490, 641-646)
         return int(int(self.hidden_size * self.mlp_ratio) * 2 / 3)
 
+    @property
+    def mlp_hidden_padded(self) -> int:
+        """SwiGLU hidden width as stored and computed (zero-padded to a multiple of 64; vpt.params)."""
+        return (self.mlp_hidden + 63) // 64 * 64
+
 
 class JiT_B_16_Config(DenoiserConfig):
     patch_size: int = 16

@@ -69,7 +69,7 @@ class JiTEngine:
         self.pool_infer = _Pool(self.device)  # no-grad forwards never clobber saved activations
         self.rope = RopeCache(cfg, self.device)
         self.D = cfg.hidden_size
-        self.F = cfg.mlp_hidden
+        self.F = cfg.mlp_hidden_padded  # zero-padded SwiGLU width (vpt.params.ParamSpec)
         self.H = cfg.num_heads
         self.T = cfg.num_time_tokens
         self._state = None
@@ -95,7 +95,7 @@ class JiTEngine:
                 d[store + "n2"] = L.view(src, pre + "norm2.weight")
                 d[store + "w12"] = L.span(src, pre + "mlp.w_1.weight", pre + "mlp.w_2.weight", (2 * F, D))
                 d[store + "b12"] = L.span(src, pre + "mlp.w_1.bias", pre + "mlp.w_2.bias", (2 * F,))
-                d[store + "w3"] = L.view(src, pre + "mlp.w_3.weight")
+                d[store + "w3"] = L.phys(src, pre + "mlp.w_3.weight")
                 d[store + "b3"] = L.view(src, pre + "mlp.w_3.bias")
             self.blk.append(d)
         fin = {}
@@ -103,7 +103,7 @@ class JiTEngine:
             fin[store + "n"] = L.view(src, "final_layer.norm_final.weight")
             fin[store + "w12"] = L.span(src, "final_layer.mlp.w_1.weight", "final_layer.mlp.w_2.weight", (2 * F, D))
             fin[store + "b12"] = L.span(src, "final_layer.mlp.w_1.bias", "final_layer.mlp.w_2.bias", (2 * F,))
-            fin[store + "w3"] = L.view(src, "final_layer.mlp.w_3.weight")
+            fin[store + "w3"] = L.phys(src, "final_layer.mlp.w_3.weight")
             fin[store + "b3"] = L.view(src, "final_layer.mlp.w_3.bias")
             fin[store + "wl"] = L.view(src, "final_layer.linear.weight")
             fin[store + "bl"] = L.view(src, "final_layer.linear.bias")

@@ -21,18 +21,34 @@ from .config import DenoiserConfig
 ALIGN = 64  # elements; keeps every view 128-B aligned in bf16 and 256-B in f32
 
 
+def _prod(shape) -> int:
+    n = 1
+    for s in shape:
+        n *= s
+    return n
+
+
 @dataclass(frozen=True)
 class ParamSpec:
+    """`shape` is the reference's (logical) shape; `stored` the physical one in the flat buffer, which
+    differs only for SwiGLU tensors whose hidden width F is not a multiple of 64 (e.g. JiT tiny: F =
+    int(1024 * 2 / 3) = 682): they are stored zero-padded to F_pad (w_1 / w_2 rows and biases, w_3
+    columns), so the GEMM operands keep 128-B aligned rows. The padding stays exactly zero through
+    training (zero weights give zero activations, zero activations give zero gradients, and the
+    optimizer keeps a zero parameter with zero gradient at zero)."""
     name: str
     shape: tuple
     offset: int
+    stored: tuple | None = None
+
+    @property
+    def phys_shape(self) -> tuple:
+        return self.stored if self.stored is not None else self.shape
 
     @property
     def numel(self) -> int:
-        n = 1
-        for s in self.shape:
-            n *= s
-        return n
+        """Elements occupied in the flat buffer (physical)."""
+        return _prod(self.phys_shape)
 
 
 def block_param_names(i: int) -> list[str]:
@@ -103,11 +119,15 @@ class ParamLayout:
         tight = set()
         for grp in _contiguous_groups(cfg):
             tight.update(grp[1:])  # members after the first follow without alignment padding
+        F, Fp = cfg.mlp_hidden, cfg.mlp_hidden_padded
         specs, off = [], 0
         for name, shape in param_shapes(cfg, n_classes):
             if name not in tight:
                 off = (off + ALIGN - 1) // ALIGN * ALIGN
-            s = ParamSpec(name, shape, off)
+            stored = None
+            if Fp != F and ".mlp.w_" in name:
+                stored = tuple(Fp if (d == F and (i == 0) == (".w_3." not in name)) else d for i, d in enumerate(shape))
+            s = ParamSpec(name, shape, off, stored)
             specs.append(s)
             off += s.numel
         self.total = (off + ALIGN - 1) // ALIGN * ALIGN
@@ -115,8 +135,17 @@ class ParamLayout:
         self.by_name = {s.name: s for s in specs}
 
     def view(self, flat: torch.Tensor, name: str) -> torch.Tensor:
+        """The parameter in its reference shape (a strided view for column-padded w_3)."""
         s = self.by_name[name]
-        return flat[s.offset:s.offset + s.numel].view(s.shape)
+        v = flat[s.offset:s.offset + s.numel].view(s.phys_shape)
+        if s.stored is None:
+            return v
+        return v[tuple(slice(0, d) for d in s.shape)]
+
+    def phys(self, flat: torch.Tensor, name: str) -> torch.Tensor:
+        """The parameter in its stored (padded) shape, as the kernels read it."""
+        s = self.by_name[name]
+        return flat[s.offset:s.offset + s.numel].view(s.phys_shape)
 
     def span(self, flat: torch.Tensor, first: str, last: str, shape: tuple) -> torch.Tensor:
         """View spanning adjacent params first..last (a fused operand)."""
