@@ -119,6 +119,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--breakdown", default=None, help="write per-shape GEMM probe totals (JSON) to this file")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -210,6 +211,11 @@ def main():
         gbs = nb / (ms * 1e-3) / 1e9 if ms else 0.0
         hbm[k] = dict(launches=n, mean_ms=round(ms, 4), mean_mb=round(nb / 1e6, 3), gb_s=round(gbs, 1),
                       frac=round(gbs / PEAK_HBM_GBS, 3))
+    if args.breakdown and rank == 0:
+        rows = {k: dict(launches=n, ms_per_step=round(t / n_probe, 4), tflops=round(w / (t * 1e-3) / 1e12, 1))
+                for k, (n, t, w) in probes["gemm"].by_key().items()}
+        rows = dict(sorted(rows.items(), key=lambda kv: -kv[1]["ms_per_step"]))
+        json.dump(rows, open(args.breakdown, "w"), indent=1)
     dom = max(stats, key=lambda k: stats[k]["total_ms"])
     ach = stats[dom]["tflops"]
     traffic, traffic_src = measured_traffic(dom)

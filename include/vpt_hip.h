@@ -197,6 +197,19 @@ int vpt_geglu_bwd(const void* dy, const void* x12, long ldx, int F, long M, void
  * quantize (quantize_4bit, load time) uses absmax_scratch f32 [n/64]. */
 int vpt_nf4_dequant(const void* packed, const void* qabsmax, const float* absmax2, const float* code2,
                     const float* offset, long n, void* out, void* stream);
+/* NF4 dequant-in-GEMM with the LoRA up-projection fused as one extra K tile (replaces, per QLoRA target,
+ * LoRALinear.forward src/modules/peft/lora.py:92-104 = Linear4bit's dequantize_4bit + matmul
+ * (src/modules/quant/bnb.py:37-129) + lora_up(lora_down(x)) * scale + add, and their input gradient).
+ * W: the NF4 tensor above, [N_w][kw] (kw = input features). w_kmajor = 1 (forward): C[M][N] = A[M][K] .
+ * Wd^T + bias + lora_a[M][r] . lora_b[N][r]^T with K = kw, N = N_w. w_kmajor = 0 (input gradient):
+ * C[M][N] = A[M][K] . Wd + lora_a[M][r] . lora_b[r][N] with K = N_w, N = kw (N % 64 == 0). lora_a null:
+ * no LoRA term; the caller pre-scales lora_a by alpha / rank. K % 64 == 0, 0 < r <= 64. The dequantised
+ * weight never exists in HBM (bit-identical values to vpt_nf4_dequant, computed per tile in LDS).
+ * out_mode 0 bf16 (resid: + bf16 residual, reference rounding) / 1 f32; alpha scales the accumulator. */
+int vpt_gemm_nf4(const void* A, long lda, const void* packed, const void* qabsmax, const float* absmax2,
+                 const float* code2, const float* offset, long kw, int w_kmajor, const void* lora_a, long lda2,
+                 const void* lora_b, long ldb2, int r, void* C, long ldc, int M, int N, int K, const void* bias,
+                 const void* resid, long ldr, int out_mode, float alpha, void* stream);
 /* Elementwise bf16: out = a + b (residual sums), out = s * a (LoRA scale gradient); n % 8 == 0. */
 int vpt_add_bf16(const void* a, const void* b, long n, void* out, void* stream);
 int vpt_scale_bf16(const void* a, long n, float s, void* out, void* stream);

@@ -21,6 +21,10 @@ Fixtures:
                          dim 128, 2 heads, context_dim 96, 2 x 80 tokens, 20 context tokens. Forward output
                          and gradients (input, context, every LoRA weight) of sum(out * dy), once in fp32
                          with fp32 attention and once in the reference's native bf16.
+  timestep.safetensors   sample_timestep for the scale_shift_sigmoid / sigmoid / uniform / shift_sigmoid /
+                         flux_shift samplers (two latent shapes, two global-RNG seeds, non-default kwargs).
+  init.safetensors       JiT.initialize_weights + ClassEncoder.initialize_weights on the micro config: per
+                         parameter the kind (normal / ones / zeros), mean, std, numel.
   sampler.safetensors    JiTModel.generate (src/models/jit/pipeline.py:378-488) on the micro config,
                          float32 execution, class context, 4 Euler steps, 2 x 64x48: starting noise,
                          token ids/masks and the final image for four cases (CFG 2.0; no CFG; CFG 3.0
@@ -258,12 +262,60 @@ def sdxl_block_fixture(meta):
                                                        B=B, n=n, nc=nc, weight_seed=11))))
 
 
+def timestep_fixture(meta):
+    """sample_timestep (src/modules/timestep/sampling.py:170-187) for every sampler type the JiT / SDXL
+    flow-match steps select, drawn from the global RNG after torch.manual_seed(seed) on CPU."""
+    samp = importlib.import_module("src.modules.timestep.sampling")
+    cases = {"scale_shift_sigmoid": {}, "scale_shift_sigmoid_m0s1": {"mean": 0.0, "std": 1.0}, "sigmoid": {},
+             "uniform": {}, "shift_sigmoid": {}, "flux_shift": {}, "shift_sigmoid_s2": {"sigmoid_scale": 2.0}}
+    out = {}
+    for name, kw in cases.items():
+        typ = name.split("_m0")[0].split("_s2")[0]
+        for shape in ((16, 3, 256, 256), (8, 4, 128, 96)):
+            for seed in (0, 7):
+                torch.manual_seed(seed)
+                t = samp.sample_timestep(latents_shape=torch.Size(shape), device="cpu", sampling_type=typ, **kw)
+                out[f"{name}/{'x'.join(map(str, shape))}/{seed}"] = t.float().contiguous()
+    save_file(out, os.path.join(HERE, "timestep.safetensors"),
+              metadata=dict(meta, cases=json.dumps({k: v for k, v in cases.items()})))
+
+
+def init_fixture(R, meta):
+    """JiT.initialize_weights (src/models/jit/denoiser.py:764-798) + ClassEncoder.initialize_weights
+    (class_encoder.py:124-125) on the micro config: per parameter [kind (0 normal / 1 ones / 2 zeros), mean,
+    std, numel] -- the distribution each tensor is drawn from (the RNG stream itself is not part of the API)."""
+    oc = micro_config()
+    torch.manual_seed(0)
+    model = R.den.Denoiser(ref_config(R, oc))
+    model.initialize_weights()
+    enc = R.ce.ClassEncoder(label2id={f"c{i}": i for i in range(20)}, embedding_dim=oc.context_dim)
+    enc.initialize_weights()
+    named = dict(model.named_parameters())
+    named["class_encoder.embedding.weight"] = enc.embedding.weight
+    names = sorted(named)
+    rows = []
+    for n in names:
+        t = named[n].detach().double()
+        kind = 1 if bool((t == 1).all()) else 2 if bool((t == 0).all()) else 0
+        rows.append([kind, t.mean().item(), t.std().item() if t.numel() > 1 else 0.0, t.numel()])
+    save_file({"stats": torch.tensor(rows, dtype=torch.float64)}, os.path.join(HERE, "init.safetensors"),
+              metadata=dict(meta, names=json.dumps(names)))
+
+
 def main():
     R = import_reference()
     meta = {"torch": torch.__version__, "threads": str(torch.get_num_threads()), "reference": REF}
     if len(sys.argv) > 1 and sys.argv[1] == "sampler":
         sampler_fixture(R, meta)
         print("sampler", os.path.getsize(os.path.join(HERE, "sampler.safetensors")))
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "init":
+        init_fixture(R, meta)
+        print("init", os.path.getsize(os.path.join(HERE, "init.safetensors")))
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "timestep":
+        timestep_fixture(meta)
+        print("timestep", os.path.getsize(os.path.join(HERE, "timestep.safetensors")))
         return
     if len(sys.argv) > 1 and sys.argv[1] == "sdxl":
         sdxl_block_fixture(meta)
@@ -348,7 +400,9 @@ def main():
     save_file({k: v.contiguous() for k, v in ops.items()}, os.path.join(HERE, "ops.safetensors"), metadata=meta_ops)
     sampler_fixture(R, meta)
     sdxl_block_fixture(meta)
-    for f in ("jit_micro", "jit_c1", "ops", "sampler", "sdxl_block"):
+    timestep_fixture(meta)
+    init_fixture(R, meta)
+    for f in ("jit_micro", "jit_c1", "ops", "sampler", "sdxl_block", "timestep", "init"):
         print(f, os.path.getsize(os.path.join(HERE, f + ".safetensors")))
 
 

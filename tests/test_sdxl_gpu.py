@@ -110,6 +110,71 @@ def test_nf4_quantize_matches_oracle(ops):
     assert rel(deq, SO.nf4_dequantize(ref).bfloat16().float()) < 1e-3
 
 
+@pytest.mark.parametrize("forward", [True, False])
+@pytest.mark.parametrize("lora", [False, True])
+def test_gemm_nf4_bit_exact_vs_dequant_gemm(ops, forward, lora):
+    """vpt_gemm_nf4 (dequant inside the GEMM, LoRA as an extra K tile) == vpt_nf4_dequant + the T128 bf16
+    GEMM over the concatenated operands [A | lora_a] . [W | lora_b] (same MFMA order: bit-exact), at a
+    partial M tile, 5 N tiles and both weight orientations."""
+    from vpt.sdxl import NF4Weight
+    Nw, Kw, M, r = 1280, 640, 300, 16
+    g = torch.Generator().manual_seed(12)
+    st = SO.nf4_quantize(torch.randn(Nw, Kw, generator=g) * 0.05)
+    w = NF4Weight.from_state(dict(st, shape=torch.tensor([Nw, Kw])))
+    Wd = w.dequantize()
+    N, K = (Nw, Kw) if forward else (Kw, Nw)
+    a = rnd(M, K, seed=13)
+    la = rnd(M, r, scale=0.5, seed=14) if lora else None
+    lb = (rnd(N, r, scale=0.1, seed=15) if forward else rnd(r, N, scale=0.1, seed=15)) if lora else None
+    bias = rnd(N, scale=0.1, seed=16) if forward else None
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops.gemm_nf4(a, w, forward, out, lora_a=la, lora_b=lb, bias=bias)
+    # reference: one dense GEMM over K + 64 (the LoRA tile zero-padded to 64 k), T128 geometry
+    pad = 64
+    a2 = torch.zeros(M, K + pad, dtype=torch.bfloat16, device=DEV)
+    a2[:, :K] = a
+    if forward:
+        b2 = torch.zeros(N, K + pad, dtype=torch.bfloat16, device=DEV)
+        b2[:, :K] = Wd
+        if lora:
+            a2[:, K:K + r] = la
+            b2[:, K:K + r] = lb
+        ref = torch.empty_like(out)
+        ops.gemm(a2 if lora else a, True, b2 if lora else Wd, True, M, N, K + (pad if lora else 0), ref, bias=bias,
+                 geometry=128)
+    else:
+        b2 = torch.zeros(K + pad, N, dtype=torch.bfloat16, device=DEV)
+        b2[:K] = Wd
+        if lora:
+            a2[:, K:K + r] = la
+            b2[K:K + r] = lb
+        ref = torch.empty_like(out)
+        ops.gemm(a2 if lora else a, True, b2 if lora else Wd, False, M, N, K + (pad if lora else 0), ref, geometry=128)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref), (out.float() - ref.float()).abs().max().item()
+
+
+def test_lora_linear_nf4_fused_vs_dequant_path(ops):
+    """The fused LoRALinearNF4 path and the dequant-to-scratch path agree (same math, one vs three bf16
+    roundings of the LoRA sum): rel <= 1e-2 on y, dx and both adapter grads, at SDXL's 640 / 2048 widths."""
+    from vpt.sdxl import LoRALinearNF4, NF4Weight
+    g = torch.Generator().manual_seed(17)
+    st = SO.nf4_quantize(torch.randn(640, 2048, generator=g) * 0.03)
+    base = NF4Weight.from_state(dict(st, shape=torch.tensor([640, 2048])))
+    down, up = rnd(16, 2048, scale=0.05, seed=18), rnd(640, 16, scale=0.05, seed=19)
+    bias = rnd(640, scale=0.1, seed=20)
+    x, dy = rnd(700, 2048, seed=21), rnd(700, 640, seed=22)
+    res = []
+    for fused in (True, False):
+        lin = LoRALinearNF4(base, bias, down, up, alpha=16.0, rank=16)
+        lin.fused = fused
+        y = lin.forward(x)
+        dx = lin.backward(dy)
+        res.append((y, dx, lin.g_up.clone(), lin.g_down.clone()))
+    for u, v in zip(*res):
+        assert rel(u, v) < 1e-2
+
+
 def _block_inputs():
     with safe_open(GOLD, "pt") as f:
         d = json.loads(f.metadata()["dims"])

@@ -812,6 +812,11 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
     float bias8[8], bias8b[8];
     unpack8(braw, bias8);
     unpack8(braw2, bias8b);
+    // The bias values must be in registers BEFORE the next item's LDS-DMA below: the compiler does not
+    // see the asm DMA, places its wait for the bias loads at their first use (in the epilogue) as
+    // vmcnt(0), and vmcnt retires in order -- that wait would drain the next item's prefetched tiles.
+#pragma unroll
+    for (int e = 0; e < 8; ++e) asm volatile("" : "+v"(bias8[e]), "+v"(bias8b[e]));
     // Every wave has passed its last K step (barrier X_nk), so ring stages 0-2 are free: DMA the next
     // item's first tiles before this item's epilogue (which stages through stage 3 only).
     const int next = item + gridDim.x;
@@ -1095,4 +1100,185 @@ extern "C" int vpt_gemm_swiglu_bwd(const void* dy, long lddy, const void* w3, lo
   g.out_mode = OUT_BF16; g.act = ACT_NONE; g.alpha = 1.f;
   g.sw = 2;
   return launch_ring<true, false, true>(g, 1, (hipStream_t)stream);
+}
+
+// ---- NF4 dequant-in-GEMM with a fused LoRA K-extension (SDXL QLoRA, BASELINE config 5) ----------------
+// Replaces, for every QLoRA target Linear (src/modules/peft/lora.py:92-104 over bnb Linear4bit,
+// src/modules/quant/bnb.py:37-129), bnb's dequantize_4bit into a bf16 weight in HBM + the GEMM + the LoRA
+// up-projection GEMM + the add, in both directions:
+//   forward  y  = x . Wd^T (+ bias) + ds . up^T        Wd [N][K] NF4 (k-major B), ds = s * x . down^T [M][r]
+//   dgrad    dx = dy . Wd       + vs . down            Wd read mn-major (B(n, k) = W[k][n]), vs = s * dy . up [M][r]
+// The NF4 B tile (128 weight rows x one 64-element NF4 block each, or 64 rows x two half blocks) is loaded
+// as packed codes + nested absmax into registers one K step ahead, dequantised exactly as bnb's
+// dequantize_4bit (f32 NF4[code] * absmax, absmax = code2[qabsmax] * absmax2[blk / 256] + offset, then
+// bf16) and written into the same LDS tile image the bf16 kernel uses; the activation operand arrives by
+// LDS-DMA. No dequantised weight ever exists in HBM. The LoRA term is one extra K tile (r <= 64 valid k,
+// zero-filled) from (ds | vs, up | down), so the sum is taken in the f32 accumulator before the single
+// bf16 rounding. 128x128 tiles, 4 waves (T128 geometry), 2 LDS stages.
+namespace {
+struct Nf4Args {
+  const uint8_t* packed;    // [N_w * K_w / 2]
+  const uint8_t* qabsmax;   // [N_w * K_w / 64]
+  const float* absmax2;     // [ceil(N_w * K_w / 64 / 256)]
+  const float* code2;       // [256]
+  const float* offset;      // [1]
+  long kw;                  // K_w: input features of the quantised Linear (row length of W)
+  const bf16_t* A2; long lda2;  // LoRA activation operand [M][r] (k-major) or null
+  const bf16_t* B2; long ldb2;  // up [N][r] (k-major, forward) or down [r][K_w] (mn-major, dgrad)
+  int r;
+};
+
+__constant__ float kNF4g[16] = {-1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f,
+                                -0.28444138169288635f, -0.18477343022823334f, -0.09105003625154495f, 0.0f,
+                                0.07958029955625534f, 0.16093020141124725f, 0.24611230194568634f,
+                                0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
+                                0.7229568362236023f, 1.0f};
+
+// The 32 codes one thread dequantises per K step (16 packed bytes) and their block's nested absmax index.
+struct Nf4Regs {
+  uint4 codes;
+  uint32_t q;   // qabsmax byte
+  float a2;     // absmax2[blk / 256]
+};
+
+template <bool BKMAJ>
+__device__ __forceinline__ long nf4_elem(const GemmArgs& g, const Nf4Args& f, int n0, int k0, int tid) {
+  if (BKMAJ) {  // forward: B(n, k) = W[n][k]; thread -> weight row n0 + tid/2, k0 + 32 * (tid & 1)
+    const int n = min(n0 + (tid >> 1), g.N - 1);
+    return (long)n * f.kw + k0 + 32 * (tid & 1);
+  } else {      // dgrad: B(n, k) = W[k][n]; thread -> weight row k0 + tid/4, columns n0 + 32 * (tid & 3)
+    const int c = min(n0 + 32 * (tid & 3), g.N - 32);
+    return (long)(k0 + (tid >> 2)) * f.kw + c;
+  }
+}
+
+template <bool BKMAJ>
+__device__ __forceinline__ Nf4Regs nf4_load(const GemmArgs& g, const Nf4Args& f, int n0, int k0, int tid) {
+  const long e = nf4_elem<BKMAJ>(g, f, n0, k0, tid);  // first of 32 consecutive elements (one half block)
+  const long blk = e >> 6;
+  Nf4Regs r;
+  r.codes = *reinterpret_cast<const uint4*>(f.packed + (e >> 1));
+  r.q = f.qabsmax[blk];
+  r.a2 = f.absmax2[blk >> 8];
+  return r;
+}
+
+// Dequantise and write the thread's 32 elements into the stage's B image (k-major [128][64] or mn-major
+// [64][128], the layouts read_frag expects).
+template <bool BKMAJ>
+__device__ __forceinline__ void nf4_store(char* lb, const Nf4Regs& r, const float* lut, const float* code2, float off,
+                                          int tid) {
+  const float am = code2[r.q] * r.a2 + off;
+  const uint32_t w[4] = {r.codes.x, r.codes.y, r.codes.z, r.codes.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // 8 elements (4 packed bytes) per 16-B chunk
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t b = (w[i] >> (8 * j)) & 0xffu;
+      v[2 * j] = lut[b >> 4] * am;       // first element in the high nibble
+      v[2 * j + 1] = lut[b & 15u] * am;
+    }
+    const uint4 pk = pack8(v);
+    if (BKMAJ) {
+      *reinterpret_cast<uint4*>(lb + kmaj_off(tid >> 1, 4 * (tid & 1) + i)) = pk;
+    } else {
+      *reinterpret_cast<uint4*>(lb + mnmaj_off<128>(tid >> 2, 8 * (tid & 3) + 2 * i)) = pk;
+    }
+  }
+}
+
+template <bool BKMAJ>
+__global__ __launch_bounds__(256, 2) void gemm_nf4_kernel(GemmArgs g, Nf4Args f) {
+  using G = Geo<128, 128, 2, 2>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* lut = reinterpret_cast<float*>(smem + G::LDS);  // NF4 table (16) + code2 (256), after the tiles
+  float* c2 = lut + 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / 2, wn = wid % 2;
+  const int tiles_n = (g.N + 127) / 128;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int m0 = wgid / tiles_n * 128, n0 = wgid % tiles_n * 128;
+
+  if (tid < 16) lut[tid] = kNF4g[tid];
+  c2[tid] = f.code2[tid];
+  const float off = f.offset[0];
+
+  floatx4 acc[G::MI][G::NI];
+#pragma unroll
+  for (int i = 0; i < G::MI; ++i)
+#pragma unroll
+    for (int j = 0; j < G::NI; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = g.K / BK;  // K % 64 == 0 (checked on the host)
+  Nf4Regs nr = nf4_load<BKMAJ>(g, f, n0, 0, tid);
+  glds_tile<true, 128, 4>(smem, tile_ptr<true>(g.A, g.lda, m0, 0), g.lda, m0, g.M, BK, wid, lane);
+  __syncthreads();  // lut / code2 visible
+  nf4_store<BKMAJ>(smem + G::A_BYTES, nr, lut, c2, off, tid);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    char* nb = smem + (cur ^ 1) * G::STAGE;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      glds_tile<true, 128, 4>(nb, tile_ptr<true>(g.A, g.lda, m0, (kt + 1) * BK), g.lda, m0, g.M, BK, wid, lane);
+      nr = nf4_load<BKMAJ>(g, f, n0, (kt + 1) * BK, tid);
+    }
+    mma_tile<true, BKMAJ, G>(smem + cur * G::STAGE, acc, wm, wn, lane);
+    if (more) nf4_store<BKMAJ>(nb + G::A_BYTES, nr, lut, c2, off, tid);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    cur ^= 1;
+  }
+  if (f.A2) {  // LoRA K-extension: k in [0, r) of (A2, B2), zero-filled to 64
+    char* st = smem + cur * G::STAGE;
+    glds_tile<true, 128, 4>(st, tile_ptr<true>(f.A2, f.lda2, m0, 0), f.lda2, m0, g.M, f.r, wid, lane);
+    glds_tile<BKMAJ, 128, 4>(st + G::A_BYTES, tile_ptr<BKMAJ>(f.B2, f.ldb2, n0, 0), f.ldb2, n0, g.N, f.r, wid, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    zero_k_tail<true, 128, 256>(st, f.r, tid);
+    zero_k_tail<BKMAJ, 128, 256>(st + G::A_BYTES, f.r, tid);
+    __syncthreads();
+    mma_tile<true, BKMAJ, G>(st, acc, wm, wn, lane);
+    __syncthreads();
+  }
+  epilogue<G>(g, acc, smem, wid, lane, m0, n0, wm, wn, 0);
+}
+}  // namespace
+
+// fwd (w_kmajor = 1): C[M][N] = A[M][K] . Wd[N][K]^T; dgrad (w_kmajor = 0): C[M][N] = A[M][K] . Wd[K][N]
+// with Wd the NF4 weight of `kw` input features ([N][kw] forward, [K][kw = N] dgrad).
+extern "C" int vpt_gemm_nf4(const void* A, long lda, const void* packed, const void* qabsmax, const float* absmax2,
+                            const float* code2, const float* offset, long kw, int w_kmajor, const void* lora_a,
+                            long lda2, const void* lora_b, long ldb2, int r, void* C, long ldc, int M, int N, int K,
+                            const void* bias, const void* resid, long ldr, int out_mode, float alpha, void* stream) {
+  VPT_CHECK_ARG(A && packed && qabsmax && absmax2 && code2 && offset && C, "vpt_gemm_nf4: null pointer");
+  VPT_CHECK_ARG(M > 0 && N > 0 && K > 0, "vpt_gemm_nf4: empty shape");
+  VPT_CHECK_ARG(K % 64 == 0 && lda % 8 == 0 && ldc % 4 == 0, "vpt_gemm_nf4: K % 64, 16-B leading dims");
+  VPT_CHECK_ARG(w_kmajor ? (kw == K && N % 4 == 0) : (kw == N && N % 64 == 0),
+                "vpt_gemm_nf4: forward needs kw == K; dgrad needs kw == N, N % 64 == 0");
+  VPT_CHECK_ARG(!lora_a || (lora_b && r > 0 && r <= 64 && lda2 % 8 == 0 && ldb2 % 8 == 0 && (w_kmajor || N % 8 == 0)),
+                "vpt_gemm_nf4: LoRA operands need 0 < r <= 64 and 16-B leading dims");
+  VPT_CHECK_ARG(out_mode == OUT_BF16 || (out_mode == OUT_F32 && !resid), "vpt_gemm_nf4: out_mode bf16 or f32");
+  GemmArgs g = {};
+  g.A = (const bf16_t*)A; g.lda = lda;
+  g.C = C; g.ldc = ldc;
+  g.bias = (const bf16_t*)bias;
+  g.resid = (const bf16_t*)resid; g.ldr = ldr;
+  g.M = M; g.N = N; g.K = K;
+  g.k_split = K; g.splits = 1; g.split_stride = 0;
+  g.out_mode = out_mode; g.act = ACT_NONE; g.alpha = alpha;
+  Nf4Args f = {(const uint8_t*)packed, (const uint8_t*)qabsmax, absmax2, code2, offset, kw,
+               (const bf16_t*)lora_a, lda2, (const bf16_t*)lora_b, ldb2, r};
+  using G = Geo<128, 128, 2, 2>;
+  const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  const int lds = G::LDS + (16 + 256) * 4;
+  hipStream_t s = (hipStream_t)stream;
+  if (w_kmajor) hipLaunchKernelGGL(gemm_nf4_kernel<true>, dim3(tiles), dim3(256), lds, s, g, f);
+  else hipLaunchKernelGGL(gemm_nf4_kernel<false>, dim3(tiles), dim3(256), lds, s, g, f);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
 }

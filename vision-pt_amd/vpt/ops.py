@@ -32,7 +32,7 @@ class KernelProbe:
         self.records: list[tuple] = []
         self.active = False
 
-    def record(self, flops: float, fn):
+    def record(self, flops: float, fn, key=None):
         if not self.active:
             return fn()
         s = torch.cuda.Event(enable_timing=True)
@@ -40,16 +40,24 @@ class KernelProbe:
         s.record()
         r = fn()
         e.record()
-        self.records.append((s, e, flops))
+        self.records.append((s, e, flops, key))
         return r
 
     def summary(self):
         """(launches, mean ms per launch, mean algorithmic FLOPs per launch)."""
         if not self.records:
             return 0, 0.0, 0.0
-        ms = [s.elapsed_time(e) for s, e, _ in self.records]
-        fl = [f for _, _, f in self.records]
+        ms = [r[0].elapsed_time(r[1]) for r in self.records]
+        fl = [r[2] for r in self.records]
         return len(ms), sum(ms) / len(ms), sum(fl) / len(fl)
+
+    def by_key(self):
+        """{key: (launches, total ms, total algorithmic work)} over the keyed launches."""
+        out: dict = {}
+        for s, e, f, k in self.records:
+            n, t, w = out.get(k, (0, 0.0, 0.0))
+            out[k] = (n + 1, t + s.elapsed_time(e), w + f)
+        return out
 
 
 PROBES: dict[str, KernelProbe] = {}
@@ -105,7 +113,8 @@ def gemm(a, a_kmajor: bool, b, b_kmajor: bool, M: int, N: int, K: int, out, *, b
     if pr is None:
         run()
     else:
-        pr.record(2.0 * M * N * K, run)
+        pr.record(2.0 * M * N * K, run, key=f"{'fwd' if a_kmajor and b_kmajor else 'dgrad' if a_kmajor else 'wgrad'}"
+                  f" M{M} N{N} K{K} s{splits}")
     return out
 
 
@@ -150,7 +159,7 @@ def linear_swiglu(x, w12, b12, x12, h):
     if pr is None:
         run()
     else:
-        pr.record(2.0 * M * 2 * F * K, run)
+        pr.record(2.0 * M * 2 * F * K, run, key=f"swiglu_fwd M{M} N{2 * F} K{K}")
     return x12, h
 
 
@@ -171,7 +180,7 @@ def linear_dgrad_swiglu(dy, w3, x12, dx12, workspace=None):
     if pr is None:
         run()
     else:
-        pr.record(2.0 * M * F * D, run)
+        pr.record(2.0 * M * F * D, run, key=f"swiglu_dgrad M{M} N{F} K{D}")
     return dx12
 
 
@@ -497,6 +506,40 @@ def scale_bf16(a, s, out=None):
 def nf4_dequant(packed, qabsmax, absmax2, code2, offset, n, out):
     call("vpt_nf4_dequant", packed.data_ptr(), qabsmax.data_ptr(), absmax2.data_ptr(), code2.data_ptr(),
          offset.data_ptr(), n, out.data_ptr(), stream())
+    return out
+
+
+def gemm_nf4(a, w, forward: bool, out, *, lora_a=None, lora_b=None, bias=None, resid=None, out_mode=OUT_BF16,
+             alpha=1.0):
+    """NF4 dequant-in-GEMM (csrc/gemm.hip gemm_nf4_kernel). `w` is a vpt.sdxl.NF4Weight [N_w, K_w].
+    forward: out[M, N_w] = a[M, K_w] . Wd^T (+bias) (+ lora_a[M, r] . lora_b[N_w, r]^T)
+    dgrad:   out[M, K_w] = a[M, N_w] . Wd      (+ lora_a[M, r] . lora_b[r, K_w])"""
+    _chk(a, BF16, "a")
+    _chk(out, BF16 if out_mode == OUT_BF16 else F32, "out")
+    M = a.shape[0]
+    Nw, Kw = w.shape
+    N, K = (Nw, Kw) if forward else (Kw, Nw)
+    if a.shape[1] != K or out.shape[0] != M or out.shape[1] != N:
+        raise ValueError(f"gemm_nf4: a {tuple(a.shape)} / out {tuple(out.shape)} do not match W {w.shape}")
+    r = 0
+    if lora_a is not None:
+        _chk(lora_a, BF16, "lora_a")
+        _chk(lora_b, BF16, "lora_b")
+        r = lora_a.shape[1]
+        if tuple(lora_b.shape) != ((N, r) if forward else (r, N)):
+            raise ValueError("gemm_nf4: lora_b shape")
+
+    def run():
+        call("vpt_gemm_nf4", a.data_ptr(), a.stride(0), w.packed.data_ptr(), w.qabsmax.data_ptr(),
+             w.absmax2.data_ptr(), w.code2.data_ptr(), w.offset.data_ptr(), Kw, int(forward), _p(lora_a),
+             0 if lora_a is None else lora_a.stride(0), _p(lora_b), 0 if lora_b is None else lora_b.stride(0), r,
+             out.data_ptr(), out.stride(0), M, N, K, _p(bias), _p(resid), 0 if resid is None else resid.stride(0),
+             out_mode, float(alpha), stream())
+    pr = PROBES.get("gemm_nf4")
+    if pr is None:
+        run()
+    else:
+        pr.record(2.0 * M * N * (K + r), run, key=f"{'fwd' if forward else 'dgrad'} M{M} N{N} K{K}")
     return out
 
 

@@ -2,8 +2,8 @@
 
 a29  LoRALinearNF4: LoRALinear (src/modules/peft/lora.py:92-104) over a bitsandbytes NF4 Linear4bit
      (src/modules/quant/bnb.py:37-129): y = bf16(bf16(x W^T + b) + bf16(s * up(down(x)))), s = alpha/rank,
-     with W dequantised from the NF4 layout by `vpt_nf4_dequant` for the GEMM. Base weight frozen; the
-     adapters train (f32 gradients).
+     with W dequantised tile by tile inside the GEMM (`vpt_gemm_nf4`, no bf16 weight in HBM) and the LoRA
+     term fused into the same GEMM as an extra K tile. Base weight frozen; the adapters train (f32 grads).
 a30  SDXLTransformerBlock: TransformerBlock.forward (src/models/sdxl/denoiser.py:258-280) --
      LayerNorm -> self-attention -> LayerNorm -> cross-attention to the text context -> LayerNorm ->
      GeGLU feed-forward, residuals -- with its 10 Linear layers as LoRALinearNF4 (the QLoRA targets),
@@ -62,7 +62,15 @@ class NF4Weight:
 
 
 class LoRALinearNF4:
-    """a29. `down` [r, in], `up` [out, r] bf16 trainable (grads `g_down`, `g_up` f32); `base` NF4 [out, in]."""
+    """a29. `down` [r, in], `up` [out, r] bf16 trainable (grads `g_down`, `g_up` f32); `base` NF4 [out, in].
+
+    forward  ds = bf16(s * x . down^T)            (one skinny GEMM, s = alpha / rank folded into its epilogue)
+             y  = bf16(x . Wd^T + b + ds . up^T)  (vpt_gemm_nf4: NF4 dequantised per tile in LDS, LoRA term as
+                                                   one extra K tile -- no bf16 weight in HBM, no LoRA add pass)
+    backward g_up += dy^T . ds;  vs = bf16(s * dy . up);  g_down += vs^T . x;
+             dx = bf16(dy . Wd + vs . down)       (vpt_gemm_nf4 in the input-gradient direction)
+    The reference (lora.py:92-104) rounds lora_down, lora_up and their scaled sum to bf16 separately; here the
+    sum is taken in f32 before one rounding (within the bf16 parity tolerance of tests/test_sdxl_gpu.py)."""
 
     def __init__(self, base: NF4Weight, bias: torch.Tensor | None, down: torch.Tensor, up: torch.Tensor,
                  alpha: float, rank: int):
@@ -71,34 +79,45 @@ class LoRALinearNF4:
         self.scale = alpha / rank
         self.g_down = torch.zeros(self.down.shape, dtype=F32, device=self.down.device)
         self.g_up = torch.zeros(self.up.shape, dtype=F32, device=self.up.device)
-        self._w = None
         self._saved = None
+        # NF4 blocks (64 elements of the flat [out][in] weight) must not straddle rows for the per-tile
+        # dequant: true for every SDXL UNet Linear (in/out features are multiples of 64); other shapes take
+        # the dequant-to-scratch path below.
+        self.fused = base.shape[0] % 64 == 0 and base.shape[1] % 64 == 0
 
     def weight(self) -> torch.Tensor:
-        """The dequantised base weight (bf16, one scratch per layer; re-dequantised every forward)."""
-        if self._w is None:
-            self._w = torch.empty(self.base.shape, dtype=BF16, device=self.down.device)
-        return self.base.dequantize(self._w)
+        """The dequantised base weight (bf16) -- for tests and export only; the hot path never builds it."""
+        return self.base.dequantize(torch.empty(self.base.shape, dtype=BF16, device=self.down.device))
 
-    def forward(self, x: torch.Tensor, save: bool = True) -> torch.Tensor:
-        W = self.weight()
-        d = ops.linear(x, self.down)                                         # lora_down(x)        [M, r]
-        lo = torch.empty(x.shape[0], self.up.shape[0], dtype=BF16, device=x.device)
-        ops.gemm(d, True, self.up, True, x.shape[0], self.up.shape[0], self.up.shape[1], lo, alpha=self.scale)
-        y = ops.linear(x, W, bias=self.bias, resid=lo)                      # bf16(bf16(xW^T+b) + lora)
-        self._saved = (x, d) if save else None
+    def forward(self, x: torch.Tensor, save: bool = True, out: torch.Tensor | None = None) -> torch.Tensor:
+        M = x.shape[0]
+        r = self.down.shape[0]
+        ds = ops.gemm(x, True, self.down, True, M, r, x.shape[1],
+                      torch.empty(M, r, dtype=BF16, device=x.device), alpha=self.scale)
+        y = out if out is not None else torch.empty(M, self.base.shape[0], dtype=BF16, device=x.device)
+        if self.fused:
+            ops.gemm_nf4(x, self.base, True, y, lora_a=ds, lora_b=self.up, bias=self.bias)
+        else:
+            lo = ops.gemm(ds, True, self.up, True, M, self.up.shape[0], r,
+                          torch.empty(M, self.up.shape[0], dtype=BF16, device=x.device))
+            ops.linear(x, self.weight(), bias=self.bias, resid=lo, out=y)
+        self._saved = (x, ds) if save else None
         return y
 
     def backward(self, dy: torch.Tensor) -> torch.Tensor:
-        """Accumulates g_up, g_down; returns dx (bf16) = dy W + bf16(s dy) up down."""
-        x, d = self._saved
-        g = ops.scale_bf16(dy, self.scale)                                   # grad of (up_out * s)
-        ops.linear_wgrad(g, d, self.g_up, accumulate=True, splits=ops.wgrad_splits(*self.up.shape, x.shape[0]))
-        dd = ops.linear_dgrad(g, self.up)                                    # [M, r]
-        ops.linear_wgrad(dd, x, self.g_down, accumulate=True,
-                         splits=ops.wgrad_splits(*self.down.shape, x.shape[0]))
-        dx_lora = ops.linear_dgrad(dd, self.down)
-        return ops.linear_dgrad(dy, self.weight(), resid=dx_lora)
+        """Accumulates g_up, g_down; returns dx (bf16)."""
+        x, ds = self._saved
+        M = x.shape[0]
+        r = self.down.shape[0]
+        ops.linear_wgrad(dy, ds, self.g_up, accumulate=True, splits=ops.wgrad_splits(*self.up.shape, M))
+        vs = ops.gemm(dy, True, self.up, False, M, r, self.up.shape[0],
+                      torch.empty(M, r, dtype=BF16, device=dy.device), alpha=self.scale)
+        ops.linear_wgrad(vs, x, self.g_down, accumulate=True, splits=ops.wgrad_splits(*self.down.shape, M))
+        dx = torch.empty(M, self.base.shape[1], dtype=BF16, device=dy.device)
+        if self.fused:
+            return ops.gemm_nf4(dy, self.base, False, dx, lora_a=vs, lora_b=self.down)
+        dx_lora = ops.linear_dgrad(vs, self.down)
+        return ops.linear_dgrad(dy, self.weight(), resid=dx_lora, out=dx)
 
 
 TARGETS = ["attn1.to_q", "attn1.to_k", "attn1.to_v", "attn1.to_out.0", "attn2.to_q", "attn2.to_k", "attn2.to_v",
