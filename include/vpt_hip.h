@@ -210,6 +210,15 @@ int vpt_gemm_nf4(const void* A, long lda, const void* packed, const void* qabsma
                  const float* code2, const float* offset, long kw, int w_kmajor, const void* lora_a, long lda2,
                  const void* lora_b, long ldb2, int r, void* C, long ldc, int M, int N, int K, const void* bias,
                  const void* resid, long ldr, int out_mode, float alpha, void* stream);
+/* SpatialTransformer (src/models/sdxl/denoiser.py:283-365) around the transformer blocks:
+ * GroupNorm(G, C, eps) on NCHW bf16 [B][C][HW] (f32 statistics mean / rstd [B*G] saved for the backward;
+ * output NCHW bf16), its input gradient (affine weights frozen under QLoRA; dres: + a second NCHW gradient),
+ * and dst[b][s][r] = src[b][r][s] (+ add) -- the NCHW <-> token-major permutes, the residual add fused. */
+int vpt_groupnorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int B, int C,
+                      int G, long HW, float eps, void* stream);
+int vpt_groupnorm_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const void* w,
+                      const void* dres, void* dx, int B, int C, int G, long HW, void* stream);
+int vpt_transpose_add(const void* src, const void* add, void* dst, int B, int R, int S, void* stream);
 /* Elementwise bf16: out = a + b (residual sums), out = s * a (LoRA scale gradient); n % 8 == 0. */
 int vpt_add_bf16(const void* a, const void* b, long n, void* out, void* stream);
 int vpt_scale_bf16(const void* a, long n, float s, void* out, void* stream);

@@ -176,3 +176,50 @@ def block_forward(x, ctx, w, heads, rank, alpha, head_dim=64):
     hid, gate = lora_linear(h, w, "ff.net.0.proj", rank, alpha).chunk(2, dim=-1)     # GeGLU (:179-186)
     x = x + lora_linear(hid * F.gelu(gate), w, "ff.net.2", rank, alpha)
     return x
+
+
+# ---------------------------------------------------------------------------- SpatialTransformer
+def spatial_param_shapes(C: int, heads: int, depth: int, context_dim: int, rank: int, head_dim: int = 64):
+    """Reference state-dict names/shapes of a SpatialTransformer (src/models/sdxl/denoiser.py:283-365) whose
+    blocks' 10 Linear layers are LoRA-wrapped; norm = GroupNorm(32, C), proj_in / proj_out plain Linears."""
+    inner = heads * head_dim
+    shapes = {"norm.weight": (C,), "norm.bias": (C,), "proj_in.weight": (inner, C), "proj_in.bias": (inner,),
+              "proj_out.weight": (C, inner), "proj_out.bias": (C,)}
+    for i in range(depth):
+        for n, s in block_param_shapes(inner, heads, context_dim, rank, head_dim).items():
+            shapes[f"transformer_blocks.{i}.{n}"] = s
+    return shapes
+
+
+def make_spatial_weights(C, heads, depth, context_dim, rank, seed, head_dim=64):
+    g = torch.Generator().manual_seed(seed)
+    w = {}
+    for n, s in spatial_param_shapes(C, heads, depth, context_dim, rank, head_dim).items():
+        leaf = n.rsplit(".", 2)[-2] if n.count(".") >= 1 else n
+        if n == "norm.weight" or n.endswith(("norm1.weight", "norm2.weight", "norm3.weight")):
+            w[n] = 1.0 + 0.1 * torch.randn(s, generator=g)
+        elif n.endswith(".bias"):
+            w[n] = 0.05 * torch.randn(s, generator=g)
+        elif "lora_down" in n:
+            w[n] = torch.randn(s, generator=g) / math.sqrt(s[1])
+        elif "lora_up" in n:
+            w[n] = 0.05 * torch.randn(s, generator=g)
+        else:
+            w[n] = torch.randn(s, generator=g) / math.sqrt(s[1])
+        del leaf
+    return w
+
+
+def spatial_forward(x, ctx, w, heads, depth, rank, alpha, head_dim=64, groups=32):
+    """SpatialTransformer.forward (denoiser.py:331-365) in fp32: GroupNorm -> NCHW->tokens -> proj_in ->
+    blocks -> proj_out -> tokens->NCHW -> + residual."""
+    B, C, H, W = x.shape
+    h = F.group_norm(x, groups, w["norm.weight"], w["norm.bias"], eps=1e-6)
+    h = h.permute(0, 2, 3, 1).reshape(B, H * W, C)
+    h = F.linear(h, w["proj_in.weight"], w["proj_in.bias"])
+    for i in range(depth):
+        pre = f"transformer_blocks.{i}."
+        wb = {k[len(pre):]: v for k, v in w.items() if k.startswith(pre)}
+        h = block_forward(h, ctx, wb, heads, rank, alpha, head_dim)
+    h = F.linear(h, w["proj_out.weight"], w["proj_out.bias"])
+    return h.reshape(B, H, W, C).permute(0, 3, 1, 2) + x

@@ -21,6 +21,9 @@ Fixtures:
                          dim 128, 2 heads, context_dim 96, 2 x 80 tokens, 20 context tokens. Forward output
                          and gradients (input, context, every LoRA weight) of sum(out * dy), once in fp32
                          with fp32 attention and once in the reference's native bf16.
+  sdxl_spatial.safetensors  the reference SpatialTransformer (denoiser.py:283-365): GroupNorm(32, 128), NF4
+                         proj_in / proj_out, 2 LoRA-wrapped blocks, context 128, 2 x 8x8 latents, 20 context
+                         tokens; fp32 and native-bf16 forward / input, context and adapter grads of sum(out*dy).
   timestep.safetensors   sample_timestep for the scale_shift_sigmoid / sigmoid / uniform / shift_sigmoid /
                          flux_shift samplers (two latent shapes, two global-RNG seeds, non-default kwargs).
   init.safetensors       JiT.initialize_weights + ClassEncoder.initialize_weights on the micro config: per
@@ -262,6 +265,83 @@ def sdxl_block_fixture(meta):
                                                        B=B, n=n, nc=nc, weight_seed=11))))
 
 
+def sdxl_spatial_fixture(meta):
+    """Reference SpatialTransformer (src/models/sdxl/denoiser.py:283-365) with 2 LoRA-wrapped blocks; every
+    Linear base (proj_in / proj_out and the 20 block targets) NF4-quantised (oracle restatement) and
+    dequantised, GroupNorm(32, 128); fp32 (fp32 SDPA) and native bf16 runs of sum(out * dy)."""
+    import functools
+    from oracle import sdxl_oracle as SO
+
+    def load(name, path):
+        spec = importlib.util.spec_from_file_location(name, path)
+        m = importlib.util.module_from_spec(spec)
+        sys.modules[name] = m
+        spec.loader.exec_module(m)
+        return m
+
+    pkg = types.ModuleType("src.models.sdxl")
+    pkg.__path__ = [REF + "/src/models/sdxl"]
+    sys.modules["src.models.sdxl"] = pkg
+    load("src.models.sdxl.config", REF + "/src/models/sdxl/config.py")
+    den = load("src.models.sdxl.denoiser", REF + "/src/models/sdxl/denoiser.py")
+    lora = importlib.import_module("src.modules.peft.lora")
+    C, heads, depth, cdim, rank, alpha, B, H, W, nc = 128, 2, 2, 128, 16, 8.0, 2, 8, 8, 20
+    w = SO.make_spatial_weights(C, heads, depth, cdim, rank, seed=21)
+    nf4 = {}
+    for k in list(w):
+        if k.endswith(".linear.weight") or k in ("proj_in.weight", "proj_out.weight"):
+            st = SO.nf4_quantize(w[k])
+            nf4[k] = st
+            w[k] = SO.nf4_dequantize(st)
+    g = torch.Generator().manual_seed(22)
+    x = torch.randn(B, C, H, W, generator=g)
+    ctx = torch.randn(B, nc, cdim, generator=g)
+    dy = torch.randn(B, C, H, W, generator=g)
+    out = {"x": x, "ctx": ctx, "dy": dy}
+    for k, st in nf4.items():
+        for kk, v in st.items():
+            out[f"nf4/{k}/{kk}"] = v
+    orig_sdpa = den.scaled_dot_product_attention
+    for mode in ("fp32", "bf16"):
+        dt = torch.float32 if mode == "fp32" else torch.bfloat16
+        st_mod = den.SpatialTransformer(in_channels=C, num_heads=heads, head_dim=64, context_dims=[cdim] * depth)
+        for blk in st_mod.transformer_blocks:
+            for t in SO.LORA_TARGETS:
+                parent_path, last = t.rsplit(".", 1)
+                parent = blk.get_submodule(parent_path)
+                wrapped = lora.LoRALinear(lora.LoRAConfig(rank=rank, alpha=alpha, dtype="float32"),
+                                          parent.get_submodule(last))
+                setattr(parent, last, wrapped)
+        sd = st_mod.state_dict()
+        for k in list(sd):
+            if k.endswith(".alpha"):
+                continue
+            sd[k] = w[k].clone()
+        st_mod.load_state_dict(sd, strict=True)
+        st_mod = st_mod.to(dt)
+        if mode == "fp32":
+            den.scaled_dot_product_attention = functools.partial(orig_sdpa, attention_dtype=torch.float32)
+        try:
+            xi = x.detach().clone().to(dt).requires_grad_(True)
+            ci = ctx.detach().clone().to(dt).requires_grad_(True)
+            y = st_mod(xi, context=ci)
+            (y.float() * dy).sum().backward()
+        finally:
+            den.scaled_dot_product_attention = orig_sdpa
+        out[f"{mode}/out"] = y.detach().float()
+        out[f"{mode}/dx"] = xi.grad.float()
+        out[f"{mode}/dctx"] = ci.grad.float()
+        for nme, prm in st_mod.named_parameters():
+            if prm.grad is not None and "lora_" in nme:
+                out[f"{mode}/grad/{nme}"] = prm.grad.float()
+    # the restated forward reproduces the reference's fp32 output (oracle self-check, recorded)
+    ref = SO.spatial_forward(x, ctx, w, heads, depth, rank, alpha)
+    out["oracle/out"] = ref.detach().float()
+    save_file({k: v.contiguous() for k, v in out.items()}, os.path.join(HERE, "sdxl_spatial.safetensors"),
+              metadata=dict(meta, dims=json.dumps(dict(C=C, heads=heads, depth=depth, context_dim=cdim, rank=rank,
+                                                       alpha=alpha, B=B, H=H, W=W, nc=nc, weight_seed=21))))
+
+
 def timestep_fixture(meta):
     """sample_timestep (src/modules/timestep/sampling.py:170-187) for every sampler type the JiT / SDXL
     flow-match steps select, drawn from the global RNG after torch.manual_seed(seed) on CPU."""
@@ -308,6 +388,10 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "sampler":
         sampler_fixture(R, meta)
         print("sampler", os.path.getsize(os.path.join(HERE, "sampler.safetensors")))
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "sdxl_spatial":
+        sdxl_spatial_fixture(meta)
+        print("sdxl_spatial", os.path.getsize(os.path.join(HERE, "sdxl_spatial.safetensors")))
         return
     if len(sys.argv) > 1 and sys.argv[1] == "init":
         init_fixture(R, meta)
@@ -402,7 +486,8 @@ def main():
     sdxl_block_fixture(meta)
     timestep_fixture(meta)
     init_fixture(R, meta)
-    for f in ("jit_micro", "jit_c1", "ops", "sampler", "sdxl_block", "timestep", "init"):
+    sdxl_spatial_fixture(meta)
+    for f in ("jit_micro", "jit_c1", "ops", "sampler", "sdxl_block", "timestep", "init", "sdxl_spatial"):
         print(f, os.path.getsize(os.path.join(HERE, f + ".safetensors")))
 
 

@@ -236,3 +236,63 @@ def test_sdxl_block_matches_reference_bf16():
         if abs(g.norm() - v.norm()) > 0.05 * v.norm() or cos(g, v) < 0.99:
             bad.append((name, g.norm().item(), v.norm().item(), cos(g, v)))
     assert not bad, bad
+
+
+def test_sdxl_spatial_transformer_matches_reference_bf16():
+    """SpatialTransformer (denoiser.py:283-365): GroupNorm, NF4 proj_in / proj_out, 2 LoRA blocks, residual,
+    forward + backward vs the reference's own native-bf16 run (tests/golden/sdxl_spatial.safetensors).
+    Bars: output rel-L2 <= 2e-2, input / context grads <= 3e-2, adapter grads norm within 5 %, cos >= 0.99."""
+    from vpt.sdxl import SDXLSpatialTransformer
+    path = os.path.join(os.path.dirname(__file__), "golden", "sdxl_spatial.safetensors")
+    with safe_open(path, "pt") as f:
+        d = json.loads(f.metadata()["dims"])
+    fx = load_file(path)
+    C, heads, depth, cdim, rank, alpha = d["C"], d["heads"], d["depth"], d["context_dim"], d["rank"], d["alpha"]
+    B, H, W, nc = d["B"], d["H"], d["W"], d["nc"]
+    sd = SO.make_spatial_weights(C, heads, depth, cdim, rank, seed=d["weight_seed"])
+    for k in list(sd):
+        if k.endswith(".linear.weight") or k in ("proj_in.weight", "proj_out.weight"):
+            sd[k] = {kk.split("/")[-1]: v for kk, v in fx.items() if kk.startswith(f"nf4/{k}/")}
+    st = SDXLSpatialTransformer(C, heads, depth, cdim, rank, alpha, sd)
+    HW = H * W
+    x = fx["x"].to(DEV).bfloat16().reshape(B, C, HW).contiguous()
+    c = fx["ctx"].to(DEV).bfloat16().reshape(B * nc, cdim).contiguous()
+    y = st.forward(x, c, B, HW, nc)
+    dx, dctx = st.backward(fx["dy"].to(DEV).bfloat16().reshape(B, C, HW).contiguous())
+    torch.cuda.synchronize()
+    assert rel(y, fx["bf16/out"].reshape(B, C, HW)) < 2e-2
+    assert rel(y, fx["fp32/out"].reshape(B, C, HW)) < 2e-2
+    assert rel(dx, fx["bf16/dx"].reshape(B, C, HW)) < 3e-2
+    assert rel(dctx, fx["bf16/dctx"].reshape(B * nc, cdim)) < 3e-2
+    grads = st.lora_grads()
+    bad = []
+    for k, v in fx.items():
+        if not k.startswith("bf16/grad/"):
+            continue
+        name = k[len("bf16/grad/"):]
+        g = grads[name].cpu()
+        if abs(g.norm() - v.norm()) > 0.05 * v.norm() or cos(g, v) < 0.99:
+            bad.append((name, g.norm().item(), v.norm().item(), cos(g, v)))
+    assert not bad and len(grads) == 2 * 10 * depth, bad
+
+
+@pytest.mark.parametrize("B,C,HW", [(2, 640, 4096), (3, 1280, 1024)])
+def test_groupnorm_and_transpose(ops, B, C, HW):
+    """GroupNorm(32, C, eps 1e-6) fwd / input-grad (frozen affine) vs torch fp32, and the NCHW<->token
+    transposes (bit-exact) with the residual add, at SDXL's two stage shapes."""
+    G = 32
+    x = rnd(B, C, HW, seed=30)
+    w = (1 + rnd(C, scale=0.1, seed=31).float()).bfloat16()
+    b = rnd(C, scale=0.1, seed=32)
+    y, mean, rstd = ops.groupnorm_fwd(x, w, b, B, C, G, HW)
+    xf = x.float().requires_grad_(True)
+    ref = torch.nn.functional.group_norm(xf, G, w.float(), b.float(), eps=1e-6)
+    assert rel(y, ref) < 5e-3
+    dy, dres = rnd(B, C, HW, seed=33), rnd(B, C, HW, seed=34)
+    dx = ops.groupnorm_bwd(dy, x, mean, rstd, w, B, C, G, HW, dres=dres)
+    ref.backward(dy.float())
+    assert rel(dx.float() - dres.float(), xf.grad) < 1e-2
+    t = ops.transpose_add(x, B, C, HW)
+    assert torch.equal(t, x.transpose(1, 2).contiguous())
+    back = ops.transpose_add(t, B, HW, C, add=dres)
+    assert torch.equal(back, (x.float() + dres.float()).bfloat16())

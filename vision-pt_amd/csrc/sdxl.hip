@@ -279,6 +279,132 @@ __global__ __launch_bounds__(256) void nf4_nested_kernel(const float* __restrict
   }
 }
 
+// ---------------------------------------------------------------- SpatialTransformer (denoiser.py:283-365)
+// GroupNorm(32, C, eps 1e-6, affine) on the NCHW stage activation: one workgroup per (batch, group) -- a group
+// is cpg * HW contiguous elements. f32 statistics (two passes: mean, then centred variance), output
+// bf16((x - mean) * rstd * w[c] + b[c]) in NCHW; the transpose to tokens is transpose_add_kernel.
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+  v = wave_sum(v);
+  const int wid = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[wid] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void groupnorm_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                            const bf16_t* __restrict__ bias, bf16_t* __restrict__ y,
+                                                            float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                            int C, int G, long HW, float eps) {
+  __shared__ float red[4];
+  const int bg = blockIdx.x, g = bg % G, cpg = C / G;
+  const long n = (long)cpg * HW;
+  const long base = (long)bg * n;  // (b * C + g * cpg) * HW
+  const int tid = threadIdx.x;
+  float s = 0.f;
+  for (long i = tid * 8L; i < n; i += 256 * 8) {
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + base + i), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += v[e];
+  }
+  const float mean = block_sum256(s, red) / (float)n;
+  float q = 0.f;
+  for (long i = tid * 8L; i < n; i += 256 * 8) {
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + base + i), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q += (v[e] - mean) * (v[e] - mean);
+  }
+  const float rstd = rsqrtf(block_sum256(q, red) / (float)n + eps);
+  if (tid == 0) { mean_out[bg] = mean; rstd_out[bg] = rstd; }
+  for (long i = tid * 8L; i < n; i += 256 * 8) {
+    const int c = g * cpg + (int)(i / HW);  // HW % 8 == 0: the 8 elements share a channel
+    const float wc = bf2f(w[c]) * rstd, bc = bf2f(bias[c]);
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + base + i), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (v[e] - mean) * wc + bc;
+    *reinterpret_cast<uint4*>(y + base + i) = pack8(v);
+  }
+}
+
+// dx = rstd * (g - (sum g + xh * sum g xh) / n) (+ dres), g = w[c] * dy, xh = (x - mean) * rstd, per group;
+// NCHW in and out (the affine weights are frozen under QLoRA: no dw / db).
+__global__ __launch_bounds__(256) void groupnorm_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                            const float* __restrict__ mean_in,
+                                                            const float* __restrict__ rstd_in,
+                                                            const bf16_t* __restrict__ w, const bf16_t* __restrict__ dres,
+                                                            bf16_t* __restrict__ dx, int C, int G, long HW) {
+  __shared__ float red[4];
+  const int bg = blockIdx.x, g = bg % G, cpg = C / G;
+  const long n = (long)cpg * HW;
+  const long base = (long)bg * n;
+  const int tid = threadIdx.x;
+  const float mean = mean_in[bg], rstd = rstd_in[bg];
+  float sg = 0.f, sgx = 0.f;
+  for (long i = tid * 8L; i < n; i += 256 * 8) {
+    const float wc = bf2f(w[g * cpg + (int)(i / HW)]);
+    float d[8], v[8];
+    unpack8(*reinterpret_cast<const uint4*>(dy + base + i), d);
+    unpack8(*reinterpret_cast<const uint4*>(x + base + i), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float gg = wc * d[e];
+      sg += gg;
+      sgx += gg * (v[e] - mean) * rstd;
+    }
+  }
+  const float mg = block_sum256(sg, red) / (float)n;
+  const float mgx = block_sum256(sgx, red) / (float)n;
+  for (long i = tid * 8L; i < n; i += 256 * 8) {
+    const float wc = bf2f(w[g * cpg + (int)(i / HW)]);
+    float d[8], v[8], r[8];
+    unpack8(*reinterpret_cast<const uint4*>(dy + base + i), d);
+    unpack8(*reinterpret_cast<const uint4*>(x + base + i), v);
+    if (dres) unpack8(*reinterpret_cast<const uint4*>(dres + base + i), r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float xh = (v[e] - mean) * rstd;
+      v[e] = rstd * (wc * d[e] - mg - xh * mgx) + (dres ? r[e] : 0.f);
+    }
+    *reinterpret_cast<uint4*>(dx + base + i) = pack8(v);
+  }
+}
+
+// dst[b][s][r] = src[b][r][s] (+ add[b][s][r]), bf16, 64 x 64 tiles through LDS: the NCHW <-> token-major
+// permutes of SpatialTransformer.forward (denoiser.py:339-345, 356-363), the residual add fused.
+__global__ __launch_bounds__(256) void transpose_add_kernel(const bf16_t* __restrict__ src, const bf16_t* __restrict__ add,
+                                                            bf16_t* __restrict__ dst, int R, int S) {
+  __shared__ float t[64][65];
+  const int b = blockIdx.z, r0 = blockIdx.y * 64, s0 = blockIdx.x * 64, tid = threadIdx.x;
+  const bf16_t* sb = src + (long)b * R * S;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {  // 64 rows x 8 chunks of 8
+    const int idx = tid + 256 * k, rr = idx >> 3, ch = idx & 7;
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(sb + (long)(r0 + rr) * S + s0 + ch * 8), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t[rr][ch * 8 + e] = v[e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = tid + 256 * k, ss = idx >> 3, ch = idx & 7;
+    const long o = (long)b * R * S + (long)(s0 + ss) * R + r0 + ch * 8;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = t[ch * 8 + e][ss];
+    if (add) {
+      float a[8];
+      unpack8(*reinterpret_cast<const uint4*>(add + o), a);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = bf2f(f2bf(v[e])) + a[e];  // bf16 tensor + bf16 residual
+    }
+    *reinterpret_cast<uint4*>(dst + o) = pack8(v);
+  }
+}
+
 inline dim3 grid1(long n, int threads = 256) { return dim3((unsigned)((n + threads - 1) / threads)); }
 
 }  // namespace
@@ -351,6 +477,35 @@ extern "C" int vpt_nf4_quantize(const void* w, long n, const float* code2, void*
   VPT_LAUNCH_CHECK();
   hipLaunchKernelGGL(nf4_nested_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, absmax_scratch, nb, code2,
                      (uint8_t*)qabsmax, absmax2, offset);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_groupnorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int B,
+                                 int C, int G, long HW, float eps, void* stream) {
+  VPT_CHECK_ARG(x && w && b && y && mean && rstd, "vpt_groupnorm_fwd: null pointer");
+  VPT_CHECK_ARG(B > 0 && G > 0 && C % G == 0 && HW % 8 == 0, "vpt_groupnorm_fwd: C % G == 0, HW % 8 == 0");
+  hipLaunchKernelGGL(groupnorm_fwd_kernel, dim3(B * G), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                     (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y, mean, rstd, C, G, HW, eps);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_groupnorm_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const void* w,
+                                 const void* dres, void* dx, int B, int C, int G, long HW, void* stream) {
+  VPT_CHECK_ARG(dy && x && mean && rstd && w && dx, "vpt_groupnorm_bwd: null pointer");
+  VPT_CHECK_ARG(B > 0 && G > 0 && C % G == 0 && HW % 8 == 0, "vpt_groupnorm_bwd: C % G == 0, HW % 8 == 0");
+  hipLaunchKernelGGL(groupnorm_bwd_kernel, dim3(B * G), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+                     (const bf16_t*)x, mean, rstd, (const bf16_t*)w, (const bf16_t*)dres, (bf16_t*)dx, C, G, HW);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_transpose_add(const void* src, const void* add, void* dst, int B, int R, int S, void* stream) {
+  VPT_CHECK_ARG(src && dst && src != dst, "vpt_transpose_add: null or aliased pointer");
+  VPT_CHECK_ARG(B > 0 && R % 64 == 0 && S % 64 == 0, "vpt_transpose_add: R, S multiples of 64");
+  hipLaunchKernelGGL(transpose_add_kernel, dim3(S / 64, R / 64, B), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)src, (const bf16_t*)add, (bf16_t*)dst, R, S);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

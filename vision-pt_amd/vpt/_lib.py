@@ -66,6 +66,9 @@ SIGNATURES: dict[str, list] = {
     "vpt_geglu_fwd": [P, L, I, L, P, P],
     "vpt_geglu_bwd": [P, P, L, I, L, P, L, P],
     "vpt_nf4_dequant": [P, P, P, P, P, L, P, P],
+    "vpt_groupnorm_fwd": [P, P, P, P, P, P, I, I, I, L, F, P],
+    "vpt_groupnorm_bwd": [P, P, P, P, P, P, P, I, I, I, L, P],
+    "vpt_transpose_add": [P, P, P, I, I, I, P],
     "vpt_gemm_nf4": [P, L, P, P, P, P, P, L, I, P, L, P, L, I, P, L, I, I, I, P, P, L, I, F, P],
     "vpt_nf4_quantize": [P, L, P, P, P, P, P, P, P],
     "vpt_add_bf16": [P, P, L, P, P],

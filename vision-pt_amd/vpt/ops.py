@@ -491,6 +491,30 @@ def geglu_bwd(dy, x12, dx12=None):
     return dx12
 
 
+def groupnorm_fwd(x, w, b, B, C, G, HW, out=None, mean=None, rstd=None, eps=1e-6):
+    """x NCHW bf16 [B, C, HW] -> GroupNorm(G, C) output NCHW bf16; mean / rstd [B*G] f32 (for the backward)."""
+    out = torch.empty_like(x) if out is None else out
+    mean = torch.empty(B * G, dtype=F32, device=x.device) if mean is None else mean
+    rstd = torch.empty(B * G, dtype=F32, device=x.device) if rstd is None else rstd
+    call("vpt_groupnorm_fwd", x.data_ptr(), w.data_ptr(), b.data_ptr(), out.data_ptr(), mean.data_ptr(),
+         rstd.data_ptr(), B, C, G, HW, eps, stream())
+    return out, mean, rstd
+
+
+def groupnorm_bwd(dy, x, mean, rstd, w, B, C, G, HW, dres=None, dx=None):
+    dx = torch.empty_like(x) if dx is None else dx
+    call("vpt_groupnorm_bwd", dy.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(), w.data_ptr(), _p(dres),
+         dx.data_ptr(), B, C, G, HW, stream())
+    return dx
+
+
+def transpose_add(src, B, R, S, add=None, out=None):
+    """out[b][s][r] = src[b][r][s] (+ add[b][s][r]) for bf16 src [B, R, S] (R, S multiples of 64)."""
+    out = torch.empty(B, S, R, dtype=BF16, device=src.device) if out is None else out
+    call("vpt_transpose_add", src.data_ptr(), _p(add), out.data_ptr(), B, R, S, stream())
+    return out
+
+
 def add_bf16(a, b, out=None):
     out = torch.empty_like(a) if out is None else out
     call("vpt_add_bf16", a.data_ptr(), b.data_ptr(), a.numel(), out.data_ptr(), stream())

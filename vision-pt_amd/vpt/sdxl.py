@@ -89,18 +89,22 @@ class LoRALinearNF4:
         """The dequantised base weight (bf16) -- for tests and export only; the hot path never builds it."""
         return self.base.dequantize(torch.empty(self.base.shape, dtype=BF16, device=self.down.device))
 
-    def forward(self, x: torch.Tensor, save: bool = True, out: torch.Tensor | None = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, save: bool = True, out: torch.Tensor | None = None,
+                resid: torch.Tensor | None = None) -> torch.Tensor:
+        """resid: a bf16 tensor added in the epilogue (the block's residual stream: bf16(resid + bf16(y)))."""
         M = x.shape[0]
         r = self.down.shape[0]
         ds = ops.gemm(x, True, self.down, True, M, r, x.shape[1],
                       torch.empty(M, r, dtype=BF16, device=x.device), alpha=self.scale)
         y = out if out is not None else torch.empty(M, self.base.shape[0], dtype=BF16, device=x.device)
         if self.fused:
-            ops.gemm_nf4(x, self.base, True, y, lora_a=ds, lora_b=self.up, bias=self.bias)
+            ops.gemm_nf4(x, self.base, True, y, lora_a=ds, lora_b=self.up, bias=self.bias, resid=resid)
         else:
             lo = ops.gemm(ds, True, self.up, True, M, self.up.shape[0], r,
                           torch.empty(M, self.up.shape[0], dtype=BF16, device=x.device))
             ops.linear(x, self.weight(), bias=self.bias, resid=lo, out=y)
+            if resid is not None:
+                y = ops.add_bf16(resid, y)
         self._saved = (x, ds) if save else None
         return y
 
@@ -138,13 +142,7 @@ class SDXLTransformerBlock:
         self.device = device
         self.lin = {}
         for t in TARGETS:
-            wt = sd[f"{t}.linear.weight"]
-            if isinstance(wt, dict):
-                base = NF4Weight.from_state(wt, device)
-            else:
-                if code2 is None:
-                    raise ValueError("dense base weights need the dynamic map `code2` to quantise")
-                base = NF4Weight.quantize(wt.to(device), code2)
+            base = _nf4_or_dense(sd[f"{t}.linear.weight"], code2, device)
             b = sd.get(f"{t}.linear.bias")
             self.lin[t] = LoRALinearNF4(base, None if b is None else b.to(device, BF16).contiguous(),
                                         sd[f"{t}.lora_down.weight"].to(device), sd[f"{t}.lora_up.weight"].to(device),
@@ -185,17 +183,17 @@ class SDXLTransformerBlock:
         q, k, v = (L[f"attn1.to_{c}"].forward(h1, save) for c in "qkv")
         q = self._qs(q)
         o1, lse1 = self._attn_fwd(q, k, v, B, n, n)
-        x1 = ops.add_bf16(x, L["attn1.to_out.0"].forward(o1, save))
+        x1 = L["attn1.to_out.0"].forward(o1, save, resid=x)
         h2, m2, r2 = ops.layernorm_fwd(x1, *self.norm["norm2"])
         q2 = self._qs(L["attn2.to_q"].forward(h2, save))
         k2 = L["attn2.to_k"].forward(ctx, save)
         v2 = L["attn2.to_v"].forward(ctx, save)
         o2, lse2 = self._attn_fwd(q2, k2, v2, B, n, nc)
-        x2 = ops.add_bf16(x1, L["attn2.to_out.0"].forward(o2, save))
+        x2 = L["attn2.to_out.0"].forward(o2, save, resid=x1)
         h3, m3, r3 = ops.layernorm_fwd(x2, *self.norm["norm3"])
         x12 = L["ff.net.0.proj"].forward(h3, save)
         gg = ops.geglu_fwd(x12)
-        y = ops.add_bf16(x2, L["ff.net.2"].forward(gg, save))
+        y = L["ff.net.2"].forward(gg, save, resid=x2)
         self._st = dict(B=B, n=n, nc=nc, x=x, x1=x1, x2=x2, m=(m1, m2, m3), r=(r1, r2, r3), q=q, k=k, v=v, o1=o1,
                         lse1=lse1, q2=q2, k2=k2, v2=v2, o2=o2, lse2=lse2, x12=x12) if save else None
         return y
@@ -227,4 +225,93 @@ class SDXLTransformerBlock:
         for t, l in self.lin.items():
             out[f"{t}.lora_down.weight"] = l.g_down
             out[f"{t}.lora_up.weight"] = l.g_up
+        return out
+
+
+class NF4Linear:
+    """A frozen NF4 Linear without adapters (SpatialTransformer proj_in / proj_out): vpt_gemm_nf4 both ways."""
+
+    def __init__(self, base: NF4Weight, bias: torch.Tensor | None):
+        self.base, self.bias = base, bias
+        if base.shape[0] % 64 or base.shape[1] % 64:
+            raise NotImplementedError("NF4Linear: in / out features must be multiples of 64")
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        y = torch.empty(x.shape[0], self.base.shape[0], dtype=BF16, device=x.device)
+        return ops.gemm_nf4(x, self.base, True, y, bias=self.bias)
+
+    def backward(self, dy: torch.Tensor) -> torch.Tensor:
+        dx = torch.empty(dy.shape[0], self.base.shape[1], dtype=BF16, device=dy.device)
+        return ops.gemm_nf4(dy, self.base, False, dx)
+
+
+def _nf4_or_dense(wt, code2, device):
+    if isinstance(wt, dict):
+        return NF4Weight.from_state(wt, device)
+    if code2 is None:
+        raise ValueError("dense base weights need the dynamic map `code2` to quantise")
+    return NF4Weight.quantize(wt.to(device), code2)
+
+
+class SDXLSpatialTransformer:
+    """SpatialTransformer.forward (src/models/sdxl/denoiser.py:283-365) on the HIP kernels, QLoRA-trained:
+    GroupNorm(32, C, eps 1e-6) on the NCHW stage activation (vpt_groupnorm_fwd) -> NCHW->tokens
+    (vpt_transpose_add) -> proj_in (NF4) -> `depth` SDXLTransformerBlocks (LoRA on their 10 Linears) ->
+    proj_out (NF4) -> tokens->NCHW + residual (vpt_transpose_add with the add fused). The backward returns the
+    input and context gradients and accumulates every adapter's gradient (GroupNorm / proj weights frozen).
+    State-dict names are the reference's (`norm.*`, `proj_in.*`, `transformer_blocks.{i}.<target>.linear.*`,
+    `.lora_down.weight`, `.lora_up.weight`, `norm{1,2,3}.*`, `proj_out.*`)."""
+
+    def __init__(self, C: int, heads: int, depth: int, context_dim: int, rank: int, alpha: float, sd: dict,
+                 code2=None, device="cuda", groups: int = 32):
+        self.C, self.heads, self.depth, self.groups = C, heads, depth, groups
+        self.inner = heads * 64
+        self.device = device
+        self.norm_w = sd["norm.weight"].to(device, BF16).contiguous()
+        self.norm_b = sd["norm.bias"].to(device, BF16).contiguous()
+        self.proj_in = NF4Linear(_nf4_or_dense(sd["proj_in.weight"], code2, device),
+                                 sd["proj_in.bias"].to(device, BF16).contiguous())
+        self.proj_out = NF4Linear(_nf4_or_dense(sd["proj_out.weight"], code2, device),
+                                  sd["proj_out.bias"].to(device, BF16).contiguous())
+        self.blocks = []
+        for i in range(depth):
+            pre = f"transformer_blocks.{i}."
+            self.blocks.append(SDXLTransformerBlock(self.inner, heads, context_dim, rank, alpha,
+                                                    {k[len(pre):]: v for k, v in sd.items() if k.startswith(pre)},
+                                                    code2=code2, device=device))
+        self._st = None
+
+    def forward(self, x: torch.Tensor, ctx: torch.Tensor, B: int, HW: int, nc: int, save: bool = True) -> torch.Tensor:
+        """x NCHW bf16 [B, C, HW] (contiguous), ctx [B*nc, context_dim] -> NCHW bf16 [B, C, HW]."""
+        C, G = self.C, self.groups
+        h, mean, rstd = ops.groupnorm_fwd(x, self.norm_w, self.norm_b, B, C, G, HW)
+        tok = ops.transpose_add(h, B, C, HW)                                  # [B, HW, C]
+        t = self.proj_in.forward(tok.view(B * HW, C))
+        for blk in self.blocks:
+            t = blk.forward(t, ctx, B, HW, nc, save)
+        u = self.proj_out.forward(t)
+        y = ops.transpose_add(u.view(B, HW, C), B, HW, C, add=x)              # [B, C, HW] + residual
+        self._st = dict(B=B, HW=HW, x=x, mean=mean, rstd=rstd) if save else None
+        return y
+
+    def backward(self, dy: torch.Tensor):
+        """dy NCHW [B, C, HW] -> (dx NCHW, dctx [B*nc, context_dim])."""
+        st = self._st
+        B, HW, C, G = st["B"], st["HW"], self.C, self.groups
+        du = ops.transpose_add(dy, B, C, HW)                                  # tokens [B, HW, C]
+        dt = self.proj_out.backward(du.view(B * HW, C))
+        dctx = None
+        for blk in reversed(self.blocks):
+            dt, dc = blk.backward(dt)
+            dctx = dc if dctx is None else ops.add_bf16(dctx, dc)
+        dtok = self.proj_in.backward(dt)
+        dh = ops.transpose_add(dtok.view(B, HW, C), B, HW, C)                 # NCHW
+        dx = ops.groupnorm_bwd(dh, st["x"], st["mean"], st["rstd"], self.norm_w, B, C, G, HW, dres=dy)
+        return dx, dctx
+
+    def lora_grads(self) -> dict[str, torch.Tensor]:
+        out = {}
+        for i, blk in enumerate(self.blocks):
+            for k, v in blk.lora_grads().items():
+                out[f"transformer_blocks.{i}.{k}"] = v
         return out
