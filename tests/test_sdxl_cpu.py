@@ -81,3 +81,11 @@ def test_nf4_format_properties():
     err = (deq - w).reshape(-1, 64).abs()
     assert torch.all(err <= am * (gap / 2 + 0.02))
     assert rel(deq, w) < 0.12
+
+
+def test_product_dynamic_map_equals_oracle():
+    """vpt.sdxl.dynamic_map (load-time quantisation, product side) == the oracle's restatement."""
+    import torch
+    from oracle import sdxl_oracle as SO
+    from vpt.sdxl import dynamic_map
+    assert torch.equal(dynamic_map(), SO.dynamic_map())

@@ -296,3 +296,27 @@ def test_groupnorm_and_transpose(ops, B, C, HW):
     assert torch.equal(t, x.transpose(1, 2).contiguous())
     back = ops.transpose_add(t, B, HW, C, add=dres)
     assert torch.equal(back, (x.float() + dres.float()).bfloat16())
+
+
+def test_sdxl_stacks_step_binds_flat_adapters(ops):
+    """C5 step plumbing (vpt.sdxl_train): two reduced stacks (640 / 1280 channels, one block, 16x16 and 8x8
+    latents); the flat gradient buffer is exactly the stacks' adapter gradients, up-projection grads are
+    non-zero and down-projection grads are exactly zero at LoRA's zero-initialised up (lora.py:71-84), the
+    context gradient is finite, and the fused optimizer runs."""
+    from vpt.sdxl_train import SDXLStacksQLoRA
+    m = SDXLStacksQLoRA(B=2, stacks=[("a", 640, 10, 1, 16), ("b", 1280, 20, 1, 8)], n_ctx=77, seed=3)
+    xs, ctx, gs = m.make_inputs(seed=4)
+    dctx = m.step(xs, ctx, gs)
+    torch.cuda.synchronize()
+    assert torch.isfinite(dctx.float()).all() and dctx.float().abs().sum() > 0
+    seen = 0
+    for (_, _, _, st) in m.stacks:
+        for k, g in st.lora_grads().items():
+            assert g.data_ptr() >= m.grads.data_ptr() and g.numel() > 0
+            seen += g.numel()
+            if "lora_down" in k:
+                assert g.abs().max().item() == 0.0, k
+            else:
+                assert g.abs().max().item() > 0, k
+    assert seen == m.grads.numel() == m.n_adapter_params()
+    assert m.flops_per_step() > 0

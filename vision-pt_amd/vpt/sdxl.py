@@ -22,6 +22,31 @@ F32 = torch.float32
 U8 = torch.uint8
 
 
+def dynamic_map(signed: bool = True, max_exponent_bits: int = 7, total_bits: int = 8) -> torch.Tensor:
+    """bitsandbytes functional.create_dynamic_map (0.48.2): the 256-value signed map the nested absmax
+    statistics are quantised over (quantize_4bit(..., compress_statistics=True)); sorted, in [-1, 1]."""
+    data = []
+    non_sign = total_bits - 1
+    extra = 2 ** (non_sign - max_exponent_bits) - 1
+    for i in range(max_exponent_bits):
+        n = int(2 ** (i + non_sign - max_exponent_bits) + 1 if signed else 2 ** (i + non_sign - max_exponent_bits + 1) + 1)
+        bnd = torch.linspace(0.1, 1, n, dtype=torch.float32)
+        mid = (bnd[:-1] + bnd[1:]) / 2.0
+        data += ((10 ** (-(max_exponent_bits - 1) + i)) * mid).tolist()
+        if signed:
+            data += (-(10 ** (-(max_exponent_bits - 1) + i)) * mid).tolist()
+    if extra > 0:
+        bnd = torch.linspace(0.1, 1, extra + 1, dtype=torch.float32)
+        mid = (bnd[:-1] + bnd[1:]) / 2.0
+        data += ((10 ** (-(max_exponent_bits - 1) + i)) * mid).tolist()
+        if signed:
+            data += (-(10 ** (-(max_exponent_bits - 1) + i)) * mid).tolist()
+    data += [0, 1.0]
+    data += [0] * (2 ** total_bits - len(data))
+    data.sort()
+    return torch.tensor(data, dtype=torch.float32)
+
+
 class NF4Weight:
     """Device-resident NF4 tensor in the bitsandbytes layout (see include/vpt_hip.h)."""
 

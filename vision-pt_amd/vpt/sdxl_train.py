@@ -1,0 +1,167 @@
+"""SDXL QLoRA step over the UNet's transformer stacks (BASELINE config 5).
+
+The reference step is SDXLForFlowMatchingTraining.train_step (train/sdxl/flow_match.py:112-176) with the
+config of configs/sdxl/flow_match/config.yml: NF4 (bitsandbytes) base weights, LoRA rank 16 / alpha 1.0 on
+every `attn1`, `attn2` and `.ff.` Linear of the UNet's transformer blocks, batch 4, RAdamScheduleFree.
+Its transformer part -- the 11 SpatialTransformers of the SDXL UNet (src/models/sdxl/denoiser.py:283-365,
+placed by DownBlocks / MidBlock / UpBlocks :640-720, :800-815, :925-940) with their 70 TransformerBlocks,
+700 LoRA targets -- is what this module runs, at the 1024^2 stage shapes (latent 128x128):
+
+  stage        channels  heads  blocks/stack  tokens  stacks
+  down 64x64      640      10        2         4096     2
+  down 32x32     1280      20       10         1024     2
+  mid  32x32     1280      20       10         1024     1
+  up   32x32     1280      20       10         1024     3
+  up   64x64      640      10        2         4096     3
+
+with the text context of 3 x 77 = 231 tokens of width 2048 (CLIP-L | CLIP-G). Everything inside the stacks
+runs on the HIP kernels (GroupNorm, NF4 dequant-in-GEMM with the LoRA term fused, LayerNorm, flash
+attention self / cross, GeGLU, transposes, residuals in GEMM epilogues), the adapters' gradients land in one
+flat f32 buffer and one fused RAdamScheduleFree launch steps them.
+
+Not executed (outside SURVEY §8's rows): the UNet's ResNet / conv / up- and down-sampling path, the VAE
+encoder and the text encoders. The stacks take synthetic stage activations as input and the step's loss is
+sum_s <out_s, g_s> with fixed synthetic g_s (the gradient the UNet's remaining graph would hand back), so
+every stack runs its full forward and backward (input, context and adapter gradients).
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import ops
+from .optim import RAdamScheduleFreeFlat
+from .sdxl import TARGETS, SDXLSpatialTransformer, dynamic_map
+
+BF16, F32 = torch.bfloat16, torch.float32
+
+# (name, channels, heads, blocks per stack, latent side) at 1024^2 (latent 128x128)
+SDXL_1024_STACKS = [("down.64.0", 640, 10, 2, 64), ("down.64.1", 640, 10, 2, 64),
+                    ("down.32.0", 1280, 20, 10, 32), ("down.32.1", 1280, 20, 10, 32),
+                    ("mid.32", 1280, 20, 10, 32),
+                    ("up.32.0", 1280, 20, 10, 32), ("up.32.1", 1280, 20, 10, 32), ("up.32.2", 1280, 20, 10, 32),
+                    ("up.64.0", 640, 10, 2, 64), ("up.64.1", 640, 10, 2, 64), ("up.64.2", 640, 10, 2, 64)]
+CONTEXT_DIM = 2048
+CONTEXT_TOKENS = 231
+
+
+def _linear_shapes(dim: int, context_dim: int) -> dict[str, tuple[int, int]]:
+    ffi = 4 * dim
+    return {"attn1.to_q": (dim, dim), "attn1.to_k": (dim, dim), "attn1.to_v": (dim, dim), "attn1.to_out.0": (dim, dim),
+            "attn2.to_q": (dim, dim), "attn2.to_k": (dim, context_dim), "attn2.to_v": (dim, context_dim),
+            "attn2.to_out.0": (dim, dim), "ff.net.0.proj": (2 * ffi, dim), "ff.net.2": (dim, ffi)}
+
+
+class SDXLStacksQLoRA:
+    """The 11 SpatialTransformers with NF4 bases and LoRA adapters; adapters in one flat bf16 buffer (grads
+    f32) stepped by RAdamScheduleFreeFlat. Synthetic random-init weights (no checkpoint is available here):
+    bases N(0, 1/in) quantised to NF4 on the device, LoRA down kaiming-uniform and up zero as LoRALinear's
+    init (src/modules/peft/lora.py:71-84), LayerNorm / GroupNorm weights 1, biases 0."""
+
+    def __init__(self, B: int = 4, rank: int = 16, alpha: float = 1.0, stacks=SDXL_1024_STACKS,
+                 context_dim: int = CONTEXT_DIM, n_ctx: int = CONTEXT_TOKENS, device="cuda", seed: int = 0,
+                 lr: float = 1e-3):
+        self.B, self.rank, self.alpha, self.n_ctx, self.cdim = B, rank, alpha, n_ctx, context_dim
+        self.stacks_cfg = list(stacks)
+        self.device = torch.device(device)
+        g = torch.Generator(device=self.device).manual_seed(seed)
+        # flat adapter layout: per stack, block, target: down [r, in] then up [out, r]
+        spans, total = [], 0
+        for (_, C, heads, depth, _) in self.stacks_cfg:
+            for _i in range(depth):
+                for t, (o, i) in _linear_shapes(heads * 64, context_dim).items():
+                    spans.append((total, (rank, i), total + rank * i, (o, rank)))
+                    total += rank * i + o * rank
+        self.params = torch.zeros(total, dtype=BF16, device=self.device)
+        self.grads = torch.zeros(total, dtype=F32, device=self.device)
+        code2 = dynamic_map().to(self.device)
+        self.stacks = []
+        k = 0
+        for (name, C, heads, depth, side) in self.stacks_cfg:
+            dim = heads * 64
+            sd = {"norm.weight": torch.ones(C, device=self.device), "norm.bias": torch.zeros(C, device=self.device),
+                  "proj_in.weight": torch.randn(dim, C, device=self.device, generator=g) / math.sqrt(C),
+                  "proj_in.bias": torch.zeros(dim, device=self.device),
+                  "proj_out.weight": torch.randn(C, dim, device=self.device, generator=g) / math.sqrt(dim),
+                  "proj_out.bias": torch.zeros(C, device=self.device)}
+            for i in range(depth):
+                pre = f"transformer_blocks.{i}."
+                for t, (o, inf) in _linear_shapes(dim, context_dim).items():
+                    d0, dsh, u0, ush = spans[k]
+                    k += 1
+                    down = self.params[d0:d0 + dsh[0] * dsh[1]].view(dsh)
+                    down.copy_(((torch.rand(dsh, device=self.device, generator=g) * 2 - 1)
+                                * math.sqrt(6.0 / inf)).to(BF16))
+                    sd[pre + f"{t}.linear.weight"] = (torch.randn(o, inf, device=self.device, generator=g)
+                                                      / math.sqrt(inf)).to(BF16)
+                    if t in ("attn1.to_out.0", "attn2.to_out.0", "ff.net.0.proj", "ff.net.2"):
+                        sd[pre + f"{t}.linear.bias"] = torch.zeros(o, device=self.device)
+                    sd[pre + f"{t}.lora_down.weight"] = down
+                    sd[pre + f"{t}.lora_up.weight"] = self.params[u0:u0 + ush[0] * ush[1]].view(ush)  # zeros
+                for n in ("norm1", "norm2", "norm3"):
+                    sd[pre + f"{n}.weight"] = torch.ones(dim, device=self.device)
+                    sd[pre + f"{n}.bias"] = torch.zeros(dim, device=self.device)
+            st = SDXLSpatialTransformer(C, heads, depth, context_dim, rank, alpha, sd, code2=code2, device=self.device)
+            self.stacks.append((name, C, side * side, st))
+            del sd
+        # bind every adapter to its flat parameter / gradient slices (LoRALinearNF4 copies nothing: bf16 views)
+        k = 0
+        for (_, _, _, st) in self.stacks:
+            for blk in st.blocks:
+                for t in TARGETS:
+                    d0, dsh, u0, ush = spans[k]
+                    k += 1
+                    lin = blk.lin[t]
+                    lin.down = self.params[d0:d0 + dsh[0] * dsh[1]].view(dsh)
+                    lin.up = self.params[u0:u0 + ush[0] * ush[1]].view(ush)
+                    lin.g_down = self.grads[d0:d0 + dsh[0] * dsh[1]].view(dsh)
+                    lin.g_up = self.grads[u0:u0 + ush[0] * ush[1]].view(ush)
+        self.opt = RAdamScheduleFreeFlat(self.params, self.grads, lr=lr)
+        self.opt.train()
+
+    def n_adapter_params(self) -> int:
+        return self.params.numel()
+
+    def make_inputs(self, seed: int = 1):
+        """Synthetic stage activations (NCHW bf16), text context [B*231, 2048] and output gradients g_s."""
+        g = torch.Generator(device=self.device).manual_seed(seed)
+        xs = [torch.randn(self.B, C, HW, device=self.device, generator=g).to(BF16) for (_, C, HW, _) in self.stacks]
+        gs = [(torch.randn(self.B, C, HW, device=self.device, generator=g) * 1e-3).to(BF16)
+              for (_, C, HW, _) in self.stacks]
+        ctx = torch.randn(self.B * self.n_ctx, self.cdim, device=self.device, generator=g).to(BF16)
+        return xs, ctx, gs
+
+    def step(self, xs, ctx, gs):
+        """One training step: forward of every stack, backward in reverse order, fused optimizer step.
+        Returns the context gradient (summed over stacks), [B*231, 2048] bf16."""
+        self.grads.zero_()
+        for x, (_, C, HW, st) in zip(xs, self.stacks):
+            st.forward(x, ctx, self.B, HW, self.n_ctx)
+        dctx = None
+        for gout, (_, C, HW, st) in zip(reversed(gs), reversed(self.stacks)):
+            _dx, dc = st.backward(gout)
+            dctx = dc if dctx is None else ops.add_bf16(dctx, dc)
+        self.opt.step()
+        return dctx
+
+    def flops_per_step(self) -> float:
+        """Algorithmic FLOPs of one step: forward + backward of every GEMM (QLoRA: no base-weight gradient;
+        LoRA down/up forward, their weight and input gradients) and attention (backward = 2x forward)."""
+        B, r, nc, cd = self.B, self.rank, self.n_ctx, self.cdim
+        f = 0.0
+        for (_, C, HW, st) in self.stacks:
+            M = B * HW
+            dim = st.inner
+            f += 2 * (2 * M * C * dim)            # proj_in / proj_out forward
+            f += 2 * (2 * M * C * dim)            # their input gradients
+            for _ in st.blocks:
+                for t, (o, i) in _linear_shapes(dim, cd).items():
+                    m = B * nc if t in ("attn2.to_k", "attn2.to_v") else M
+                    f += 2 * m * o * i + 2 * m * r * (i + o)          # base + LoRA forward
+                    f += 2 * m * o * i + 2 * (2 * m * r * (i + o))    # input grad + LoRA grads
+                heads = st.heads
+                f += 3 * 4 * B * heads * HW * HW * 64                 # self-attention fwd + bwd
+                f += 3 * 4 * B * heads * HW * nc * 64                 # cross-attention fwd + bwd
+        return f
