@@ -210,6 +210,17 @@ int vpt_gemm_nf4(const void* A, long lda, const void* packed, const void* qabsma
                  const float* code2, const float* offset, long kw, int w_kmajor, const void* lora_a, long lda2,
                  const void* lora_b, long ldb2, int r, void* C, long ldc, int M, int N, int K, const void* bias,
                  const void* resid, long ldr, int out_mode, float alpha, void* stream);
+/* LoRA rank-16 skinny products (lora.py:92-104 lora_down / lora_up and their weight gradients):
+ * lora_proj  Y[M][16] = alpha * X[M][K] . W^T, W = down [16][K] (w_kmajor = 1) or up [K][16] (0); K % 128 == 0.
+ * lora_wgrad2 both adapter gradients of one LoRA Linear: g_up [N_out][16] (+)= alpha * dY^T . dS and
+ * g_down [16][N_in] (+)= alpha * X^T . vS, f32; split-M partial sums in ws_up / ws_down
+ * (lora_wgrad_workspace(M, N) bytes each), summed in a fixed order (deterministic). */
+int vpt_lora_proj(const void* X, long ldx, const void* W, int w_kmajor, void* Y, long ldy, int M, int K, int r,
+                  float alpha, void* stream);
+long vpt_lora_wgrad_workspace(int M, int N);
+int vpt_lora_wgrad2(const void* dY, long lddy, const void* dS, long ldds, float* g_up, int n_out, const void* X,
+                    long ldx, const void* vS, long ldvs, float* g_down, int n_in, int M, int accumulate, float alpha,
+                    void* ws_up, void* ws_down, void* stream);
 /* SpatialTransformer (src/models/sdxl/denoiser.py:283-365) around the transformer blocks:
  * GroupNorm(G, C, eps) on NCHW bf16 [B][C][HW] (f32 statistics mean / rstd [B*G] saved for the backward;
  * output NCHW bf16), its input gradient (affine weights frozen under QLoRA; dres: + a second NCHW gradient),

@@ -320,3 +320,24 @@ def test_sdxl_stacks_step_binds_flat_adapters(ops):
                 assert g.abs().max().item() > 0, k
     assert seen == m.grads.numel() == m.n_adapter_params()
     assert m.flops_per_step() > 0
+
+
+@pytest.mark.parametrize("M,K,N", [(16384, 640, 5120), (1000, 1280, 2048), (924, 2048, 1280)])
+def test_lora_skinny_kernels_vs_torch(ops, M, K, N):
+    """vpt_lora_proj (both W layouts) and vpt_lora_wgrad (both output layouts, accumulate) vs fp32 torch on
+    the same bf16 operands: rel <= 5e-3 (bf16 output rounding) / 1e-5 (f32 sums)."""
+    x, dy = rnd(M, K, seed=40), rnd(M, N, seed=41)
+    down, up = rnd(16, K, scale=0.05, seed=42), rnd(N, 16, scale=0.05, seed=43)
+    ds = torch.empty(M, 16, dtype=torch.bfloat16, device=DEV)
+    ops.lora_proj(x, down, True, ds, alpha=0.5)
+    assert rel(ds, 0.5 * x.float() @ down.float().t()) < 5e-3
+    vs = torch.empty(M, 16, dtype=torch.bfloat16, device=DEV)
+    ops.lora_proj(dy, up, False, vs, alpha=2.0)
+    assert rel(vs, 2.0 * dy.float() @ up.float()) < 5e-3
+    g_up = torch.full((N, 16), 0.25, device=DEV)
+    g_down = torch.full((16, K), -0.5, device=DEV)
+    ops.lora_wgrad2(dy, ds, g_up, x, vs, g_down, accumulate=True, alpha=3.0)
+    assert rel(g_up, 0.25 + 3.0 * dy.float().t() @ ds.float()) < 1e-5
+    assert rel(g_down, -0.5 + 3.0 * vs.float().t() @ x.float()) < 1e-5
+    ops.lora_wgrad2(dy, ds, g_up, x, vs, g_down, accumulate=False)
+    assert rel(g_up, dy.float().t() @ ds.float()) < 1e-5 and rel(g_down, vs.float().t() @ x.float()) < 1e-5

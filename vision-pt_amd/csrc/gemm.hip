@@ -1170,14 +1170,15 @@ __device__ __forceinline__ void nf4_store(char* lb, const Nf4Regs& r, const floa
                                           int tid) {
   const float am = code2[r.q] * r.a2 + off;
   const uint32_t w[4] = {r.codes.x, r.codes.y, r.codes.z, r.codes.w};
+  const float2_t* lut2 = reinterpret_cast<const float2_t*>(lut);  // [256] (NF4[b >> 4], NF4[b & 15])
 #pragma unroll
   for (int i = 0; i < 4; ++i) {  // 8 elements (4 packed bytes) per 16-B chunk
     float v[8];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint32_t b = (w[i] >> (8 * j)) & 0xffu;
-      v[2 * j] = lut[b >> 4] * am;       // first element in the high nibble
-      v[2 * j + 1] = lut[b & 15u] * am;
+      const float2_t pr = lut2[(w[i] >> (8 * j)) & 0xffu];  // one b64 read per packed byte
+      v[2 * j] = pr[0] * am;       // first element in the high nibble
+      v[2 * j + 1] = pr[1] * am;
     }
     const uint4 pk = pack8(v);
     if (BKMAJ) {
@@ -1192,8 +1193,8 @@ template <bool BKMAJ>
 __global__ __launch_bounds__(256, 2) void gemm_nf4_kernel(GemmArgs g, Nf4Args f) {
   using G = Geo<128, 128, 2, 2>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* lut = reinterpret_cast<float*>(smem + G::LDS);  // NF4 table (16) + code2 (256), after the tiles
-  float* c2 = lut + 16;
+  float* lut = reinterpret_cast<float*>(smem + G::LDS);  // byte -> NF4 pair table (256 x 2) + code2 (256)
+  float* c2 = lut + 512;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / 2, wn = wid % 2;
   const int tiles_n = (g.N + 127) / 128;
@@ -1202,7 +1203,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nf4_kernel(GemmArgs g, Nf4Args f)
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   const int m0 = wgid / tiles_n * 128, n0 = wgid % tiles_n * 128;
 
-  if (tid < 16) lut[tid] = kNF4g[tid];
+  lut[2 * tid] = kNF4g[tid >> 4];
+  lut[2 * tid + 1] = kNF4g[tid & 15];
   c2[tid] = f.code2[tid];
   const float off = f.offset[0];
 
@@ -1275,10 +1277,194 @@ extern "C" int vpt_gemm_nf4(const void* A, long lda, const void* packed, const v
                (const bf16_t*)lora_a, lda2, (const bf16_t*)lora_b, ldb2, r};
   using G = Geo<128, 128, 2, 2>;
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
-  const int lds = G::LDS + (16 + 256) * 4;
+  const int lds = G::LDS + (512 + 256) * 4;
   hipStream_t s = (hipStream_t)stream;
   if (w_kmajor) hipLaunchKernelGGL(gemm_nf4_kernel<true>, dim3(tiles), dim3(256), lds, s, g, f);
   else hipLaunchKernelGGL(gemm_nf4_kernel<false>, dim3(tiles), dim3(256), lds, s, g, f);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+// ---- LoRA rank-r projections and their weight gradients (r = 16: QLoRA C5; lora.py:92-104) -------------
+// Skinny shapes the 128x128 tile kernels waste 7/8 of a tile on: memory-bound reads of one [M][K] operand.
+//   lora_proj:  Y[M][16] = alpha * sum_k X[m][k] W(j, k),  W = down [16][K] (w_kmajor) or up [K][16]
+//   lora_wgrad: G (+)= alpha * sum_m X[m][n] S[m][j],       G [N][16] (up grad) or [16][N] (down grad)
+// MFMA 16x16x32 bf16; W / S / X tiles transposed through padded LDS images; the wgrad reduction over the
+// M tokens is split across workgroups into f32 slabs summed in a fixed order (deterministic).
+namespace {
+constexpr int LKC = 128;         // K chunk of W staged per step (lora_proj)
+constexpr int LKP = LKC + 8;     // padded LDS row (bf16): conflict-free b128 row reads
+
+__global__ __launch_bounds__(256) void lora_proj_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W,
+                                                        int w_kmajor, bf16_t* __restrict__ Y, long ldy, int M, int K,
+                                                        float alpha) {
+  __shared__ __attribute__((aligned(16))) bf16_t ws[16 * LKP];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int row = blockIdx.x * 64 + wid * 16 + (lane & 15);
+  const int g = lane >> 4;
+  const bf16_t* xr = X + (long)min(row, M - 1) * ldx + 8 * g;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  uint4 xa[LKC / 32], xn[LKC / 32];
+#pragma unroll
+  for (int s = 0; s < LKC / 32; ++s) xa[s] = *reinterpret_cast<const uint4*>(xr + 32 * s);
+  for (int k0 = 0; k0 < K; k0 += LKC) {
+    __syncthreads();
+    if (w_kmajor) {  // down [16][K]: 16 rows x 16 chunks of 16 B
+      const int j = tid >> 4, c = tid & 15;
+      *reinterpret_cast<uint4*>(&ws[j * LKP + c * 8]) = *reinterpret_cast<const uint4*>(W + (long)j * K + k0 + c * 8);
+    } else if (tid < LKC) {  // up [K][16]: one 32-B row per thread, transposed into [16][k]
+      const uint4 a = *reinterpret_cast<const uint4*>(W + (long)(k0 + tid) * 16);
+      const uint4 b = *reinterpret_cast<const uint4*>(W + (long)(k0 + tid) * 16 + 8);
+      const uint32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        ws[(2 * e) * LKP + tid] = (bf16_t)(v[e] & 0xffff);
+        ws[(2 * e + 1) * LKP + tid] = (bf16_t)(v[e] >> 16);
+      }
+    }
+    const bool more = k0 + LKC < K;  // next chunk's activations in flight under this chunk's MFMAs
+    if (more) {
+#pragma unroll
+      for (int s = 0; s < LKC / 32; ++s) xn[s] = *reinterpret_cast<const uint4*>(xr + k0 + LKC + 32 * s);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < LKC / 32; ++s) {
+      const bf16x8 b = as_frag(*reinterpret_cast<const uint4*>(&ws[(lane & 15) * LKP + 32 * s + 8 * g]));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(xa[s]), b, acc, 0, 0, 0);
+    }
+    if (more) {
+#pragma unroll
+      for (int s = 0; s < LKC / 32; ++s) xa[s] = xn[s];
+    }
+  }
+  // D[m][j]: lane holds rows 4g..4g+3 of the wave's 16, column j = lane & 15
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = blockIdx.x * 64 + wid * 16 + 4 * g + r;
+    if (m < M) Y[(long)m * ldy + (lane & 15)] = f2bf(acc[r] * alpha);
+  }
+}
+
+constexpr int LMC = 32;  // m rows per wgrad step
+
+// One wgrad job: G (+)= alpha * X[M][N]^T . S[M][16] (trans: G stored [16][N]); split over gridDim.y.
+struct LoraWgradJob {
+  const bf16_t* X; long ldx;
+  const bf16_t* S; long lds;
+  float* G;
+  float* part;   // [splits][N][16]
+  int N, trans, mchunk, splits;
+};
+
+__global__ __launch_bounds__(256) void lora_wgrad_kernel(LoraWgradJob j0, LoraWgradJob j1, int M) {
+  const LoraWgradJob jb = blockIdx.z ? j1 : j0;
+  if ((int)blockIdx.x >= jb.N / 64 || (int)blockIdx.y >= jb.splits) return;
+  __shared__ __attribute__((aligned(16))) bf16_t xt[64 * (LMC + 8)];  // [n][m]
+  __shared__ __attribute__((aligned(16))) bf16_t st[16 * (LMC + 8)];  // [j][m]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4;
+  const int n0 = blockIdx.x * 64;
+  const int mb = blockIdx.y * jb.mchunk, me = min(M, mb + jb.mchunk);
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int m0 = mb; m0 < me; m0 += LMC) {
+    {  // X tile: 32 rows x 64 n (8 chunks of 8 per row) -> [n][m]
+      const int mr = tid >> 3, c = tid & 7;
+      const int m = m0 + mr;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (m < me) v = *reinterpret_cast<const uint4*>(jb.X + (long)m * jb.ldx + n0 + c * 8);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xt[(c * 8 + 2 * e) * (LMC + 8) + mr] = (bf16_t)(w[e] & 0xffff);
+        xt[(c * 8 + 2 * e + 1) * (LMC + 8) + mr] = (bf16_t)(w[e] >> 16);
+      }
+      if (tid < 64) {  // S tile: 32 rows x 16 j -> [j][m]
+        const int sm = tid >> 1, h = tid & 1;
+        uint4 u = make_uint4(0, 0, 0, 0);
+        if (m0 + sm < me) u = *reinterpret_cast<const uint4*>(jb.S + (long)(m0 + sm) * jb.lds + h * 8);
+        const uint32_t q[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          st[(h * 8 + 2 * e) * (LMC + 8) + sm] = (bf16_t)(q[e] & 0xffff);
+          st[(h * 8 + 2 * e + 1) * (LMC + 8) + sm] = (bf16_t)(q[e] >> 16);
+        }
+      }
+    }
+    __syncthreads();
+    const bf16x8 a = as_frag(*reinterpret_cast<const uint4*>(&xt[(wid * 16 + (lane & 15)) * (LMC + 8) + 8 * g]));
+    const bf16x8 b = as_frag(*reinterpret_cast<const uint4*>(&st[(lane & 15) * (LMC + 8) + 8 * g]));
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+    __syncthreads();
+  }
+  // D[n][j]: rows n = n0 + 16 wid + 4g + r, column j = lane & 15 -> part[split][n][j]
+  float* p = jb.part + ((long)blockIdx.y * jb.N + n0 + wid * 16 + 4 * g) * 16 + (lane & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) p[r * 16] = acc[r];
+}
+
+// G (+)= alpha * (sum of the split slabs in split order): deterministic; blockIdx.y selects the job.
+__global__ void lora_wgrad_reduce_kernel(LoraWgradJob j0, LoraWgradJob j1, float alpha, int accumulate) {
+  const LoraWgradJob jb = blockIdx.y ? j1 : j0;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // element (n, j) of [N][16]
+  if (i >= jb.N * 16) return;
+  float sum = 0.f;
+  for (int z = 0; z < jb.splits; ++z) sum += jb.part[(long)z * jb.N * 16 + i];
+  const int n = i >> 4, j = i & 15;
+  float* d = jb.G + (jb.trans ? (long)j * jb.N + n : (long)i);
+  *d = (accumulate ? *d : 0.f) + alpha * sum;
+}
+}  // namespace
+
+extern "C" int vpt_lora_proj(const void* X, long ldx, const void* W, int w_kmajor, void* Y, long ldy, int M, int K, int r,
+                             float alpha, void* stream) {
+  VPT_CHECK_ARG(X && W && Y, "vpt_lora_proj: null pointer");
+  VPT_CHECK_ARG(r == 16, "vpt_lora_proj: rank 16 (the C5 configuration) only");
+  VPT_CHECK_ARG(M > 0 && K > 0 && K % LKC == 0 && ldx % 8 == 0, "vpt_lora_proj: K % 128 == 0, 16-B leading dim");
+  hipLaunchKernelGGL(lora_proj_kernel, dim3((M + 63) / 64), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)X, ldx,
+                     (const bf16_t*)W, w_kmajor, (bf16_t*)Y, ldy, M, K, alpha);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+static int lora_wgrad_splits(int M, int N) {
+  const int nb = N / 64;
+  int splits = 1024 / (nb > 0 ? nb : 1);
+  const int maxs = (M + 255) / 256;
+  return splits < 1 ? 1 : (splits > maxs ? maxs : splits);
+}
+
+// f32 partial slabs [splits][N][16] of one wgrad.
+extern "C" long vpt_lora_wgrad_workspace(int M, int N) { return (long)lora_wgrad_splits(M, N) * N * 16 * 4; }
+
+static LoraWgradJob lora_job(const void* X, long ldx, const void* S, long lds_, float* G, int trans, int M, int N,
+                             void* ws) {
+  LoraWgradJob j;
+  j.X = (const bf16_t*)X; j.ldx = ldx; j.S = (const bf16_t*)S; j.lds = lds_; j.G = G; j.part = (float*)ws;
+  j.N = N; j.trans = trans;
+  j.splits = lora_wgrad_splits(M, N);
+  int mc = (M + j.splits - 1) / j.splits;
+  j.mchunk = (mc + LMC - 1) / LMC * LMC;
+  j.splits = (M + j.mchunk - 1) / j.mchunk;
+  return j;
+}
+
+// Both adapter gradients of one LoRA Linear in two launches (slabs, then the ordered sum):
+//   G_up [N_out][16] (+)= alpha * dY[M][N_out]^T . dS[M][16]
+//   G_down [16][N_in] (+)= alpha * X[M][N_in]^T . vS[M][16]     (ws_up / ws_down: lora_wgrad_workspace bytes)
+extern "C" int vpt_lora_wgrad2(const void* dY, long lddy, const void* dS, long ldds, float* g_up, int n_out,
+                               const void* X, long ldx, const void* vS, long ldvs, float* g_down, int n_in, int M,
+                               int accumulate, float alpha, void* ws_up, void* ws_down, void* stream) {
+  VPT_CHECK_ARG(dY && dS && g_up && X && vS && g_down && ws_up && ws_down, "vpt_lora_wgrad2: null pointer");
+  VPT_CHECK_ARG(M > 0 && n_out % 64 == 0 && n_in % 64 == 0 && lddy % 8 == 0 && ldx % 8 == 0 && ldds % 8 == 0 &&
+                    ldvs % 8 == 0, "vpt_lora_wgrad2: widths % 64, 16-B leading dims");
+  const LoraWgradJob j0 = lora_job(dY, lddy, dS, ldds, g_up, 0, M, n_out, ws_up);
+  const LoraWgradJob j1 = lora_job(X, ldx, vS, ldvs, g_down, 1, M, n_in, ws_down);
+  hipStream_t s = (hipStream_t)stream;
+  const int gx = max(n_out, n_in) / 64, gy = max(j0.splits, j1.splits);
+  hipLaunchKernelGGL(lora_wgrad_kernel, dim3(gx, gy, 2), dim3(256), 0, s, j0, j1, M);
+  VPT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(lora_wgrad_reduce_kernel, dim3((max(n_out, n_in) * 16 + 255) / 256, 2), dim3(256), 0, s, j0, j1,
+                     alpha, accumulate);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

@@ -69,6 +69,9 @@ SIGNATURES: dict[str, list] = {
     "vpt_groupnorm_fwd": [P, P, P, P, P, P, I, I, I, L, F, P],
     "vpt_groupnorm_bwd": [P, P, P, P, P, P, P, I, I, I, L, P],
     "vpt_transpose_add": [P, P, P, I, I, I, P],
+    "vpt_lora_proj": [P, L, P, I, P, L, I, I, I, F, P],
+    "vpt_lora_wgrad_workspace": [I, I],
+    "vpt_lora_wgrad2": [P, L, P, L, P, I, P, L, P, L, P, I, I, I, F, P, P, P],
     "vpt_gemm_nf4": [P, L, P, P, P, P, P, L, I, P, L, P, L, I, P, L, I, I, I, P, P, L, I, F, P],
     "vpt_nf4_quantize": [P, L, P, P, P, P, P, P, P],
     "vpt_add_bf16": [P, P, L, P, P],
@@ -91,6 +94,7 @@ DIAG_SIGNATURES: dict[str, list] = {
     "vpt_attn_set_fused_workspace": [P],
 }
 _RESTYPES = {
+    "vpt_lora_wgrad_workspace": C.c_long,
     "vpt_gemm_workspace_bytes": C.c_long,
     "vpt_attn_fused_workspace_bytes": C.c_long,
     "vpt_cover_resize_crop_workspace": C.c_long,
@@ -100,7 +104,7 @@ _RESTYPES = {
     "vpt_build_info": C.c_char_p,
 }
 # Entry points that return a value (size / count / string) rather than a status code.
-_VALUE_FNS = {"vpt_gemm_workspace_bytes", "vpt_attn_fused_workspace_bytes", "vpt_cover_resize_crop_workspace", "vpt_gemm_swiglu_bwd_workspace", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
+_VALUE_FNS = {"vpt_lora_wgrad_workspace", "vpt_gemm_workspace_bytes", "vpt_attn_fused_workspace_bytes", "vpt_cover_resize_crop_workspace", "vpt_gemm_swiglu_bwd_workspace", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
               "vpt_colsum_blocks", "vpt_attn_q_scale", "vpt_last_error_string", "vpt_abi_version", "vpt_build_info"}
 
 

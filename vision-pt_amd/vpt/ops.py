@@ -567,6 +567,38 @@ def gemm_nf4(a, w, forward: bool, out, *, lora_a=None, lora_b=None, bias=None, r
     return out
 
 
+def lora_proj(x, w, w_kmajor: bool, out, alpha=1.0):
+    """out[M, 16] = alpha * x[M, K] . W^T, W = down [16, K] (w_kmajor) or up [K, 16] (csrc/gemm.hip lora_proj)."""
+    _chk(x, BF16, "x")
+    _chk(w, BF16, "w")
+    M, K = x.shape
+    call("vpt_lora_proj", x.data_ptr(), x.stride(0), w.data_ptr(), int(w_kmajor), out.data_ptr(), out.stride(0), M, K,
+         16, float(alpha), stream())
+    return out
+
+
+_LORA_WS: dict = {}  # per (device, tag, bytes): split slabs, reused across launches on one stream
+
+
+def _lora_ws(dev, tag, nbytes):
+    ws = _LORA_WS.get((dev, tag, nbytes))
+    if ws is None:
+        ws = _LORA_WS[(dev, tag, nbytes)] = torch.empty(nbytes // 4, dtype=F32, device=dev)
+    return ws
+
+
+def lora_wgrad2(dy, ds, g_up, x, vs, g_down, accumulate=True, alpha=1.0):
+    """Both LoRA adapter gradients (csrc/gemm.hip lora_wgrad): g_up[N_out,16] (+)= alpha dy^T ds and
+    g_down[16,N_in] (+)= alpha vs^T x, f32, deterministic split-M partial sums; 2 launches."""
+    M, n_out = dy.shape
+    n_in = x.shape[1]
+    ws_up = _lora_ws(dy.device, "up", int(lib.vpt_lora_wgrad_workspace(M, n_out)))
+    ws_dn = _lora_ws(dy.device, "down", int(lib.vpt_lora_wgrad_workspace(M, n_in)))
+    call("vpt_lora_wgrad2", dy.data_ptr(), dy.stride(0), ds.data_ptr(), ds.stride(0), g_up.data_ptr(), n_out,
+         x.data_ptr(), x.stride(0), vs.data_ptr(), vs.stride(0), g_down.data_ptr(), n_in, M, int(accumulate),
+         float(alpha), ws_up.data_ptr(), ws_dn.data_ptr(), stream())
+
+
 def nf4_quantize(w, code2, packed, qabsmax, absmax2, offset, scratch):
     call("vpt_nf4_quantize", w.data_ptr(), w.numel(), code2.data_ptr(), packed.data_ptr(), qabsmax.data_ptr(),
          absmax2.data_ptr(), offset.data_ptr(), scratch.data_ptr(), stream())

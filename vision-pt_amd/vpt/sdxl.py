@@ -109,6 +109,8 @@ class LoRALinearNF4:
         # dequant: true for every SDXL UNet Linear (in/out features are multiples of 64); other shapes take
         # the dequant-to-scratch path below.
         self.fused = base.shape[0] % 64 == 0 and base.shape[1] % 64 == 0
+        # rank-16 skinny kernels (vpt_lora_proj / vpt_lora_wgrad) where the widths allow; generic GEMMs otherwise
+        self.skinny = rank == 16 and self.down.shape[0] == 16 and base.shape[0] % 128 == 0 and base.shape[1] % 128 == 0
 
     def weight(self) -> torch.Tensor:
         """The dequantised base weight (bf16) -- for tests and export only; the hot path never builds it."""
@@ -119,8 +121,11 @@ class LoRALinearNF4:
         """resid: a bf16 tensor added in the epilogue (the block's residual stream: bf16(resid + bf16(y)))."""
         M = x.shape[0]
         r = self.down.shape[0]
-        ds = ops.gemm(x, True, self.down, True, M, r, x.shape[1],
-                      torch.empty(M, r, dtype=BF16, device=x.device), alpha=self.scale)
+        ds = torch.empty(M, r, dtype=BF16, device=x.device)
+        if self.skinny:
+            ops.lora_proj(x, self.down, True, ds, alpha=self.scale)
+        else:
+            ops.gemm(x, True, self.down, True, M, r, x.shape[1], ds, alpha=self.scale)
         y = out if out is not None else torch.empty(M, self.base.shape[0], dtype=BF16, device=x.device)
         if self.fused:
             ops.gemm_nf4(x, self.base, True, y, lora_a=ds, lora_b=self.up, bias=self.bias, resid=resid)
@@ -138,10 +143,14 @@ class LoRALinearNF4:
         x, ds = self._saved
         M = x.shape[0]
         r = self.down.shape[0]
-        ops.linear_wgrad(dy, ds, self.g_up, accumulate=True, splits=ops.wgrad_splits(*self.up.shape, M))
-        vs = ops.gemm(dy, True, self.up, False, M, r, self.up.shape[0],
-                      torch.empty(M, r, dtype=BF16, device=dy.device), alpha=self.scale)
-        ops.linear_wgrad(vs, x, self.g_down, accumulate=True, splits=ops.wgrad_splits(*self.down.shape, M))
+        vs = torch.empty(M, r, dtype=BF16, device=dy.device)
+        if self.skinny:
+            ops.lora_proj(dy, self.up, False, vs, alpha=self.scale)
+            ops.lora_wgrad2(dy, ds, self.g_up, x, vs, self.g_down)
+        else:
+            ops.linear_wgrad(dy, ds, self.g_up, accumulate=True, splits=ops.wgrad_splits(*self.up.shape, M))
+            ops.gemm(dy, True, self.up, False, M, r, self.up.shape[0], vs, alpha=self.scale)
+            ops.linear_wgrad(vs, x, self.g_down, accumulate=True, splits=ops.wgrad_splits(*self.down.shape, M))
         dx = torch.empty(M, self.base.shape[1], dtype=BF16, device=dy.device)
         if self.fused:
             return ops.gemm_nf4(dy, self.base, False, dx, lora_a=vs, lora_b=self.down)
