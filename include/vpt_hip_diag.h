@@ -36,6 +36,8 @@ int vpt_attn_set_variant(int v);
 /* f32 dQ accumulator of the fused backward variants 10-13: [B*H][round_up(n, 64)][64]. */
 long vpt_attn_fused_workspace_bytes(int B, int H, int n);
 int vpt_attn_set_fused_workspace(void* ws);
+/* Backward kernel pair: 1 = 64 rows per wave (production default), 0 = the 32-row pair (A/B). */
+int vpt_attn_set_rows64(int on);
 
 #ifdef __cplusplus
 }

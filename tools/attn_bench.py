@@ -1,7 +1,7 @@
 """Developer A/B of the attention backward at the bench's shapes (JiT-B/16, 1024^2, B=8, 12 heads,
-n = 4170 of which 4106 always-valid keys and a masked context tail): the production fused pass
-(variant 0) against round 1's split dK/dV + recomputing dQ kernels (variant 9, diagnostic library),
-numerics of one against the other and timing (HIP events, interleaved rounds).
+n = 4170 of which 4106 always-valid keys and a masked context tail): the 64-rows-per-wave dK/dV + dQ
+pair (production) against the 32-row pair (diagnostic library switch vpt_attn_set_rows64), numerics of
+one against the other and timing (HIP events, interleaved rounds).
 
   VPT_DIAG=1 python tools/attn_bench.py [--rounds 3]
 """
@@ -54,36 +54,32 @@ def main():
     do = torch.randn(B * rows, D, device=dev, generator=g).bfloat16()
     q4, k4, v4 = (ops._t4(qkv, B, rows, H, c) for c in (0, D, 2 * D))
     o4 = ops._t4(o, B, rows, H)
-    ws = torch.empty(int(ops.lib.vpt_attn_fused_workspace_bytes(B, H, n)) // 4, device=dev)
-    ops.lib.vpt_attn_set_fused_workspace(ws.data_ptr())
     ops.attn_fwd(q4, k4, v4, o4, lse, kb, B, H, rows, n, n_dense)
     outs = {}
-    for var in (13, 0):
-        ops.lib.vpt_attn_set_variant(var)
+    for r64 in (0, 1, 2, 4, 3):  # 32-row pair vs 64-row variants (bit mask), same inputs
+        ops.lib.vpt_attn_set_rows64(r64)
         gr = [torch.zeros(B * rows, D, dtype=torch.bfloat16, device=dev) for _ in range(3)]
         ops.attn_bwd(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, kb, *(ops._t4(t, B, rows, H) for t in gr),
                      B, H, rows, n, n_dense)
-        outs[var] = gr
-    ops.lib.vpt_attn_set_variant(0)
+        outs[r64] = gr
     torch.cuda.synchronize()
     res = {}
     for i, nm in enumerate(("dq", "dk", "dv")):
-        a, b = outs[13][i].float(), outs[0][i].float()
-        res[f"rel_{nm}_fused_vs_split"] = ((a - b).norm() / b.norm()).item()
-        res[f"finite_{nm}"] = bool(torch.isfinite(a).all().item())
+        for r64 in (1, 2, 4, 3):
+            a, b = outs[r64][i].float(), outs[0][i].float()
+            res[f"rel_{nm}_v{r64}_vs_rows32"] = ((a - b).norm() / b.norm()).item()
     fl = 4.0 * B * H * n * n * 64
-    t = {0: [], 13: [], 10: [], 11: [], 12: []}
+    t = {0: [], 1: [], 2: [], 4: [], 3: []}
     for _ in range(args.rounds):
-        for var in t:
-            ops.lib.vpt_attn_set_variant(var)
-            t[var].append(timeit(lambda: ops.attn_bwd(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, kb,
+        for r64 in t:
+            ops.lib.vpt_attn_set_rows64(r64)
+            t[r64].append(timeit(lambda: ops.attn_bwd(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, kb,
                                                       *(ops._t4(x, B, rows, H) for x in outs[0]), B, H, rows, n,
                                                       n_dense)))
-    ops.lib.vpt_attn_set_variant(0)
+    ops.lib.vpt_attn_set_rows64(0)
     tf = timeit(lambda: ops.attn_fwd(q4, k4, v4, o4, lse, kb, B, H, rows, n, n_dense))
-    for var, name in ((13, "fused"), (0, "split_production"), (10, "fused_abl_no_atomics"), (11, "fused_abl_plain_stores"),
-                      (12, "fused_abl_no_dq")):
-        ms = sorted(t[var])[len(t[var]) // 2]
+    for r64, name in ((0, "rows32"), (1, "dkdv64"), (2, "dq64_occ2"), (4, "dq64_occ1"), (3, "dkdv64_dq64occ2")):
+        ms = sorted(t[r64])[len(t[r64]) // 2]
         res[f"bwd_ms_{name}"] = round(ms, 4)
         res[f"bwd_alg_tflops_{name}"] = round(2 * fl / (ms * 1e-3) / 1e12, 1)
     res["fwd_ms"] = round(tf, 4)

@@ -52,6 +52,8 @@ constexpr float kTau = 8.f;  // forward lazy-rescale threshold, log2 units
 int g_variant = 0;  // backward kernel variant (vpt_attn_set_variant; 1, 2 = timing-only ablations)
 int g_waves = 4;    // waves per block (vpt_attn_set_variant 3 -> 8-wave blocks, A/B only)
 float g_tau = kTau; // forward lazy-rescale threshold (vpt_attn_set_rescale_threshold)
+int g_rows64 = 0;   // backward variants (vpt_attn_set_rows64 bit mask, A/B): 1 = 64-key dK/dV, 2 = 64-query dQ
+                    // at 2 waves / SIMD, 4 = 64-query dQ at 1 wave / SIMD; 0 = the 32-row pair
 #else
 constexpr int g_variant = 0, g_waves = 4;
 constexpr float g_tau = kTau;
@@ -596,6 +598,233 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dq_kernel(AttnArgs g) {
 }
 
 #ifdef VPT_DIAG
+// ------------------------------------------------------------------ backward, 64 rows per wave
+// The 32-row kernels above read the LDS operand tiles (Q / dO rows and transposes for dK/dV; K / V rows
+// and K transposed for dQ) once per 32 rows they own, which at two 4-wave blocks per CU loads the LDS array
+// about as long as the MFMAs run. Here every wave owns TWO 32-row sub-blocks (64 keys for dK/dV, 64
+// queries for dQ): each LDS fragment read feeds both sub-blocks' MFMA chains, halving LDS operand traffic
+// per MFMA. Twice the accumulators (dK/dV: 128 f32 per lane) -> one wave per SIMD (512 registers).
+// Measured SLOWER than the 32-row pair at B=8 1024^2 (profiles/r02/r02i_attn_bwd_rows64_ab.json: dK/dV64
+// 1.91 ms and dQ64 1.84 ms per backward vs 1.58 ms): with one wave per SIMD the compiler-scheduled body
+// exposes the LDS / exp latencies the second wave used to hide, and dQ64 at two waves per SIMD spills.
+// Kept in the diagnostic build for A/B (vpt_attn_set_rows64).
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv64_kernel(AttnArgs g) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];     // [buf][Q / dO]
+  __shared__ __attribute__((aligned(16))) float lstat[2][2][64];     // [buf][lse / delta]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
+  const int b = blockIdx.z, hd = blockIdx.y;
+  const int k0 = blockIdx.x * (64 * NW) + wid * 64;
+  const bf16_t* Q = g.q.p + b * g.q.sb + hd * g.q.sh;
+  const bf16_t* dO = g.dO.p + b * g.dO.sb + hd * g.dO.sh;
+  const float* LSE = g.lse + b * g.l_sb + hd * g.l_sh;
+  const float* DEL = g.delta_in + b * g.l_sb + hd * g.l_sh;
+
+  bf16x8 kf[2][4], vf[2][4];
+  bool kmasked[2];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    const int key = k0 + 32 * kb + (lane & 31);
+    load_row_frags(kf[kb], g.k.p + b * g.k.sb + hd * g.k.sh, g.k.sr, key, g.nk, lane);
+    load_row_frags(vf[kb], g.v.p + b * g.v.sb + hd * g.v.sh, g.v.sr, key, g.nk, lane);
+    kmasked[kb] = key_bias(g, b, key) == kNegInf;
+  }
+  floatx16 dvT[2][2], dkT[2][2];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int db = 0; db < 2; ++db) dvT[kb][db] = dkT[kb][db] = splat16(0.f);
+
+  const int nt = (g.n + 63) / 64;
+  const void* Qu = uniform_ptr(Q);
+  const void* Du = uniform_ptr(dO);
+  const void* Lu = uniform_ptr(LSE);
+  const void* Eu = uniform_ptr(DEL);
+  auto stage = [&](int buf, int r0) {
+    dma_rows<NW>(lds[buf][0], Qu, g.q.sr, r0, g.n, wid, lane);
+    dma_rows<NW>(lds[buf][1], Du, g.dO.sr, r0, g.n, wid, lane);
+    if (wid == 0) dma_stat(lstat[buf][0], Lu, r0, g.n, lane);
+    else if (wid == 1) dma_stat(lstat[buf][1], Eu, r0, g.n, lane);
+  };
+  auto settle = [&](int buf, int r0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (g.n - r0 < 64) {
+      zero_rows<NW>(lds[buf][0], g.n - r0, tid);
+      zero_rows<NW>(lds[buf][1], g.n - r0, tid);
+      __syncthreads();
+    }
+  };
+  stage(0, 0);
+  settle(0, 0);
+  int cur = 0;
+  for (int t = 0; t < nt; ++t) {
+    const bool more = t + 1 < nt;
+    if (more) stage(cur ^ 1, (t + 1) * 64);
+    const char* lq = lds[cur][0];
+    const char* ld = lds[cur][1];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      // S' = Q~.K^T - LSE and dP' = dO.V^T - delta for both key sub-blocks from one set of row fragments
+      const floatx16 cs = rows16(lstat[cur][0], 32 * qb, h), cd = rows16(lstat[cur][1], 32 * qb, h);
+      bf16x8 qa[4], da[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) { qa[ks] = frag_rows(lq, 32 * qb, ks, lane); da[ks] = frag_rows(ld, 32 * qb, ks, lane); }
+      floatx16 sc[2], dp[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) { sc[kb] = cs; dp[kb] = cd; }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          sc[kb] = mfma32(qa[ks], kf[kb][ks], sc[kb]);
+          dp[kb] = mfma32(da[ks], vf[kb][ks], dp[kb]);
+        }
+      __builtin_amdgcn_s_setprio(0);
+      bf16x8 pp[2][2], pd[2][2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        floatx16 P, dS;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = __builtin_amdgcn_exp2f(sc[kb][i]);
+          P[i] = p;
+          dS[i] = p * dp[kb][i];
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) { pp[kb][s2] = pack_acc(P, s2); pd[kb][s2] = pack_acc(dS, s2); }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 tv[2], tq[2];
+#pragma unroll
+        for (int db = 0; db < 2; ++db) { tv[db] = frag_tr(ld, db, 2 * qb + s2, lane); tq[db] = frag_tr(lq, db, 2 * qb + s2, lane); }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            dvT[kb][db] = mfma32(tv[db], pp[kb][s2], dvT[kb][db]);
+            dkT[kb][db] = mfma32(tq[db], pd[kb][s2], dkT[kb][db]);
+          }
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    if (more) settle(cur ^ 1, (t + 1) * 64);
+    cur ^= 1;
+  }
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    const int key = k0 + 32 * kb + (lane & 31);
+    store_T(g.dv, (long)b * g.dv.sb + hd * g.dv.sh, dvT[kb], 1.f, key, g.nk, lane, kmasked[kb]);
+    store_T(g.dk, (long)b * g.dk.sb + hd * g.dk.sh, dkT[kb], 0.69314718055994531f, key, g.nk, lane, kmasked[kb]);
+  }
+}
+
+template <int NW, int OCC>
+__global__ __launch_bounds__(64 * NW, OCC) void attn_bwd_dq64_kernel(AttnArgs g) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];  // [buf][K / V]
+  extern __shared__ __attribute__((aligned(16))) float kbl[];   // key bias of keys kb0.. (fill_key_bias)
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
+  const int b = blockIdx.z, hd = blockIdx.y;
+  const int q0 = blockIdx.x * (64 * NW) + wid * 64;
+  const bf16_t* K = g.k.p + b * g.k.sb + hd * g.k.sh;
+  const bf16_t* V = g.v.p + b * g.v.sb + hd * g.v.sh;
+
+  bf16x8 qf[2][4], df[2][4];
+  floatx16 nlse[2], ndel[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int qrow = q0 + 32 * qb + (lane & 31);
+    load_row_frags(qf[qb], g.q.p + b * g.q.sb + hd * g.q.sh, g.q.sr, qrow, g.n, lane);
+    load_row_frags(df[qb], g.dO.p + b * g.dO.sb + hd * g.dO.sh, g.dO.sr, qrow, g.n, lane);
+    const long lo = b * g.l_sb + hd * g.l_sh + qrow;
+    nlse[qb] = splat16(qrow < g.n ? g.lse[lo] : -__builtin_huge_valf());
+    ndel[qb] = splat16(qrow < g.n ? g.delta_in[lo] : 0.f);
+  }
+  floatx16 dqT[2][2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) dqT[qb][0] = dqT[qb][1] = splat16(0.f);
+
+  const int nt = (g.nk + 63) / 64;
+  const void* Ku = uniform_ptr(K);
+  const void* Vu = uniform_ptr(V);
+  fill_key_bias<NW>(kbl, g, b, tid);
+  dma_rows<NW>(lds[0][0], Ku, g.k.sr, 0, g.nk, wid, lane);
+  dma_rows<NW>(lds[0][1], Vu, g.v.sr, 0, g.nk, wid, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int cur = 0;
+  for (int t = 0; t < nt; ++t) {
+    const int kv0 = t * 64;
+    const bool more = t + 1 < nt;
+    if (more) {
+      dma_rows<NW>(lds[cur ^ 1][0], Ku, g.k.sr, kv0 + 64, g.nk, wid, lane);
+      dma_rows<NW>(lds[cur ^ 1][1], Vu, g.v.sr, kv0 + 64, g.nk, wid, lane);
+    }
+    const char* lk = lds[cur][0];
+    const char* lv = lds[cur][1];
+    const bool dense = kv0 + 64 <= g.n_dense;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      bf16x8 ka[4], va[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) { ka[ks] = frag_rows(lk, 32 * kb, ks, lane); va[ks] = frag_rows(lv, 32 * kb, ks, lane); }
+      floatx16 sc[2], dp[2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) { sc[qb] = nlse[qb]; dp[qb] = ndel[qb]; }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          sc[qb] = mfma32(ka[ks], qf[qb][ks], sc[qb]);
+          dp[qb] = mfma32(va[ks], df[qb][ks], dp[qb]);
+        }
+      __builtin_amdgcn_s_setprio(0);
+      bf16x8 pd[2][2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        if (!dense) {  // scalar branch: only the context / padding key tiles carry a bias
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) {
+            const floatx4 bias = *reinterpret_cast<const floatx4*>(&kbl[kv0 - g.kb0 + 32 * kb + 8 * g4 + 4 * h]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sc[qb][4 * g4 + e] += bias[e];
+          }
+        }
+        floatx16 dS;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dS[i] = __builtin_amdgcn_exp2f(sc[qb][i]) * dp[qb][i];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) pd[qb][s2] = pack_acc(dS, s2);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 tk[2];
+#pragma unroll
+        for (int db = 0; db < 2; ++db) tk[db] = frag_tr(lk, db, 2 * kb + s2, lane);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+          for (int db = 0; db < 2; ++db) dqT[qb][db] = mfma32(tk[db], pd[qb][s2], dqT[qb][db]);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    cur ^= 1;
+  }
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+    store_T(g.dq, (long)b * g.dq.sb + hd * g.dq.sh, dqT[qb], g.scale, q0 + 32 * qb + (lane & 31), g.n, lane, false);
+}
+
+#endif  // VPT_DIAG
+
+#ifdef VPT_DIAG
 // ------------------------------------------------------------------ backward, fused (diagnostic build)
 // Measured slower than the split pair on this shape (see vpt_attn_bwd); kept for A/B (variant 13).
 // One pass over (key block, query tile) pairs computes all three gradients: the 7 products of the
@@ -978,6 +1207,23 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
   // measured 2.66 ms vs 1.55 ms for this pair (1.14 ms with the atomics removed).
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, s, g, H, rows);
   VPT_LAUNCH_CHECK();
+#ifdef VPT_DIAG
+  if (g_rows64) {  // 64 rows per wave (attn_bwd_dkdv64_kernel / attn_bwd_dq64_kernel)
+    if (g_rows64 & 1)
+      hipLaunchKernelGGL((attn_bwd_dkdv64_kernel<4>), dim3((nk + 255) / 256, H, B), dim3(256), 0, s, g);
+    else
+      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<8, 4>), dim3((nk + 127) / 128, H, B), dim3(256), 0, s, g);
+    VPT_LAUNCH_CHECK();
+    if (g_rows64 & 2)
+      hipLaunchKernelGGL((attn_bwd_dq64_kernel<4, 2>), dim3((n + 255) / 256, H, B), dim3(256), key_bias_lds_bytes(g), s, g);
+    else if (g_rows64 & 4)
+      hipLaunchKernelGGL((attn_bwd_dq64_kernel<4, 1>), dim3((n + 255) / 256, H, B), dim3(256), key_bias_lds_bytes(g), s, g);
+    else
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 4>), dim3((n + 127) / 128, H, B), dim3(256), key_bias_lds_bytes(g), s, g);
+    VPT_LAUNCH_CHECK();
+    return VPT_OK;
+  }
+#endif
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<8, 4>), dim3((nk + 127) / 128, H, B), dim3(256), 0, s, g);
   VPT_LAUNCH_CHECK();
   hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 4>), dim3((n + 127) / 128, H, B), dim3(256), key_bias_lds_bytes(g), s, g);
@@ -990,6 +1236,12 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
 extern "C" int vpt_attn_set_rescale_threshold(float tau) {
   VPT_CHECK_ARG(tau >= 0.f && tau <= 64.f, "vpt_attn_set_rescale_threshold: tau in [0, 64]");
   g_tau = tau;
+  return VPT_OK;
+}
+
+// A/B hook: 1 = the 64-rows-per-wave backward pair (production), 0 = the 32-row pair.
+extern "C" int vpt_attn_set_rows64(int on) {
+  g_rows64 = on;
   return VPT_OK;
 }
 
