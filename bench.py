@@ -120,6 +120,8 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--breakdown", default=None, help="write per-shape GEMM probe totals (JSON) to this file")
+    ap.add_argument("--grad-ckpt", action="store_true",
+                    help="gradient checkpointing on (denoiser.py:945-967): keep block inputs, recompute in backward")
     ap.add_argument("--workload", default="c3", choices=["c3", "c5"],
                     help="c3: JiT-B/16 1024^2 bucketed (the headline); c5: SDXL QLoRA transformer stacks")
     args = ap.parse_args()
@@ -143,6 +145,7 @@ def main():
     cfg = JiT_B_16_Config()
     trainer = JiTTrainer(cfg, N_CLASSES, JiTTrainingConfig(loss_target="image"), device=device, seed=1234 + rank)
     trainer.engine.init_weights(seed=0)  # identical on every rank (replaces DDP's broadcast)
+    trainer.engine.set_gradient_checkpointing(args.grad_ckpt)
     opt = RAdamScheduleFreeFlat(trainer.engine.params, trainer.engine.grads, lr=1e-4)
     opt.train()
     # bf16 wire: the reference's DDP all-reduces the bf16 .grad tensors of its bf16 parameters
@@ -233,7 +236,7 @@ def main():
                    "model": "JiT-B/16", "per_gpu_batch": args.batch, "global_batch": args.batch * world,
                    "seq_len": "4042-4170 tokens", "buckets_wh": BUCKETS, "parallelism": f"dp{world}",
                    "loss_target": "image", "optimizer": "RAdamScheduleFree (fused HIP)",
-                   "grad_allreduce": "bf16 wire, per-block buckets overlapped with backward" if world > 1 else None, "grad_checkpointing": False},
+                   "grad_allreduce": "bf16 wire, per-block buckets overlapped with backward" if world > 1 else None, "grad_checkpointing": bool(args.grad_ckpt)},
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                      "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,

@@ -106,8 +106,10 @@ class HipDenoiser(nn.Module):
         self.engine.init_weights(seed)
 
     def set_gradient_checkpointing(self, enable: bool = True):
-        # Activations are kept (memory is sized for 288 GB HBM); recompute is not needed.
+        """denoiser.py:800-801 + forward_block 945-967: keep only the block inputs in training forwards and
+        recompute each block's intermediates in backward (identical gradients: the kernels are deterministic)."""
         self.gradient_checkpointing = enable
+        self.engine.set_gradient_checkpointing(enable)
 
     def _forward_engine(self, image, timestep, context, original_size, target_size, crop_coords, context_mask,
                         save: bool):

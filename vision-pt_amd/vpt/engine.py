@@ -73,6 +73,7 @@ class JiTEngine:
         self.H = cfg.num_heads
         self.T = cfg.num_time_tokens
         self._state = None
+        self.gradient_checkpointing = False
         self._bind()
 
     # ------------------------------------------------------------------ parameter views
@@ -185,27 +186,14 @@ class JiTEngine:
         x = pool.get("x0", (M, D))
         ops.assemble_tokens(pe2, semb, temb, p["time_position_embeds"], ctx, n_ctx, B, np_, rows, x)
         # --- blocks (denoiser.py:1087-1113)
-        lse_ld = rows
         for i, w in enumerate(self.blk):
             if n_ctx and self._ctx_refresh(i):
                 ops.ctx_rows(x, B, n_pre, rows, n_ctx, ctx=ctx)
-            n_i = rows if (n_ctx and self._ctx_present(i)) else n_pre
-            tag = f"b{i}." if save else "s."
-            xn1, rstd1 = ops.rmsnorm_fwd(x, w["pn1"], pool.get(tag + "xn1", (M, D)), pool.get(tag + "rstd1", (M,), F32))
-            qkv = ops.linear(xn1, w["pwqkv"], w["pbqkv"], out=pool.get(tag + "qkv", (M, 3 * D)))
-            qk = ops.qknorm_rope_fwd(qkv, w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, rows,
-                                     out=pool.get(tag + "qk", (M, 2 * D)),
-                                     q_scale=ops.attn_q_scale(1.0 / math.sqrt(cfg.head_dim)))
-            o = pool.get(tag + "o", (M, D))
-            lse = pool.get(tag + "lse", (B, Hh, lse_ld), F32)
-            ops.attn_fwd(ops._t4(qk, B, rows, Hh, 0), ops._t4(qk, B, rows, Hh, D), ops._t4(qkv, B, rows, Hh, 2 * D),
-                         ops._t4(o, B, rows, Hh, 0), lse, kbias, B, Hh, rows, n_i, n_pre, 1.0 / math.sqrt(cfg.head_dim))
-            xm = ops.linear(o, w["pwo"], w["pbo"], resid=x, out=pool.get(tag + "xm", (M, D)))
-            xn2, rstd2 = ops.rmsnorm_fwd(xm, w["pn2"], pool.get(tag + "xn2", (M, D)), pool.get(tag + "rstd2", (M,), F32))
-            x12, h = ops.linear_swiglu(xn2, w["pw12"], w["pb12"], pool.get(tag + "x12", (M, 2 * F)),
-                                       pool.get(tag + "h", (M, F)))
             x_next = pool.get(f"x{i + 1}" if save else ("xa" if i % 2 == 0 else "xb"), (M, D))
-            ops.linear(h, w["pw3"], w["pb3"], resid=xm, out=x_next)
+            # gradient checkpointing (denoiser.py:945-967): only the block inputs x{i} are kept; the block's
+            # intermediates go to one scratch set and are recomputed in backward
+            tag = ("ck." if self.gradient_checkpointing else f"b{i}.") if save else "s."
+            self._block_forward(i, x, x_next, tag, pool, B, rows, n_ctx, n_pre, kbias, cos_t, sin_t)
             x = x_next
         # --- final layer + (per-patch) output (denoiser.py:1115-1116, 535-543)
         f = self.fin
@@ -216,8 +204,34 @@ class JiTEngine:
         f3 = ops.linear(fh, f["pw3"], f["pb3"], out=pool.get("f3", (M2, D)))
         out = ops.linear(f3, f["pwl"], f["pbl"], out=pool.get("out", (M2, f["pwl"].shape[0])))
         self._state = dict(B=B, H=H, W=W, np_=np_, rows=rows, n_ctx=n_ctx, n_pre=n_pre, M=M, kbias=kbias,
-                           zp=zp, ctx_raw=ctx_raw, cos=cos_t, sin=sin_t) if save else None
+                           zp=zp, ctx_raw=ctx_raw, cos=cos_t, sin=sin_t,
+                           ckpt=self.gradient_checkpointing) if save else None
         return out
+
+    def _block_forward(self, i, x, x_next, tag, pool, B, rows, n_ctx, n_pre, kbias, cos_t, sin_t):
+        """JiTBlock.forward (denoiser.py:582-649) of block i: x -> x_next, intermediates under `tag`."""
+        cfg, D, F, Hh = self.cfg, self.D, self.F, self.H
+        w = self.blk[i]
+        M = x.shape[0]
+        n_i = rows if (n_ctx and self._ctx_present(i)) else n_pre
+        xn1, rstd1 = ops.rmsnorm_fwd(x, w["pn1"], pool.get(tag + "xn1", (M, D)), pool.get(tag + "rstd1", (M,), F32))
+        qkv = ops.linear(xn1, w["pwqkv"], w["pbqkv"], out=pool.get(tag + "qkv", (M, 3 * D)))
+        qk = ops.qknorm_rope_fwd(qkv, w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, rows,
+                                 out=pool.get(tag + "qk", (M, 2 * D)),
+                                 q_scale=ops.attn_q_scale(1.0 / math.sqrt(cfg.head_dim)))
+        o = pool.get(tag + "o", (M, D))
+        lse = pool.get(tag + "lse", (B, Hh, rows), F32)
+        ops.attn_fwd(ops._t4(qk, B, rows, Hh, 0), ops._t4(qk, B, rows, Hh, D), ops._t4(qkv, B, rows, Hh, 2 * D),
+                     ops._t4(o, B, rows, Hh, 0), lse, kbias, B, Hh, rows, n_i, n_pre, 1.0 / math.sqrt(cfg.head_dim))
+        xm = ops.linear(o, w["pwo"], w["pbo"], resid=x, out=pool.get(tag + "xm", (M, D)))
+        xn2, rstd2 = ops.rmsnorm_fwd(xm, w["pn2"], pool.get(tag + "xn2", (M, D)), pool.get(tag + "rstd2", (M,), F32))
+        x12, h = ops.linear_swiglu(xn2, w["pw12"], w["pb12"], pool.get(tag + "x12", (M, 2 * F)),
+                                   pool.get(tag + "h", (M, F)))
+        ops.linear(h, w["pw3"], w["pb3"], resid=xm, out=x_next)
+
+    def set_gradient_checkpointing(self, enable: bool = True):
+        """JiT.set_gradient_checkpointing (denoiser.py:800-801): keep only block inputs, recompute in backward."""
+        self.gradient_checkpointing = bool(enable)
 
     def _ctx_present(self, i: int) -> bool:
         cs = self.cfg.context_start_block
@@ -282,10 +296,14 @@ class JiTEngine:
         delta = pool.get("delta", (B, Hh, rows), F32)
         pre_zeroed = False
         scale = 1.0 / math.sqrt(cfg.head_dim)
+        ck = st.get("ckpt", False)
         for i in reversed(range(cfg.depth)):
             w = self.blk[i]
-            tag = f"b{i}."
+            tag = "ck." if ck else f"b{i}."
             x_in = pool.get(f"x{i}" if i > 0 else "x0", (M, D))
+            if ck:  # recompute the block's intermediates from its saved input (x{i+1} is left untouched)
+                self._block_forward(i, x_in, pool.get("ck.xout", (M, D)), tag, pool, B, rows, n_ctx, n_pre,
+                                    st["kbias"], cos_t, sin_t)
             xn1, qkv, qk, o = (pool.get(tag + n, s) for n, s in (("xn1", (M, D)), ("qkv", (M, 3 * D)),
                                                                  ("qk", (M, 2 * D)), ("o", (M, D))))
             xm, xn2, x12, h = (pool.get(tag + n, s) for n, s in (("xm", (M, D)), ("xn2", (M, D)),
