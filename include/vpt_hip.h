@@ -174,6 +174,9 @@ int vpt_radam_sf_step(void* y, const void* grad, int grad_bf16, float* z, float*
                       float bias_correction2, float eps, float ckp1, float adaptive_y_lr, float lr, float decay,
                       float grad_scale, int adam, void* stream);
 int vpt_sf_lerp(void* y, const float* z, long n, float w, void* stream);
+/* EMA copy of the flat bf16 parameters (swa_utils.AveragedModel(get_ema_avg_fn(decay)), use_buffers=False;
+ * src/trainer/common.py:211-216, 385-386): first = 1 copies, else ema = bf16(bf16(d*ema) + bf16((1-d)*p)). */
+int vpt_ema_update(void* ema, const void* param, long n, float decay, int first, void* stream);
 int vpt_sf_init(const void* y, float* z, float* v, long n, void* stream);
 
 

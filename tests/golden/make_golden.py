@@ -24,6 +24,8 @@ Fixtures:
   sdxl_spatial.safetensors  the reference SpatialTransformer (denoiser.py:283-365): GroupNorm(32, 128), NF4
                          proj_in / proj_out, 2 LoRA-wrapped blocks, context 128, 2 x 8x8 latents, 20 context
                          tokens; fp32 and native-bf16 forward / input, context and adapter grads of sum(out*dy).
+  saving.safetensors     ModelSavingStrategy.should_save over every (epoch, step) of six strategies, which
+                         invalid strategies raise, and the callback file-name template.
   timestep.safetensors   sample_timestep for the scale_shift_sigmoid / sigmoid / uniform / shift_sigmoid /
                          flux_shift samplers (two latent shapes, two global-RNG seeds, non-default kwargs).
   init.safetensors       JiT.initialize_weights + ClassEncoder.initialize_weights on the micro config: per
@@ -342,6 +344,45 @@ def sdxl_spatial_fixture(meta):
                                                        alpha=alpha, B=B, H=H, W=W, nc=nc, weight_seed=21))))
 
 
+def saving_fixture(meta):
+    """ModelSavingStrategy.should_save (src/saving/util.py:15-120) decisions over every (epoch, step) of
+    several strategies, and the callback file-name template (util.py:135, common.py:162-164)."""
+    util = importlib.import_module("src.saving.util")
+    cases = [dict(total_epochs=3, steps_per_epoch=10, per_epochs=1, per_steps=None, save_last=True),
+             dict(total_epochs=4, steps_per_epoch=7, per_epochs=2, per_steps=None, save_last=True),
+             dict(total_epochs=2, steps_per_epoch=12, per_epochs=0.25, per_steps=None, save_last=True),
+             dict(total_epochs=3, steps_per_epoch=10, per_epochs=None, per_steps=4, save_last=False),
+             dict(total_epochs=3, steps_per_epoch=10, per_epochs=1, per_steps=7, save_last=True),
+             dict(total_epochs=2, steps_per_epoch=5, per_epochs=None, per_steps=None, save_last=False)]
+    out = {}
+    for ci, c in enumerate(cases):
+        st = util.ModelSavingStrategy(**c)
+        rows = []
+        step = 0
+        for epoch in range(1, c["total_epochs"] + 1):
+            for _ in range(c["steps_per_epoch"]):
+                step += 1
+                rows.append([epoch, step, int(st.should_save(epoch, step))])
+        out[f"case{ci}"] = torch.tensor(rows, dtype=torch.int64)
+    bad = [dict(total_epochs=3, steps_per_epoch=10, per_epochs=1.5, per_steps=None, save_last=True),
+           dict(total_epochs=3, steps_per_epoch=10, per_epochs=0.5, per_steps=3, save_last=True),
+           dict(total_epochs=3, steps_per_epoch=10, per_epochs=4, per_steps=None, save_last=True),
+           dict(total_epochs=3, steps_per_epoch=10, per_epochs=None, per_steps=31, save_last=True)]
+    raised = []
+    for c in bad:
+        try:
+            util.ModelSavingStrategy(**c)
+            raised.append(0)
+        except ValueError:
+            raised.append(1)
+    out["bad_raises"] = torch.tensor(raised)
+    tmpl = util.ModelSavingCallback.save_name_template
+    names = [tmpl.format(name="jit", epoch=e, steps=s) for e, s in ((1, 10), (12, 123456))]
+    save_file(out, os.path.join(HERE, "saving.safetensors"),
+              metadata=dict(meta, cases=json.dumps(cases), bad=json.dumps(bad), names=json.dumps(names),
+                            template=tmpl))
+
+
 def timestep_fixture(meta):
     """sample_timestep (src/modules/timestep/sampling.py:170-187) for every sampler type the JiT / SDXL
     flow-match steps select, drawn from the global RNG after torch.manual_seed(seed) on CPU."""
@@ -392,6 +433,10 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "sdxl_spatial":
         sdxl_spatial_fixture(meta)
         print("sdxl_spatial", os.path.getsize(os.path.join(HERE, "sdxl_spatial.safetensors")))
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "saving":
+        saving_fixture(meta)
+        print("saving", os.path.getsize(os.path.join(HERE, "saving.safetensors")))
         return
     if len(sys.argv) > 1 and sys.argv[1] == "init":
         init_fixture(R, meta)
@@ -487,7 +532,8 @@ def main():
     timestep_fixture(meta)
     init_fixture(R, meta)
     sdxl_spatial_fixture(meta)
-    for f in ("jit_micro", "jit_c1", "ops", "sampler", "sdxl_block", "timestep", "init", "sdxl_spatial"):
+    saving_fixture(meta)
+    for f in ("jit_micro", "jit_c1", "ops", "sampler", "sdxl_block", "timestep", "init", "sdxl_spatial", "saving"):
         print(f, os.path.getsize(os.path.join(HERE, f + ".safetensors")))
 
 

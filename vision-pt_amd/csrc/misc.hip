@@ -465,6 +465,17 @@ __global__ void lerp_to_z_kernel(bf16_t* __restrict__ y, const float* __restrict
   y[i] = f2bf(yy + w * (z[i] - yy));
 }
 
+// EMA of the bf16 parameters (torch.optim.swa_utils.AveragedModel + get_ema_avg_fn, use_buffers=False, as
+// src/trainer/common.py:211-216 / :385-386 run it on bf16 parameters): ema = bf16(bf16(d * ema) +
+// bf16((1 - d) * p)) -- the foreach bf16 tensor arithmetic's roundings; the first update copies.
+__global__ void ema_update_kernel(bf16_t* __restrict__ ema, const bf16_t* __restrict__ p, long n, float d, float omd,
+                                  int copy) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (copy) { ema[i] = p[i]; return; }
+  ema[i] = f2bf(bf2f(f2bf(d * bf2f(ema[i]))) + bf2f(f2bf(omd * bf2f(p[i]))));
+}
+
 __global__ void init_z_kernel(const bf16_t* __restrict__ y, float* __restrict__ z, float* __restrict__ v, long n) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -716,6 +727,15 @@ extern "C" int vpt_sf_lerp(void* y, const float* z, long n, float w, void* strea
   VPT_CHECK_ARG(y && z, "vpt_sf_lerp: bad args");
   if (n == 0) return VPT_OK;
   hipLaunchKernelGGL(lerp_to_z_kernel, grid1(n), dim3(256), 0, (hipStream_t)stream, (bf16_t*)y, z, n, w);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_ema_update(void* ema, const void* param, long n, float decay, int first, void* stream) {
+  VPT_CHECK_ARG(ema && param && decay >= 0.f && decay <= 1.f, "vpt_ema_update: bad args");
+  if (n == 0) return VPT_OK;
+  hipLaunchKernelGGL(ema_update_kernel, grid1(n), dim3(256), 0, (hipStream_t)stream, (bf16_t*)ema,
+                     (const bf16_t*)param, n, decay, (float)(1.0 - (double)decay), first);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

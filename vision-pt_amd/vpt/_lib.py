@@ -72,6 +72,7 @@ SIGNATURES: dict[str, list] = {
     "vpt_lora_proj": [P, L, P, I, P, L, I, I, I, F, P],
     "vpt_lora_wgrad_workspace": [I, I],
     "vpt_lora_wgrad2": [P, L, P, L, P, I, P, L, P, L, P, I, I, I, F, P, P, P],
+    "vpt_ema_update": [P, P, L, F, I, P],
     "vpt_gemm_nf4": [P, L, P, P, P, P, P, L, I, P, L, P, L, I, P, L, I, I, I, P, P, L, I, F, P],
     "vpt_nf4_quantize": [P, L, P, P, P, P, P, P, P],
     "vpt_add_bf16": [P, P, L, P, P],

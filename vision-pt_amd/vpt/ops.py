@@ -447,6 +447,10 @@ def sf_lerp(y, z, w):
     call("vpt_sf_lerp", y.data_ptr(), z.data_ptr(), y.numel(), w, stream())
 
 
+def ema_update(ema, params, decay, first):
+    call("vpt_ema_update", ema.data_ptr(), params.data_ptr(), params.numel(), float(decay), int(first), stream())
+
+
 def sf_init(y, z, v):
     call("vpt_sf_init", y.data_ptr(), z.data_ptr(), v.data_ptr(), y.numel(), stream())
 
