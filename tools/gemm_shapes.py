@@ -56,6 +56,9 @@ def main():
             fl = 2.0 * M * N * K
             sp = ops.wgrad_splits(N, K, M)
             put(f"{name}.fwd", fl, timeit(lambda: ops.linear(x, w, b, out=y)))
+            if K == N or name == "w3":  # residual epilogue (O / W3 projections)
+                r = torch.randn(M, N, device=dev).bfloat16()
+                put(f"{name}.fwd_resid", fl, timeit(lambda: ops.linear(x, w, b, resid=r, out=y)))
             put(f"{name}.dgrad", fl, timeit(lambda: ops.linear_dgrad(dy, w, out=dx)))
             put(f"{name}.wgrad_s{sp}", fl, timeit(lambda: ops.linear_wgrad(dy, x, dw, splits=sp, workspace=ws)))
             put(f"{name}.bias_grad", fl, timeit(lambda: ops.bias_grad(dy, b.float())))

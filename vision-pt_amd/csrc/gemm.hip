@@ -819,16 +819,27 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
     for (int e = 0; e < 8; ++e) asm volatile("" : "+v"(bias8[e]), "+v"(bias8b[e]));
     // Every wave has passed its last K step (barrier X_nk), so ring stages 0-2 are free: DMA the next
     // item's first tiles before this item's epilogue (which stages through stage 3 only).
+    // An epilogue that loads from memory (residual, SwiGLU x12, f32 accumulate) would drain those DMAs at
+    // its first compiler-placed wait (in-order vmcnt; the compiler does not see the asm DMAs), so for those
+    // modes the next item's prefetch follows the epilogue instead (EPI_PREFETCH_AFTER).
     const int next = item + gridDim.x;
+    const bool epi_loads = g.resid != nullptr || g.sw == 2 || g.out_mode == OUT_F32_ACC;
     RingItem nx;
     if (next < items) {
       nx = ring_item<AK, BK_, SW>(g, next, items, tiles, tiles_n, wid, lane);
+      if (!epi_loads) {
+        ring_issue<AK, BK_, SW>(g, nx, 0, lds0, wid, lane);
+        if (nx.nk > 1) ring_issue<AK, BK_, SW>(g, nx, 1, lds0, wid, lane);
+        if (nx.nk > 2) ring_issue<AK, BK_, SW>(g, nx, 2, lds0, wid, lane);
+      }
+    }
+    if (SW) epilogue_ring_swf(g, acc, stg, lane, it, wm, wn, bias8, bias8b);
+    else epilogue_ring(g, acc, stg, lane, it, wm, wn, bias8);
+    if (next < items && epi_loads) {
       ring_issue<AK, BK_, SW>(g, nx, 0, lds0, wid, lane);
       if (nx.nk > 1) ring_issue<AK, BK_, SW>(g, nx, 1, lds0, wid, lane);
       if (nx.nk > 2) ring_issue<AK, BK_, SW>(g, nx, 2, lds0, wid, lane);
     }
-    if (SW) epilogue_ring_swf(g, acc, stg, lane, it, wm, wn, bias8, bias8b);
-    else epilogue_ring(g, acc, stg, lane, it, wm, wn, bias8);
     if (TL) tl_stamp(g, kth, 3, wid, lane);
     ++kth;
     if (next >= items) break;
@@ -836,7 +847,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
     // X_0, which every wave reaches only after its staging reads (raw_barrier: lgkmcnt(0) first).
     item = next;
     it = nx;
-    pend = S;
+    pend = epi_loads ? 0 : S;  // epilogue-load modes stored BEFORE the next item's DMAs: nothing younger
   }
 }
 
