@@ -911,6 +911,7 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ part, long n, int
 // Geometry choice: the 256x256 ring when its grid (x split-K slices) fills most of the 256 CUs,
 // otherwise 128x128 (2 blocks/CU, 4x the tiles). `req` (128 / 256) forces one (vpt_gemm_bf16_tiled).
 #ifdef VPT_DIAG
+int g_nf4_abl = 0;                    // vpt_gemm_set_nf4_ablation (timing only)
 unsigned long long* g_dbg = nullptr;  // vpt_gemm_set_debug
 int g_geo_override = 0;               // vpt_gemm_set_geometry
 int g_ring_grid_override = 0;         // vpt_gemm_set_ring_grid
@@ -1026,6 +1027,12 @@ extern "C" int vpt_gemm_set_geometry(int geo) {
 extern "C" int vpt_gemm_set_ring_grid(int blocks) {
   VPT_CHECK_ARG(blocks >= 0 && blocks <= 65536, "vpt_gemm_set_ring_grid: 0..65536");
   g_ring_grid_override = blocks;
+  return VPT_OK;
+}
+
+// NF4 GEMM timing ablation (WRONG results): 0 off, 1 no dequant, 2 no NF4 loads and no dequant.
+extern "C" int vpt_gemm_set_nf4_ablation(int a) {
+  g_nf4_abl = a;
   return VPT_OK;
 }
 
@@ -1200,7 +1207,9 @@ __device__ __forceinline__ void nf4_store(char* lb, const Nf4Regs& r, const floa
   }
 }
 
-template <bool BKMAJ>
+// ABL (diagnostic build, timing only, WRONG results): 1 = no dequant (codes loaded, B tile not rewritten),
+// 2 = no NF4 code loads either (B tile stale).
+template <bool BKMAJ, int ABL = 0>
 __global__ __launch_bounds__(256, 2) void gemm_nf4_kernel(GemmArgs g, Nf4Args f) {
   using G = Geo<128, 128, 2, 2>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1238,10 +1247,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nf4_kernel(GemmArgs g, Nf4Args f)
     const bool more = kt + 1 < nk;
     if (more) {
       glds_tile<true, 128, 4>(nb, tile_ptr<true>(g.A, g.lda, m0, (kt + 1) * BK), g.lda, m0, g.M, BK, wid, lane);
-      nr = nf4_load<BKMAJ>(g, f, n0, (kt + 1) * BK, tid);
+      if (ABL < 2) nr = nf4_load<BKMAJ>(g, f, n0, (kt + 1) * BK, tid);
     }
     mma_tile<true, BKMAJ, G>(smem + cur * G::STAGE, acc, wm, wn, lane);
-    if (more) nf4_store<BKMAJ>(nb + G::A_BYTES, nr, lut, c2, off, tid);
+    if (more && ABL == 0) nf4_store<BKMAJ>(nb + G::A_BYTES, nr, lut, c2, off, tid);
+    if (more && ABL == 1) asm volatile("" :: "v"(nr.codes.x), "v"(nr.codes.w), "v"(nr.q), "v"(nr.a2));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     cur ^= 1;
@@ -1290,6 +1300,20 @@ extern "C" int vpt_gemm_nf4(const void* A, long lda, const void* packed, const v
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
   const int lds = G::LDS + (512 + 256) * 4;
   hipStream_t s = (hipStream_t)stream;
+#ifdef VPT_DIAG
+  if (g_nf4_abl == 1) {
+    if (w_kmajor) hipLaunchKernelGGL((gemm_nf4_kernel<true, 1>), dim3(tiles), dim3(256), lds, s, g, f);
+    else hipLaunchKernelGGL((gemm_nf4_kernel<false, 1>), dim3(tiles), dim3(256), lds, s, g, f);
+    VPT_LAUNCH_CHECK();
+    return VPT_OK;
+  }
+  if (g_nf4_abl == 2) {
+    if (w_kmajor) hipLaunchKernelGGL((gemm_nf4_kernel<true, 2>), dim3(tiles), dim3(256), lds, s, g, f);
+    else hipLaunchKernelGGL((gemm_nf4_kernel<false, 2>), dim3(tiles), dim3(256), lds, s, g, f);
+    VPT_LAUNCH_CHECK();
+    return VPT_OK;
+  }
+#endif
   if (w_kmajor) hipLaunchKernelGGL(gemm_nf4_kernel<true>, dim3(tiles), dim3(256), lds, s, g, f);
   else hipLaunchKernelGGL(gemm_nf4_kernel<false>, dim3(tiles), dim3(256), lds, s, g, f);
   VPT_LAUNCH_CHECK();
