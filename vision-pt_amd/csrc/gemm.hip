@@ -1330,54 +1330,74 @@ namespace {
 constexpr int LKC = 128;         // K chunk of W staged per step (lora_proj)
 constexpr int LKP = LKC + 8;     // padded LDS row (bf16): conflict-free b128 row reads
 
-__global__ __launch_bounds__(256) void lora_proj_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W,
-                                                        int w_kmajor, bf16_t* __restrict__ Y, long ldy, int M, int K,
-                                                        float alpha) {
+// One wave per 16 rows (64-thread workgroups, M/16 of them): 128-k chunks with the activation fragments of
+// LPD chunks in flight in registers (a 4-deep ring), so the memory latency is paid once, not per chunk.
+// W = down [16][K]: B fragments straight from global memory (L2-resident, prefetched with the chunk);
+// W = up [K][16]: each chunk transposed through the wave's LDS image.
+constexpr int LPD = 4;
+__global__ __launch_bounds__(64) void lora_proj_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W,
+                                                       int w_kmajor, bf16_t* __restrict__ Y, long ldy, int M, int K,
+                                                       float alpha) {
   __shared__ __attribute__((aligned(16))) bf16_t ws[16 * LKP];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int row = blockIdx.x * 64 + wid * 16 + (lane & 15);
-  const int g = lane >> 4;
+  const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
+  const int row = blockIdx.x * 16 + j;
   const bf16_t* xr = X + (long)min(row, M - 1) * ldx + 8 * g;
+  const bf16_t* wr = W + (long)j * K + 8 * g;  // down: row j
+  const int nch = K / LKC;
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-  uint4 xa[LKC / 32], xn[LKC / 32];
+  uint4 xb[LPD][LKC / 32], wb[LPD][LKC / 32];
 #pragma unroll
-  for (int s = 0; s < LKC / 32; ++s) xa[s] = *reinterpret_cast<const uint4*>(xr + 32 * s);
-  for (int k0 = 0; k0 < K; k0 += LKC) {
-    __syncthreads();
-    if (w_kmajor) {  // down [16][K]: 16 rows x 16 chunks of 16 B
-      const int j = tid >> 4, c = tid & 15;
-      *reinterpret_cast<uint4*>(&ws[j * LKP + c * 8]) = *reinterpret_cast<const uint4*>(W + (long)j * K + k0 + c * 8);
-    } else if (tid < LKC) {  // up [K][16]: one 32-B row per thread, transposed into [16][k]
-      const uint4 a = *reinterpret_cast<const uint4*>(W + (long)(k0 + tid) * 16);
-      const uint4 b = *reinterpret_cast<const uint4*>(W + (long)(k0 + tid) * 16 + 8);
-      const uint32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  for (int u = 0; u < LPD; ++u)
+    if (u < nch) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        ws[(2 * e) * LKP + tid] = (bf16_t)(v[e] & 0xffff);
-        ws[(2 * e + 1) * LKP + tid] = (bf16_t)(v[e] >> 16);
+      for (int s = 0; s < LKC / 32; ++s) {
+        xb[u][s] = *reinterpret_cast<const uint4*>(xr + u * LKC + 32 * s);
+        if (w_kmajor) wb[u][s] = *reinterpret_cast<const uint4*>(wr + u * LKC + 32 * s);
       }
     }
-    const bool more = k0 + LKC < K;  // next chunk's activations in flight under this chunk's MFMAs
-    if (more) {
+  for (int c0 = 0; c0 < nch; c0 += LPD) {
 #pragma unroll
-      for (int s = 0; s < LKC / 32; ++s) xn[s] = *reinterpret_cast<const uint4*>(xr + k0 + LKC + 32 * s);
-    }
-    __syncthreads();
+    for (int u = 0; u < LPD; ++u) {
+      const int c = c0 + u;
+      if (c < nch) {
+        if (!w_kmajor) {  // up [K][16]: 128 rows of 32 B, two per lane, transposed into [16][k]
+          __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int s = 0; s < LKC / 32; ++s) {
-      const bf16x8 b = as_frag(*reinterpret_cast<const uint4*>(&ws[(lane & 15) * LKP + 32 * s + 8 * g]));
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(xa[s]), b, acc, 0, 0, 0);
-    }
-    if (more) {
+          for (int h = 0; h < 2; ++h) {
+            const int kr = lane + 64 * h;
+            const uint4 a = *reinterpret_cast<const uint4*>(W + (long)(c * LKC + kr) * 16);
+            const uint4 b = *reinterpret_cast<const uint4*>(W + (long)(c * LKC + kr) * 16 + 8);
+            const uint32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
-      for (int s = 0; s < LKC / 32; ++s) xa[s] = xn[s];
+            for (int e = 0; e < 8; ++e) {
+              ws[(2 * e) * LKP + kr] = (bf16_t)(v[e] & 0xffff);
+              ws[(2 * e + 1) * LKP + kr] = (bf16_t)(v[e] >> 16);
+            }
+          }
+          __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+          __builtin_amdgcn_wave_barrier();
+        }
+#pragma unroll
+        for (int s = 0; s < LKC / 32; ++s) {
+          const bf16x8 bf = w_kmajor ? as_frag(wb[u][s])
+                                     : as_frag(*reinterpret_cast<const uint4*>(&ws[j * LKP + 32 * s + 8 * g]));
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(xb[u][s]), bf, acc, 0, 0, 0);
+        }
+        if (c + LPD < nch) {
+#pragma unroll
+          for (int s = 0; s < LKC / 32; ++s) {
+            xb[u][s] = *reinterpret_cast<const uint4*>(xr + (c + LPD) * LKC + 32 * s);
+            if (w_kmajor) wb[u][s] = *reinterpret_cast<const uint4*>(wr + (c + LPD) * LKC + 32 * s);
+          }
+        }
+      }
     }
   }
   // D[m][j]: lane holds rows 4g..4g+3 of the wave's 16, column j = lane & 15
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int m = blockIdx.x * 64 + wid * 16 + 4 * g + r;
-    if (m < M) Y[(long)m * ldy + (lane & 15)] = f2bf(acc[r] * alpha);
+    const int m = blockIdx.x * 16 + 4 * g + r;
+    if (m < M) Y[(long)m * ldy + j] = f2bf(acc[r] * alpha);
   }
 }
 
@@ -1401,35 +1421,50 @@ __global__ __launch_bounds__(256) void lora_wgrad_kernel(LoraWgradJob j0, LoraWg
   const int n0 = blockIdx.x * 64;
   const int mb = blockIdx.y * jb.mchunk, me = min(M, mb + jb.mchunk);
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int m0 = mb; m0 < me; m0 += LMC) {
-    {  // X tile: 32 rows x 64 n (8 chunks of 8 per row) -> [n][m]
-      const int mr = tid >> 3, c = tid & 7;
-      const int m = m0 + mr;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (m < me) v = *reinterpret_cast<const uint4*>(jb.X + (long)m * jb.ldx + n0 + c * 8);
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  // the global reads of LPD steps are in flight in registers (a 4-deep ring): one latency per chunk, not per step
+  const int mr = tid >> 3, c = tid & 7;   // X tile: 32 rows x 64 n, one 16-B chunk per thread
+  const int sm = tid >> 1, hh = tid & 1;  // S tile: 32 rows x 16 j, threads 0..63
+  auto ldx_ = [&](int m0) {
+    const int m = m0 + mr;
+    return m < me ? *reinterpret_cast<const uint4*>(jb.X + (long)m * jb.ldx + n0 + c * 8) : make_uint4(0, 0, 0, 0);
+  };
+  auto lds_ = [&](int m0) {
+    return (tid < 64 && m0 + sm < me) ? *reinterpret_cast<const uint4*>(jb.S + (long)(m0 + sm) * jb.lds + hh * 8)
+                                      : make_uint4(0, 0, 0, 0);
+  };
+  uint4 xv[LPD], sv[LPD];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        xt[(c * 8 + 2 * e) * (LMC + 8) + mr] = (bf16_t)(w[e] & 0xffff);
-        xt[(c * 8 + 2 * e + 1) * (LMC + 8) + mr] = (bf16_t)(w[e] >> 16);
-      }
-      if (tid < 64) {  // S tile: 32 rows x 16 j -> [j][m]
-        const int sm = tid >> 1, h = tid & 1;
-        uint4 u = make_uint4(0, 0, 0, 0);
-        if (m0 + sm < me) u = *reinterpret_cast<const uint4*>(jb.S + (long)(m0 + sm) * jb.lds + h * 8);
-        const uint32_t q[4] = {u.x, u.y, u.z, u.w};
+  for (int u = 0; u < LPD; ++u) { xv[u] = ldx_(mb + u * LMC); sv[u] = lds_(mb + u * LMC); }
+  for (int q0 = mb; q0 < me; q0 += LPD * LMC) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          st[(h * 8 + 2 * e) * (LMC + 8) + sm] = (bf16_t)(q[e] & 0xffff);
-          st[(h * 8 + 2 * e + 1) * (LMC + 8) + sm] = (bf16_t)(q[e] >> 16);
+    for (int u = 0; u < LPD; ++u) {
+      const int m0 = q0 + u * LMC;
+      if (m0 < me) {
+        {
+          const uint32_t w[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            xt[(c * 8 + 2 * e) * (LMC + 8) + mr] = (bf16_t)(w[e] & 0xffff);
+            xt[(c * 8 + 2 * e + 1) * (LMC + 8) + mr] = (bf16_t)(w[e] >> 16);
+          }
+          if (tid < 64) {
+            const uint32_t q[4] = {sv[u].x, sv[u].y, sv[u].z, sv[u].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              st[(hh * 8 + 2 * e) * (LMC + 8) + sm] = (bf16_t)(q[e] & 0xffff);
+              st[(hh * 8 + 2 * e + 1) * (LMC + 8) + sm] = (bf16_t)(q[e] >> 16);
+            }
+          }
         }
+        xv[u] = ldx_(m0 + LPD * LMC);  // refill the ring slot LPD steps ahead
+        sv[u] = lds_(m0 + LPD * LMC);
+        __syncthreads();
+        const bf16x8 a = as_frag(*reinterpret_cast<const uint4*>(&xt[(wid * 16 + (lane & 15)) * (LMC + 8) + 8 * g]));
+        const bf16x8 b = as_frag(*reinterpret_cast<const uint4*>(&st[(lane & 15) * (LMC + 8) + 8 * g]));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+        __syncthreads();
       }
     }
-    __syncthreads();
-    const bf16x8 a = as_frag(*reinterpret_cast<const uint4*>(&xt[(wid * 16 + (lane & 15)) * (LMC + 8) + 8 * g]));
-    const bf16x8 b = as_frag(*reinterpret_cast<const uint4*>(&st[(lane & 15) * (LMC + 8) + 8 * g]));
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
-    __syncthreads();
   }
   // D[n][j]: rows n = n0 + 16 wid + 4g + r, column j = lane & 15 -> part[split][n][j]
   float* p = jb.part + ((long)blockIdx.y * jb.N + n0 + wid * 16 + 4 * g) * 16 + (lane & 15);
@@ -1455,7 +1490,7 @@ extern "C" int vpt_lora_proj(const void* X, long ldx, const void* W, int w_kmajo
   VPT_CHECK_ARG(X && W && Y, "vpt_lora_proj: null pointer");
   VPT_CHECK_ARG(r == 16, "vpt_lora_proj: rank 16 (the C5 configuration) only");
   VPT_CHECK_ARG(M > 0 && K > 0 && K % LKC == 0 && ldx % 8 == 0, "vpt_lora_proj: K % 128 == 0, 16-B leading dim");
-  hipLaunchKernelGGL(lora_proj_kernel, dim3((M + 63) / 64), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)X, ldx,
+  hipLaunchKernelGGL(lora_proj_kernel, dim3((M + 15) / 16), dim3(64), 0, (hipStream_t)stream, (const bf16_t*)X, ldx,
                      (const bf16_t*)W, w_kmajor, (bf16_t*)Y, ldy, M, K, alpha);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
