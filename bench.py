@@ -191,7 +191,7 @@ def main():
     # ---- probe pass (after the timed region): one round of the 5 buckets with HIP events around every
     # launch of the MFMA ops (algorithmic FLOPs) and the memory-bound ops (algorithmic HBM bytes)
     mfma_ops = ("attn_fwd", "attn_bwd", "gemm")
-    hbm_ops = ("rmsnorm_fwd", "rmsnorm_bwd", "qknorm_rope_fwd", "qknorm_rope_bwd", "bias_grad", "patchify",
+    hbm_ops = ("rmsnorm_fwd", "rmsnorm_bwd", "qknorm_rope_fwd", "qknorm_rope_bwd", "patchify",
                "flow_loss", "radam_sf_step")
     probes = {k: ops.KernelProbe(k) for k in mfma_ops + hbm_ops}
     ops.PROBES.update(probes)

@@ -49,6 +49,17 @@ int vpt_gemm_bf16_tiled(const void* A, long lda, int a_kmajor, const void* B, lo
                         long ldc, int M, int N, int K, const void* bias, const void* resid, long ldr, int out_mode,
                         int act, int splits, void* workspace, float alpha, int geometry, int ring_grid,
                         void* stream);
+/* nn.Linear weight and bias gradient in one call (torch autograd of F.linear for every Linear of
+ * src/models/jit/denoiser.py, e.g. :318-323 attention projections, :492-504 SwiGLU, :535-543 FinalLayer):
+ * dw[N][K] (=|+=) dy[M][N]^T . x[M][K] and, if db != NULL, db[N] (=|+=) sum_m dy[m][N], both f32
+ * (accumulate = 1 adds). On the 256x256 ring geometry the bias sums ride the GEMM (MFMAs of the dy fragments
+ * against an all-ones fragment, reduced with the split-K slabs in one launch); otherwise the colsum path of
+ * vpt_bias_grad runs after the GEMM. workspace: vpt_linear_wgrad_workspace_bytes(M, N, K, splits) bytes.
+ * geometry / ring_grid as vpt_gemm_bf16_tiled (0 = automatic). Deterministic. */
+int vpt_linear_wgrad(const void* dy, long lddy, const void* x, long ldx, float* dw, long lddw, float* db, long M,
+                     int N, int K, int accumulate, int splits, void* workspace, int geometry, int ring_grid,
+                     void* stream);
+long vpt_linear_wgrad_workspace_bytes(long M, int N, int K, int splits);
 
 /* Fused SwiGLU MLP GEMMs (src/models/jit/denoiser.py:480-506 SwiGLU, :535-543 FinalLayer):
  * forward: x12 [M][2F] = x.W12^T + b12 (W12 = w_1 | w_2 rows, [2F][K]) and h [M][F] =

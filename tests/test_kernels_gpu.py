@@ -120,6 +120,52 @@ def test_gemm_ring_persistent_grid(ops, grid):
         assert rel(out, dy.float().t() @ x.float()) < 1e-5
 
 
+@pytest.mark.parametrize("grid", [3, 0])
+@pytest.mark.parametrize("M,N,K", [(1100, 776, 200), (2100, 768, 768)])
+def test_gemm_ring_epilogue_loads(ops, grid, M, N, K):
+    """Ring epilogue modes that read memory (residual add, f32 accumulate into C), whose operands are
+    preloaded in groups before the next item's LDS-DMA: several items per block (grid 3) and one block
+    per CU (grid 0), ragged last row / column tiles. Against the T128 kernel (same roundings) and fp32."""
+    t = dict(geometry=256, ring_grid=grid)
+    x = rnd(M, K, seed=140)
+    w = rnd(N, K, scale=0.05, seed=141)
+    b = rnd(N, scale=0.1, seed=142)
+    r = rnd(M, N, seed=143)
+    y = ops.linear(x, w, bias=b, resid=r, **t)
+    lin = (x.float() @ w.float().t() + b.float()).to(torch.bfloat16)
+    assert rel(y, (lin.float() + r.float()).to(torch.bfloat16)) < 5e-3
+    y128 = ops.linear(x, w, bias=b, resid=r, geometry=128)
+    assert (y.float() - y128.float()).abs().max().item() <= 2 * (y128.float().abs().max().item() * 2 ** -8)
+    dy = rnd(M, N, seed=144)
+    out0 = rnd(N, K, seed=145, dtype=torch.float32)
+    out = out0.clone()
+    ops.linear_wgrad(dy, x, out, accumulate=True, splits=1, **t)
+    assert rel(out, out0 + dy.float().t() @ x.float()) < 1e-5
+
+
+@pytest.mark.parametrize("geo,grid,splits", [(256, 0, 1), (256, 3, 5), (256, 0, 9), (128, 0, 1), (128, 0, 3)])
+@pytest.mark.parametrize("M,N,K", [(1100, 776, 200), (4170, 768, 768), (333, 264, 136)])
+def test_linear_wgrad_fused_bias(ops, geo, grid, splits, M, N, K):
+    """Weight + bias gradient in one call (vpt_linear_wgrad): on the ring the bias sums are MFMAs of the dy
+    fragments against an all-ones fragment in the first output tile's items (ragged row tiles, several
+    items per block, split-K partial sums reduced with the slabs); on T128 the colsum fallback. Store and
+    accumulate modes, against fp32 torch and against the standalone colsum kernel."""
+    dy = rnd(M, N, seed=150)
+    x = rnd(M, K, seed=151)
+    out = torch.empty(N, K, dtype=torch.float32, device=DEV)
+    b = torch.empty(N, dtype=torch.float32, device=DEV)
+    ops.linear_wgrad(dy, x, out, splits=splits, bias_out=b, geometry=geo, ring_grid=grid)
+    ref_w, ref_b = dy.float().t() @ x.float(), dy.float().sum(0)
+    assert rel(out, ref_w) < 1e-5
+    assert rel(b, ref_b) < 1e-5
+    bc = torch.empty_like(b)
+    ops.bias_grad(dy, bc)
+    assert rel(b, bc) < 1e-6
+    ops.linear_wgrad(dy, x, out, accumulate=True, splits=splits, bias_out=b, geometry=geo, ring_grid=grid)
+    assert rel(out, 2 * ref_w) < 1e-5
+    assert rel(b, 2 * ref_b) < 1e-5
+
+
 @pytest.mark.parametrize("M", [5192, 33360])
 def test_swiglu_fused_epilogues_match_unfused(ops, M):
     """The fused SwiGLU ring epilogues the bench runs (forward sw=1: W1|W2 GEMM -> x12, h; backward sw=2:

@@ -50,6 +50,9 @@ struct GemmArgs {
   int sw;
   bf16_t* C2; long ldc2;
   const bf16_t* aux; long ldaux;
+  // row sums of A over this item's K slice (wgrad direction: the bias gradient sum_t dY[t][m]), f32 at
+  // rsum[split * M + m]; ring kernel (RS instantiation) only
+  float* rsum;
 };
 
 // ---- LDS images -----------------------------------------------------------------------------
@@ -525,13 +528,99 @@ __device__ __forceinline__ void ring_issue(const GemmArgs& g, const RingItem& it
   }
 }
 
-// Ring epilogue. Per 16-row fragment of the wave's 128x64 sub-tile: stage the f32 accumulators in the
-// wave's 4 KB slice of ring stage 3 (16 rows x 64 floats, 16-B slot ^= row & 1: conflict-free b128
-// reads, 2-way b32 writes), read back 2 rows x 8 consecutive columns per lane, apply alpha / bias /
-// SiLU / residual / accumulate, and store with buffer stores. Rows past M fall outside the buffer's
-// num_records and columns past N carry an offset past it, so the hardware drops them without a
-// branch: every wave issues exactly ring_stores(out_mode) store instructions, which the next item's
-// counted vmcnt waits rely on (stores are younger than that item's first three K tiles).
+// Buffer descriptors and per-lane offsets of one item's epilogue (output, residual, SwiGLU x12).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+struct EpiAddr {
+  __amdgpu_buffer_rsrc_t rs, rr, ra;
+  uint32_t voff, rvoff, avoff;
+  int rstride, rrstride, rastride;
+  bool col_ok;
+};
+
+__device__ __forceinline__ EpiAddr epi_addr(const GemmArgs& g, const RingItem& it, int wm, int wn, int lane) {
+  EpiAddr e;
+  const int es = g.out_mode == OUT_BF16 ? 2 : 4;
+  const int rows_here = min(256, g.M - it.m0);
+  char* cbase = (char*)g.C + ((long)it.split * g.split_stride + (long)it.m0 * g.ldc + it.n0) * es;
+  e.rs = __builtin_amdgcn_make_buffer_rsrc(cbase, (short)0, rows_here * (int)g.ldc * es, 0x00020000);
+  const int tcol = wn * 64 + (lane & 7) * 8;  // column within the tile
+  e.col_ok = it.n0 + tcol < g.N;
+  const int lrow = wm * 128 + (lane >> 3);  // tile row of (fragment 0, p = 0)
+  // lane part of the store offset; fragment i / half p add the wave-uniform soffset (i*16 + p*8) rows
+  e.voff = e.col_ok ? (uint32_t)((lrow * (int)g.ldc + tcol) * es) : 0x80000000u;
+  e.rstride = (int)g.ldc * es;  // bytes per row
+  // residual rows of this tile (bf16, leading dim ldr), addressed like C
+  const bf16_t* rbase = g.resid ? g.resid + (long)it.m0 * g.ldr + it.n0 : g.resid;
+  e.rr = __builtin_amdgcn_make_buffer_rsrc((void*)rbase, (short)0, g.resid ? rows_here * (int)g.ldr * 2 : 0, 0x00020000);
+  e.rrstride = (int)g.ldr * 2;
+  e.rvoff = e.col_ok ? (uint32_t)((lrow * (int)g.ldr + tcol) * 2) : 0x80000000u;
+  // fused SwiGLU backward: x12 rows of this tile (bf16, leading dim ldaux)
+  const bf16_t* abase = g.aux ? g.aux + (long)it.m0 * g.ldaux + it.n0 : g.aux;
+  e.ra = __builtin_amdgcn_make_buffer_rsrc((void*)abase, (short)0, g.aux ? rows_here * (int)g.ldaux * 2 : 0, 0x00020000);
+  e.rastride = (int)g.ldaux * 2;
+  e.avoff = e.col_ok ? (uint32_t)((lrow * (int)g.ldaux + tcol) * 2) : 0x80000000u;
+  return e;
+}
+
+// Epilogue operands read from memory (residual, SwiGLU-backward x12, f32 accumulate target) arrive in
+// groups of 8 loads (32 VGPRs), waited for once per group. Issued per fragment inside the epilogue, each
+// load's compiler-placed wait was a vmcnt(0) (16 serial HBM round trips per item) and, being younger than
+// the prefetched tiles, drained them. The first group is loaded BEFORE the next item's LDS-DMA; a later
+// group is loaded right after the previous group's stores (its wait then also covers the DMAs, by then
+// long in flight). Residual: 2 loads per fragment, groups of 4 fragments; x12 / accumulate: 4 loads per
+// fragment, groups of 2. Slot of fragment il (in its group), half p, part e: resid 2il + p, else 4il + 2p + e.
+// Epilogue modes (a template parameter of the ring kernel, so that each mode gets its own register
+// allocation): 0 = no loads (bf16 / f32 out, bias, SiLU), 1 = residual, 2 = fused SwiGLU backward (x12),
+// 3 = f32 accumulate into C.
+enum { EPI_PLAIN = 0, EPI_RESID = 1, EPI_SWB = 2, EPI_ACC = 3 };
+__host__ __device__ constexpr int epi_frags(int epi) {  // fragments per preload group (0: no loads)
+  return epi == EPI_RESID ? 4 : (epi == EPI_SWB || epi == EPI_ACC) ? 2 : 0;
+}
+__host__ __device__ inline int epi_mode(const GemmArgs& g) {
+  return g.sw == 2 ? EPI_SWB : g.out_mode == OUT_F32_ACC ? EPI_ACC : g.resid ? EPI_RESID : EPI_PLAIN;
+}
+struct EpiPre {
+  u32x4 v[8];
+};
+template <int EPI, int I0>
+__device__ __forceinline__ void epi_preload(const GemmArgs& g, const EpiAddr& e, EpiPre& pre) {
+  if (EPI == EPI_SWB) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int so = ((I0 + i) * 16 + p * 8) * e.rastride;
+        pre.v[4 * i + 2 * p] = __builtin_amdgcn_raw_buffer_load_b128(e.ra, (int)e.avoff, so, 0);
+        pre.v[4 * i + 2 * p + 1] =
+            __builtin_amdgcn_raw_buffer_load_b128(e.ra, (int)(e.col_ok ? e.avoff + g.N * 2 : e.avoff), so, 0);
+      }
+  } else if (EPI == EPI_ACC) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int so = ((I0 + i) * 16 + p * 8) * e.rstride;
+        pre.v[4 * i + 2 * p] = __builtin_amdgcn_raw_buffer_load_b128(e.rs, (int)e.voff, so, 0);
+        pre.v[4 * i + 2 * p + 1] = __builtin_amdgcn_raw_buffer_load_b128(e.rs, (int)e.voff, so + 16, 0);
+      }
+  } else if (EPI == EPI_RESID) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        pre.v[2 * i + p] =
+            __builtin_amdgcn_raw_buffer_load_b128(e.rr, (int)e.rvoff, ((I0 + i) * 16 + p * 8) * e.rrstride, 0);
+  }
+}
+
+// Ring epilogue over fragments [i0, i1). Per 16-row fragment of the wave's 128x64 sub-tile: stage the
+// f32 accumulators in the wave's 4 KB slice of ring stage 3 (16 rows x 64 floats, 16-B slot ^= row & 1:
+// conflict-free b128 reads, 2-way b32 writes), read back 2 rows x 8 consecutive columns per lane, apply
+// alpha / bias / SiLU / residual / accumulate (operands from `pre`, group of i0), and store with buffer
+// stores. Rows past M fall outside the buffer's num_records and columns past N carry an offset past it,
+// so the hardware drops them without a branch: every wave issues exactly ring_stores(out_mode) store
+// instructions, which the next item's counted vmcnt waits rely on (stores are younger than that item's
+// first three K tiles).
 __device__ __forceinline__ int ring_stores(const GemmArgs& g) {
   if (g.sw == 1) return 24;  // x1, x2, h per lane and fragment
   if (g.sw == 2) return 32;  // dx1, dx2 per lane, fragment and half
@@ -542,35 +631,13 @@ __device__ __forceinline__ int stg_off(int row, int col) {
   return row * 256 + (((col >> 2) ^ (row & 1)) << 4) + ((col & 3) << 2);
 }
 
+template <int EPI, int I0, int I1>
 __device__ __forceinline__ void epilogue_ring(const GemmArgs& g, const floatx4 (&acc)[8][4], char* stg, int lane,
-                                              const RingItem& it, int wm, int wn, const float (&bias8)[8]) {
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const int es = g.out_mode == OUT_BF16 ? 2 : 4;
-  const int rows_here = min(256, g.M - it.m0);
-  char* cbase = (char*)g.C + ((long)it.split * g.split_stride + (long)it.m0 * g.ldc + it.n0) * es;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(cbase, (short)0, rows_here * (int)g.ldc * es,
-                                                                       0x00020000);
+                                              const EpiAddr& e, const float (&bias8)[8], const EpiPre& pre) {
   const int cw = lane & 7;
-  const int tcol = wn * 64 + cw * 8;  // column within the tile
-  const bool col_ok = it.n0 + tcol < g.N;
-  const int lrow = wm * 128 + (lane >> 3);  // tile row of (fragment 0, p = 0)
-  // lane part of the store offset; fragment i / half p add the wave-uniform soffset (i*16 + p*8) rows
-  const uint32_t voff = col_ok ? (uint32_t)((lrow * (int)g.ldc + tcol) * es) : 0x80000000u;
-  const int rstride = (int)g.ldc * es;  // bytes per row
-  // residual rows of this tile (bf16, leading dim ldr), addressed like C
-  const bf16_t* rbase = g.resid ? g.resid + (long)it.m0 * g.ldr + it.n0 : g.resid;
-  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)rbase, (short)0,
-                                                                       g.resid ? rows_here * (int)g.ldr * 2 : 0, 0x00020000);
-  const int rrstride = (int)g.ldr * 2;
-  const uint32_t rvoff = col_ok ? (uint32_t)((lrow * (int)g.ldr + tcol) * 2) : 0x80000000u;
-  // fused SwiGLU backward: x12 rows of this tile (bf16, leading dim ldaux)
-  const bf16_t* abase = g.aux ? g.aux + (long)it.m0 * g.ldaux + it.n0 : g.aux;
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)abase, (short)0,
-                                                                       g.aux ? rows_here * (int)g.ldaux * 2 : 0, 0x00020000);
-  const int rastride = (int)g.ldaux * 2;
-  const uint32_t avoff = col_ok ? (uint32_t)((lrow * (int)g.ldaux + tcol) * 2) : 0x80000000u;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = I0; i < I1; ++i) {
+    const int il = i - I0;  // fragment within the preload group
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -585,59 +652,56 @@ __device__ __forceinline__ void epilogue_ring(const GemmArgs& g, const floatx4 (
       const floatx4 x1 = *reinterpret_cast<const floatx4*>(stg + stg_off(lr, cw * 8 + 4));
       float o[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = o[e] * g.alpha + bias8[e];
+      for (int q = 0; q < 8; ++q) o[q] = o[q] * g.alpha + bias8[q];
       if (g.act == ACT_SILU) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = o[e] / (1.f + __expf(-o[e]));
+        for (int q = 0; q < 8; ++q) o[q] = o[q] / (1.f + __expf(-o[q]));
       }
-      const int soff = (i * 16 + p * 8) * rstride;
-      if (g.sw == 2) {
+      const int soff = (i * 16 + p * 8) * e.rstride;
+      if (EPI == EPI_SWB) {
         // fused SwiGLU backward (the reference's SwiGLU autograd, denoiser.py:480-506, as swiglu_bwd_kernel):
         // o = dh; x1, x2 from x12; dx1 -> column c, dx2 -> column F + c of dx12 (F = N)
-        const u32x4 a4 = __builtin_amdgcn_raw_buffer_load_b128(ra, (int)avoff, (i * 16 + p * 8) * rastride, 0);
-        const u32x4 b4 = __builtin_amdgcn_raw_buffer_load_b128(ra, (int)(col_ok ? avoff + g.N * 2 : avoff),
-                                                               (i * 16 + p * 8) * rastride, 0);
+        const u32x4 a4 = pre.v[4 * il + 2 * p], b4 = pre.v[4 * il + 2 * p + 1];
         float a[8], b[8], d1[8], d2[8];
         unpack8(make_uint4(a4[0], a4[1], a4[2], a4[3]), a);
         unpack8(make_uint4(b4[0], b4[1], b4[2], b4[3]), b);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float gd = bf2f(f2bf(o[e]));  // dh is a bf16 tensor in the reference
-          const float sg = 1.f / (1.f + expf(-a[e]));
-          const float sv = bf2f(f2bf(a[e] * sg));
-          const float ds = bf2f(f2bf(gd * b[e]));
-          d2[e] = gd * sv;
-          d1[e] = ds * (sg * (1.f + a[e] * (1.f - sg)));
+        for (int q = 0; q < 8; ++q) {
+          const float gd = bf2f(f2bf(o[q]));  // dh is a bf16 tensor in the reference
+          const float sg = 1.f / (1.f + expf(-a[q]));
+          const float sv = bf2f(f2bf(a[q] * sg));
+          const float ds = bf2f(f2bf(gd * b[q]));
+          d2[q] = gd * sv;
+          d1[q] = ds * (sg * (1.f + a[q] * (1.f - sg)));
         }
         const uint4 w1 = pack8(d1), w2 = pack8(d2);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{w1.x, w1.y, w1.z, w1.w}, rs, (int)voff, soff, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{w2.x, w2.y, w2.z, w2.w}, rs, (int)(col_ok ? voff + g.N * 2 : voff),
-                                               soff, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{w1.x, w1.y, w1.z, w1.w}, e.rs, (int)e.voff, soff, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{w2.x, w2.y, w2.z, w2.w}, e.rs,
+                                               (int)(e.col_ok ? e.voff + g.N * 2 : e.voff), soff, 0);
       } else if (g.out_mode == OUT_BF16) {
-        if (g.resid) {
-          // reference semantics: residual + bf16(linear output), rounded again to bf16. Buffer load over
-          // the tile's residual rows: out-of-range rows / columns read 0 (their stores are dropped).
-          const u32x4 r4 = __builtin_amdgcn_raw_buffer_load_b128(rr, (int)rvoff, (i * 16 + p * 8) * rrstride, 0);
+        if (EPI == EPI_RESID) {
+          // reference semantics: residual + bf16(linear output), rounded again to bf16. Out-of-range rows /
+          // columns read 0 (their stores are dropped).
+          const u32x4 r4 = pre.v[2 * il + p];
           float rv[8];
           unpack8(make_uint4(r4[0], r4[1], r4[2], r4[3]), rv);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = bf2f(f2bf(o[e])) + rv[e];
+          for (int q = 0; q < 8; ++q) o[q] = bf2f(f2bf(o[q])) + rv[q];
         }
         const uint4 w = pack8(o);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{w.x, w.y, w.z, w.w}, rs, (int)voff, soff, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{w.x, w.y, w.z, w.w}, e.rs, (int)e.voff, soff, 0);
       } else {
-        if (g.out_mode == OUT_F32_ACC) {
-          const u32x4 a0 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)voff, soff, 0);
-          const u32x4 a1 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)voff, soff + 16, 0);
+        if (EPI == EPI_ACC) {
+          const u32x4 a0 = pre.v[4 * il + 2 * p], a1 = pre.v[4 * il + 2 * p + 1];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) { o[e] += __uint_as_float(a0[e]); o[4 + e] += __uint_as_float(a1[e]); }
+          for (int q = 0; q < 4; ++q) { o[q] += __uint_as_float(a0[q]); o[4 + q] += __uint_as_float(a1[q]); }
         }
         __builtin_amdgcn_raw_buffer_store_b128(
-            u32x4{__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3])}, rs,
-            (int)voff, soff, 0);
+            u32x4{__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3])}, e.rs,
+            (int)e.voff, soff, 0);
         __builtin_amdgcn_raw_buffer_store_b128(
-            u32x4{__float_as_uint(o[4]), __float_as_uint(o[5]), __float_as_uint(o[6]), __float_as_uint(o[7])}, rs,
-            (int)voff, soff + 16, 0);
+            u32x4{__float_as_uint(o[4]), __float_as_uint(o[5]), __float_as_uint(o[6]), __float_as_uint(o[7])}, e.rs,
+            (int)e.voff, soff + 16, 0);
       }
     }
   }
@@ -710,7 +774,8 @@ __device__ __forceinline__ void tl_stamp(const GemmArgs& g, int k, int phase, in
     g.dbg[((long)blockIdx.x * 4 + k) * 4 + phase] = __builtin_amdgcn_s_memrealtime();
 }
 
-template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false, bool STAMP = false, bool TL = false, int SW = 0>
+template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false, bool STAMP = false, bool TL = false, int SW = 0,
+          int EPI = EPI_PLAIN, bool RS = false>
 __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
   using G = GR;
   constexpr int A32 = 256 * RBK * 2, STAGE32 = 2 * A32;
@@ -756,6 +821,12 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
     for (int i = 0; i < G::MI; ++i)
 #pragma unroll
       for (int j = 0; j < G::NI; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // RS (fused bias gradient): the items of the first N tile also sum their A rows over k, as MFMAs of
+    // the A fragments against an all-ones B fragment; wave (wm, wn) takes fragments 2wn and 2wn + 1 of its
+    // 128 rows (2 extra MFMAs per K step). wn is made wave-uniform so the fragment pick is a scalar branch.
+    floatx4 racc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+    const bool rs_on = RS && it.n0 == 0;
+    const int wn_u = __builtin_amdgcn_readfirstlane(wn);
 
     if (pend && nk >= 3) wait_vm_pend(pend);  // tile 0 landed: tiles 1, 2 and the stores are younger
     else wait_younger(min(2, nk - 1));
@@ -796,6 +867,16 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < G::NI; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if (rs_on) {
+        const bf16x8 ones = as_frag(make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u));
+        bf16x8 r0, r1;
+        if (wn_u == 0) { r0 = af[0]; r1 = af[1]; }
+        else if (wn_u == 1) { r0 = af[2]; r1 = af[3]; }
+        else if (wn_u == 2) { r0 = af[4]; r1 = af[5]; }
+        else { r0 = af[6]; r1 = af[7]; }
+        racc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(r0, ones, racc[0], 0, 0, 0);
+        racc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(r1, ones, racc[1], 0, 0, 0);
+      }
       __builtin_amdgcn_s_setprio(0);
       if (STAMP) { t1 = stamp(); seg[4] += t1 - t0; t0 = t1; }
       if (DMAC) bare_barrier(); else raw_barrier();  // X_kt+1
@@ -809,6 +890,22 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
     }
     if (PP && wm == 0) raw_barrier();
     if (TL) tl_stamp(g, kth, 2, wid, lane);
+    if (rs_on && (lane & 15) == 0) {
+      // D layout of the ones-MFMA: lane holds rows 4*(lane>>4) + r of the fragment (every column equal);
+      // issued before the next item's DMA, so the counted waits never see these stores
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        const int row = it.m0 + wm * 128 + (2 * wn_u + f) * 16 + 4 * (lane >> 4);
+        float* dst = g.rsum + (long)it.split * g.M + row;
+        if (row + 3 < g.M && (g.M & 3) == 0) {
+          *reinterpret_cast<floatx4*>(dst) = racc[f];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (row + r < g.M) dst[r] = racc[f][r];
+        }
+      }
+    }
     float bias8[8], bias8b[8];
     unpack8(braw, bias8);
     unpack8(braw2, bias8b);
@@ -816,29 +913,50 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
     // see the asm DMA, places its wait for the bias loads at their first use (in the epilogue) as
     // vmcnt(0), and vmcnt retires in order -- that wait would drain the next item's prefetched tiles.
 #pragma unroll
-    for (int e = 0; e < 8; ++e) asm volatile("" : "+v"(bias8[e]), "+v"(bias8b[e]));
+    for (int e = 0; e < 8; ++e) {
+      asm volatile("" : "+v"(bias8[e]));
+      if (SW) asm volatile("" : "+v"(bias8b[e]));
+    }
     // Every wave has passed its last K step (barrier X_nk), so ring stages 0-2 are free: DMA the next
     // item's first tiles before this item's epilogue (which stages through stage 3 only).
-    // An epilogue that loads from memory (residual, SwiGLU x12, f32 accumulate) would drain those DMAs at
-    // its first compiler-placed wait (in-order vmcnt; the compiler does not see the asm DMAs), so for those
-    // modes the next item's prefetch follows the epilogue instead (EPI_PREFETCH_AFTER).
+    // Epilogue operands read from memory (residual, SwiGLU x12, f32 accumulate) are loaded first and
+    // waited for once, so no wait inside the epilogue drains those DMAs (in-order vmcnt; the compiler
+    // does not see the asm DMAs). A second preload group (x12 / accumulate, fragments 4-7) is loaded
+    // after the first group's stores: its wait also covers the DMAs, by then long in flight.
     const int next = item + gridDim.x;
-    const bool epi_loads = g.resid != nullptr || g.sw == 2 || g.out_mode == OUT_F32_ACC;
+    constexpr int GF = SW ? 0 : epi_frags(EPI);
+    EpiAddr ea;
+    EpiPre pre;
+    if (!SW) {
+      ea = epi_addr(g, it, wm, wn, lane);
+      if (GF) {
+        epi_preload<EPI, 0>(g, ea, pre);
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the first group landed (nothing else in flight)
+      }
+    }
     RingItem nx;
     if (next < items) {
       nx = ring_item<AK, BK_, SW>(g, next, items, tiles, tiles_n, wid, lane);
-      if (!epi_loads) {
-        ring_issue<AK, BK_, SW>(g, nx, 0, lds0, wid, lane);
-        if (nx.nk > 1) ring_issue<AK, BK_, SW>(g, nx, 1, lds0, wid, lane);
-        if (nx.nk > 2) ring_issue<AK, BK_, SW>(g, nx, 2, lds0, wid, lane);
-      }
-    }
-    if (SW) epilogue_ring_swf(g, acc, stg, lane, it, wm, wn, bias8, bias8b);
-    else epilogue_ring(g, acc, stg, lane, it, wm, wn, bias8);
-    if (next < items && epi_loads) {
       ring_issue<AK, BK_, SW>(g, nx, 0, lds0, wid, lane);
       if (nx.nk > 1) ring_issue<AK, BK_, SW>(g, nx, 1, lds0, wid, lane);
       if (nx.nk > 2) ring_issue<AK, BK_, SW>(g, nx, 2, lds0, wid, lane);
+    }
+    if (SW) {
+      epilogue_ring_swf(g, acc, stg, lane, it, wm, wn, bias8, bias8b);
+    } else if (GF == 2) {
+      epilogue_ring<EPI, 0, 2>(g, acc, stg, lane, ea, bias8, pre);
+      epi_preload<EPI, 2>(g, ea, pre);
+      epilogue_ring<EPI, 2, 4>(g, acc, stg, lane, ea, bias8, pre);
+      epi_preload<EPI, 4>(g, ea, pre);
+      epilogue_ring<EPI, 4, 6>(g, acc, stg, lane, ea, bias8, pre);
+      epi_preload<EPI, 6>(g, ea, pre);
+      epilogue_ring<EPI, 6, 8>(g, acc, stg, lane, ea, bias8, pre);
+    } else if (GF == 4) {
+      epilogue_ring<EPI, 0, 4>(g, acc, stg, lane, ea, bias8, pre);
+      epi_preload<EPI, 4>(g, ea, pre);
+      epilogue_ring<EPI, 4, 8>(g, acc, stg, lane, ea, bias8, pre);
+    } else {
+      epilogue_ring<EPI, 0, 8>(g, acc, stg, lane, ea, bias8, pre);
     }
     if (TL) tl_stamp(g, kth, 3, wid, lane);
     ++kth;
@@ -847,7 +965,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
     // X_0, which every wave reaches only after its staging reads (raw_barrier: lgkmcnt(0) first).
     item = next;
     it = nx;
-    pend = epi_loads ? 0 : S;  // epilogue-load modes stored BEFORE the next item's DMAs: nothing younger
+    pend = S;  // the epilogue's S stores are younger than the next item's pre-issued tiles 0-2
   }
 }
 
@@ -867,7 +985,26 @@ int launch_ring(const GemmArgs& g, int splits, hipStream_t s) {
   const int items = ((g.M + 255) / 256) * ((g.N + 255) / 256) * splits;
   const int rg = g.ring_grid > 0 ? g.ring_grid : kRingGrid;
   const int grid = items < rg ? items : rg;
-  hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, SW>), dim3(grid), dim3(512), LDS, s, g);
+  const int epi = SW ? EPI_PLAIN : epi_mode(g);
+  if (!AK && !SW && g.rsum) {  // fused bias gradient (wgrad direction)
+    if (epi == EPI_ACC)
+      hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, 0, EPI_ACC, true>), dim3(grid), dim3(512), LDS,
+                         s, g);
+    else
+      hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, 0, EPI_PLAIN, true>), dim3(grid), dim3(512),
+                         LDS, s, g);
+  } else if (epi == EPI_RESID)
+    hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, SW, SW ? 0 : EPI_RESID>), dim3(grid), dim3(512),
+                       LDS, s, g);
+  else if (epi == EPI_SWB)
+    hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, SW, SW ? 0 : EPI_SWB>), dim3(grid), dim3(512),
+                       LDS, s, g);
+  else if (epi == EPI_ACC)
+    hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, SW, SW ? 0 : EPI_ACC>), dim3(grid), dim3(512),
+                       LDS, s, g);
+  else
+    hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, SW, EPI_PLAIN>), dim3(grid), dim3(512), LDS, s,
+                       g);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
@@ -890,8 +1027,19 @@ int launch_geo(const GemmArgs& g, int splits, int geo, hipStream_t s) {
   return launch<AK, BK_, 128, 128, 2, 2>(g, splits, s);
 }
 
+// Fixed-order sum of the split-K partial slabs (blocks [0, cblocks)) and, in the same launch, of the
+// per-split row sums of a fused bias gradient (blocks from cblocks: rout[m] (+)= sum_z rpart[z][m]).
 __global__ void splitk_reduce_kernel(const float* __restrict__ part, long n, int splits, long stride,
-                                     void* out, int out_mode) {
+                                     void* out, int out_mode, long cblocks, const float* __restrict__ rpart,
+                                     int rsplits, int rn, float* rout, int racc) {
+  if ((long)blockIdx.x >= cblocks) {
+    const long m = ((long)blockIdx.x - cblocks) * blockDim.x + threadIdx.x;
+    if (m >= rn) return;
+    float v = rpart[m];
+    for (int z = 1; z < rsplits; ++z) v += rpart[(long)z * rn + m];
+    rout[m] = racc ? rout[m] + v : v;
+    return;
+  }
   const long i4 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i4 >= n) return;
   floatx4 s = *reinterpret_cast<const floatx4*>(part + i4);
@@ -927,7 +1075,8 @@ int pick_geo(int M, int N, int splits, int req) {
 
 int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, int b_kmajor, void* C, long ldc, int M,
               int N, int K, const void* bias, const void* resid, long ldr, int out_mode, int act, int splits,
-              void* workspace, float alpha, int geo_req, int ring_grid, void* stream);
+              void* workspace, float alpha, int geo_req, int ring_grid, void* stream, float* rsum_out = nullptr,
+              int rsum_acc = 0, bool* rsum_done = nullptr);
 
 }  // namespace
 
@@ -950,9 +1099,12 @@ extern "C" int vpt_gemm_bf16_tiled(const void* A, long lda, int a_kmajor, const 
 }
 
 namespace {
+// rsum_out (wgrad direction, ring geometry only): also rsum_out[m] (+)= sum_k A(m, k) (the bias gradient),
+// from per-split row sums in the workspace behind the split slabs; *rsum_done tells whether it was done.
 int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, int b_kmajor, void* C, long ldc, int M,
               int N, int K, const void* bias, const void* resid, long ldr, int out_mode, int act, int splits,
-              void* workspace, float alpha, int geo_req, int ring_grid, void* stream) {
+              void* workspace, float alpha, int geo_req, int ring_grid, void* stream, float* rsum_out, int rsum_acc,
+              bool* rsum_done) {
   VPT_CHECK_ARG(A && B && C, "vpt_gemm_bf16: null operand");
   VPT_CHECK_ARG(M > 0 && N > 0 && K > 0, "vpt_gemm_bf16: empty shape");
   VPT_CHECK_ARG(N % 4 == 0, "vpt_gemm_bf16: N%4 required");
@@ -998,17 +1150,25 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
     g.out_mode = out_mode;
   }
   const int geo = pick_geo(M, N, splits, geo_req);
+  const bool rs = rsum_out && !a_kmajor && geo == 256 && N % 8 == 0 && workspace != nullptr;
+  if (rsum_done) *rsum_done = rs;
+  float* rpart = nullptr;
+  if (rs) {  // per-split row sums behind the split slabs (16-B aligned)
+    rpart = reinterpret_cast<float*>(workspace) + (splits > 1 ? ((long)splits * M * N + 3) / 4 * 4 : 0);
+    g.rsum = rpart;
+  }
   int rc;
   if (a_kmajor && b_kmajor) rc = launch_geo<true, true>(g, splits, geo, s);
   else if (a_kmajor && !b_kmajor) rc = launch_geo<true, false>(g, splits, geo, s);
   else if (!a_kmajor && b_kmajor) rc = launch_geo<false, true>(g, splits, geo, s);
   else rc = launch_geo<false, false>(g, splits, geo, s);
-  if (rc != VPT_OK || splits == 1) return rc;
-  const long n = (long)M * N;
+  if (rc != VPT_OK || (splits == 1 && !rs)) return rc;
+  const long n = splits > 1 ? (long)M * N : 0;
   const int threads = 256;
-  const long blocks = (n / 4 + threads - 1) / threads;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(threads), 0, s,
-                     (const float*)workspace, n, splits, (long)M * N, C, final_mode);
+  const long cblocks = (n / 4 + threads - 1) / threads;
+  const long rblocks = rs ? (M + threads - 1) / threads : 0;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(cblocks + rblocks), dim3(threads), 0, s, (const float*)workspace, n,
+                     splits, (long)M * N, C, final_mode, cblocks, rpart, splits, M, rsum_out, rsum_acc);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
@@ -1047,6 +1207,38 @@ extern "C" long vpt_gemm_workspace_bytes(int M, int N, int K, int splits) {
   (void)K;
   if (splits <= 1) return 0;
   return (long)splits * M * N * 4;
+}
+
+// ---- nn.Linear weight + bias gradient in one ring GEMM (torch autograd of F.linear; every Linear of
+// denoiser.py, e.g. :318-323 / :492-504) -------------------------------------------------------------
+// dw [N][K] (=|+=) dy^T . x and db [N] (=|+=) column sums of dy [M][N], both f32. On the 256x256 ring the
+// column sums are row sums of the GEMM's mn-major A operand, taken by MFMAs against an all-ones fragment
+// in the items of the first output tile and reduced with the split-K slabs in one launch; otherwise the
+// colsum kernel (vpt_bias_grad) runs after the GEMM on the same workspace.
+extern "C" int vpt_colsum_blocks(long M);
+extern "C" int vpt_bias_grad(const void* in, long ld, long M, int N, float* part, float* out, int accumulate,
+                             void* stream);
+
+extern "C" long vpt_linear_wgrad_workspace_bytes(long M, int N, int K, int splits) {
+  const int s = splits < 1 ? 1 : splits;
+  const long slab = s > 1 ? ((long)s * N * K + 3) / 4 * 4 : 0;
+  const long ring = (slab + (long)s * N) * 4;
+  const long cs = (long)vpt_colsum_blocks(M) * N * 4;
+  return ring > cs ? ring : cs;
+}
+
+extern "C" int vpt_linear_wgrad(const void* dy, long lddy, const void* x, long ldx, float* dw, long lddw, float* db,
+                                long M, int N, int K, int accumulate, int splits, void* workspace, int geometry,
+                                int ring_grid, void* stream) {
+  VPT_CHECK_ARG(dy && x && dw && M > 0 && M < (1L << 31), "vpt_linear_wgrad: bad args");
+  VPT_CHECK_ARG(!db || workspace, "vpt_linear_wgrad: a bias gradient needs the workspace");
+  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256, "vpt_linear_wgrad: geometry 0, 128 or 256");
+  bool done = false;
+  const int rc = gemm_impl(dy, lddy, 0, x, ldx, 0, dw, lddw, N, K, (int)M, nullptr, nullptr, 0,
+                           accumulate ? OUT_F32_ACC : OUT_F32, ACT_NONE, splits, workspace, 1.f, geometry, ring_grid,
+                           stream, db, accumulate, &done);
+  if (rc != VPT_OK || !db || done) return rc;
+  return vpt_bias_grad(dy, lddy, M, N, (float*)workspace, db, accumulate, stream);
 }
 
 // ---- fused SwiGLU GEMMs (the JiT MLP, denoiser.py:480-506; FinalLayer 535-543) ---------------------

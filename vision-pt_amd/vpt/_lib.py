@@ -25,6 +25,8 @@ SIGNATURES: dict[str, list] = {
     "vpt_gemm_bf16": [P, L, I, P, L, I, P, L, I, I, I, P, P, L, I, I, I, P, F, P],
     "vpt_gemm_workspace_bytes": [I, I, I, I],
     "vpt_gemm_bf16_tiled": [P, L, I, P, L, I, P, L, I, I, I, P, P, L, I, I, I, P, F, I, I, P],
+    "vpt_linear_wgrad": [P, L, P, L, P, L, P, L, I, I, I, I, P, I, I, P],
+    "vpt_linear_wgrad_workspace_bytes": [L, I, I, I],
     "vpt_gemm_swiglu_fwd": [P, L, P, L, P, P, L, P, L, I, I, I, P],
     "vpt_gemm_swiglu_bwd_workspace": [I, I, I],
     "vpt_gemm_swiglu_bwd": [P, L, P, L, P, L, P, L, I, I, I, P, P],
@@ -99,6 +101,7 @@ DIAG_SIGNATURES: dict[str, list] = {
 _RESTYPES = {
     "vpt_lora_wgrad_workspace": C.c_long,
     "vpt_gemm_workspace_bytes": C.c_long,
+    "vpt_linear_wgrad_workspace_bytes": C.c_long,
     "vpt_attn_fused_workspace_bytes": C.c_long,
     "vpt_cover_resize_crop_workspace": C.c_long,
     "vpt_gemm_swiglu_bwd_workspace": C.c_long,
@@ -107,7 +110,7 @@ _RESTYPES = {
     "vpt_build_info": C.c_char_p,
 }
 # Entry points that return a value (size / count / string) rather than a status code.
-_VALUE_FNS = {"vpt_lora_wgrad_workspace", "vpt_gemm_workspace_bytes", "vpt_attn_fused_workspace_bytes", "vpt_cover_resize_crop_workspace", "vpt_gemm_swiglu_bwd_workspace", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
+_VALUE_FNS = {"vpt_lora_wgrad_workspace", "vpt_gemm_workspace_bytes", "vpt_linear_wgrad_workspace_bytes", "vpt_attn_fused_workspace_bytes", "vpt_cover_resize_crop_workspace", "vpt_gemm_swiglu_bwd_workspace", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
               "vpt_colsum_blocks", "vpt_attn_q_scale", "vpt_last_error_string", "vpt_abi_version", "vpt_build_info"}
 
 

@@ -255,32 +255,29 @@ class JiTEngine:
         if zero_grads:
             self.grads.zero_()
         acc = not zero_grads
-        ws = pool.get("wgrad_ws", (self._ws_elems(M),), F32)
-        colp = pool.get("colsum_part", (ops.colsum_blocks(max(M, M2)), max(2 * F, 3 * D)), F32)
+        ws = pool.get("wgrad_ws", (self._ws_elems(max(M, M2)),), F32)
         f, g = self.fin, self.g
 
-        def wgrad(dy, xin, out):
+        def wgrad(dy, xin, out, bias=None):
+            """weight gradient, and with `bias` the bias gradient in the same GEMM (vpt_linear_wgrad)"""
             Mr, N = dy.shape
             K = xin.shape[1]
-            s = min(ops.wgrad_splits(N, K, Mr), max(1, ws.numel() // (N * K)))
-            ops.linear_wgrad(dy, xin, out.view(N, K), accumulate=acc, splits=s, workspace=ws)
-
-        def bgrad(dy, out):
-            ops.bias_grad(dy, out.view(-1), part=colp, accumulate=acc)
+            s = ops.wgrad_splits(N, K, Mr)
+            while s > 1 and ops.linear_wgrad_workspace_bytes(Mr, N, K, s) > ws.numel() * 4:
+                s -= 1
+            ops.linear_wgrad(dy, xin, out.view(N, K), accumulate=acc, splits=s, workspace=ws,
+                             bias_out=None if bias is None else bias.view(-1))
 
         # --- final layer
         f3, fh, f12, xnf, xf = (pool.get(n, s) for n, s in (("f3", (M2, D)), ("fh", (M2, F)), ("f12", (M2, 2 * F)),
                                                           ("xnf", (M2, D)), ("xf", (M2, D))))
         rstdf = pool.get("rstdf", (M2,), F32)
-        wgrad(dout, f3, f["gwl"])
-        bgrad(dout, f["gbl"])
+        wgrad(dout, f3, f["gwl"], f["gbl"])
         df3 = ops.linear_dgrad(dout, f["pwl"], out=pool.get("d_a", (M2, D)))
-        wgrad(df3, fh, f["gw3"])
-        bgrad(df3, f["gb3"])
+        wgrad(df3, fh, f["gw3"], f["gb3"])
         df12 = ops.linear_dgrad_swiglu(df3, f["pw3"], f12, pool.get("d_x12", (M2, 2 * F)),
                                        workspace=pool.get("d_h", (M2, F)))
-        wgrad(df12, xnf, f["gw12"])
-        bgrad(df12, f["gb12"])
+        wgrad(df12, xnf, f["gw12"], f["gb12"])
         dxnf = ops.linear_dgrad(df12, f["pw12"], out=pool.get("d_b", (M2, D)))
         dxf, part = ops.rmsnorm_bwd(dxnf, xf, rstdf, f["pn"], dx=pool.get("d_c", (M2, D)),
                                     dw_part=pool.get("rms_part", (ops.rmsnorm_bwd_blocks(max(M, M2)), D), F32))
@@ -316,19 +313,16 @@ class JiTEngine:
                 dqk.zero_()
                 pre_zeroed = True
             # MLP
-            wgrad(dx, h, w["gw3"])
-            bgrad(dx, w["gb3"])
+            wgrad(dx, h, w["gw3"], w["gb3"])
             dx12 = ops.linear_dgrad_swiglu(dx, w["pw3"], x12, pool.get("d_x12", (M, 2 * F)),
                                            workspace=pool.get("d_h", (M, F)))
-            wgrad(dx12, xn2, w["gw12"])
-            bgrad(dx12, w["gb12"])
+            wgrad(dx12, xn2, w["gw12"], w["gb12"])
             dxn2 = ops.linear_dgrad(dx12, w["pw12"], out=pool.get("d_b", (M, D)))
             dxm, part = ops.rmsnorm_bwd(dxn2, xm, rstd2, w["pn2"], dres=dx, dx=pool.get("dx_b", (M, D)),
                                         dw_part=pool.get("rms_part", (ops.rmsnorm_bwd_blocks(max(M, M2)), D), F32))
             ops.reduce_rows(part[:ops.rmsnorm_bwd_blocks(M)], w["gn2"], acc)
             # attention
-            wgrad(dxm, o, w["gwo"])
-            bgrad(dxm, w["gbo"])
+            wgrad(dxm, o, w["gwo"], w["gbo"])
             do = ops.linear_dgrad(dxm, w["pwo"], out=pool.get("d_o", (M, D)))
             ops.attn_bwd(ops._t4(qk, B, rows, Hh, 0), ops._t4(qk, B, rows, Hh, D), ops._t4(qkv, B, rows, Hh, 2 * D),
                          ops._t4(o, B, rows, Hh, 0), ops._t4(do, B, rows, Hh, 0), lse, delta, st["kbias"],
@@ -337,8 +331,7 @@ class JiTEngine:
             qpart = ops.qknorm_rope_bwd(dqk, qkv, w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, rows, dqkv,
                                         dw_part=pool.get("qk_part", (ops.qknorm_rope_blocks(M), 128), F32))
             ops.reduce_rows(qpart[:ops.qknorm_rope_blocks(M)], w["gqk_norm"], acc)
-            wgrad(dqkv, xn1, w["gwqkv"])
-            bgrad(dqkv, w["gbqkv"])
+            wgrad(dqkv, xn1, w["gwqkv"], w["gbqkv"])
             dxn1 = ops.linear_dgrad(dqkv, w["pwqkv"], out=pool.get("d_b", (M, D)))
             dx_new, part = ops.rmsnorm_bwd(dxn1, x_in, rstd1, w["pn1"], dres=dxm, dx=pool.get("dx_a", (M, D)),
                                            dw_part=pool.get("rms_part", (ops.rmsnorm_bwd_blocks(max(M, M2)), D), F32))
@@ -357,25 +350,21 @@ class JiTEngine:
             self.g["time_position_embeds"].add_(pool.get("dtpe_tmp", (self.T, D), F32))
         bd = cfg.bottleneck_dim
         pe1 = pool.get("pe1", (M2, bd))
-        wgrad(dpe2, pe1, g["patch_embedder.proj_2.weight"])
-        bgrad(dpe2, g["patch_embedder.proj_2.bias"])
+        wgrad(dpe2, pe1, g["patch_embedder.proj_2.weight"], g["patch_embedder.proj_2.bias"])
         dpe1 = ops.linear_dgrad(dpe2, self.p["patch_embedder.proj_2.weight"].view(D, bd), out=pool.get("d_pe1", (M2, bd)))
         wgrad(dpe1, st["zp"], g["patch_embedder.proj_1.weight"])
         for pre, rowsn, dy in (("time_embedder", B, dtime), ("image_size_embedder", 6 * B, dsize)):
             k = "t" if pre == "time_embedder" else "s"
             a1, h1 = pool.get(k + "_a1", (rowsn, D)), pool.get(k + "_h1", (rowsn, D))
             emb_in = pool.get(("temb_in" if k == "t" else "semb_in"), (rowsn, 256))
-            wgrad(dy, h1, g[pre + ".mlp.2.weight"])
-            bgrad(dy, g[pre + ".mlp.2.bias"])
+            wgrad(dy, h1, g[pre + ".mlp.2.weight"], g[pre + ".mlp.2.bias"])
             dh1 = ops.linear_dgrad(dy, self.p[pre + ".mlp.2.weight"], out=pool.get("d_h1", (rowsn, D)))
             da1 = ops.silu_bwd(dh1, a1, pool.get("d_a1", (rowsn, D)))
-            wgrad(da1, emb_in, g[pre + ".mlp.0.weight"])
-            bgrad(da1, g[pre + ".mlp.0.bias"])
+            wgrad(da1, emb_in, g[pre + ".mlp.0.weight"], g[pre + ".mlp.0.bias"])
         dctx_raw = None
         if n_ctx:
             dctx_b = ops.cast_f32_bf16(dctx, pool.get("dctx_bf16", (B * n_ctx, D)))
-            wgrad(dctx_b, st["ctx_raw"], g["context_embedder.weight"])
-            bgrad(dctx_b, g["context_embedder.bias"])
+            wgrad(dctx_b, st["ctx_raw"], g["context_embedder.weight"], g["context_embedder.bias"])
             dctx_raw = ops.linear_dgrad(dctx_b, self.p["context_embedder.weight"],
                                         out=pool.get("d_ctx_raw", (B * n_ctx, cfg.context_dim)))
         return dctx_raw
@@ -386,10 +375,11 @@ class JiTEngine:
         return self.g["time_position_embeds"]
 
     def _ws_elems(self, M: int) -> int:
+        """f32 elements of the wgrad workspace: the largest split-K slab set + per-split bias sums (or the
+        colsum partials of the non-ring fallback) over the engine's weight-gradient shapes."""
         D, F = self.D, self.F
         best = 1
-        for N, K in ((D, F), (2 * F, D), (3 * D, D), (D, D)):
+        for N, K in ((D, F), (2 * F, D), (3 * D, D), (D, D), (self.fin["pwl"].shape[0], D)):
             s = ops.wgrad_splits(N, K, M)
-            if s > 1:
-                best = max(best, s * N * K)
+            best = max(best, ops.linear_wgrad_workspace_bytes(M, N, K, s) // 4 + 1)
         return best

@@ -137,12 +137,36 @@ def linear_dgrad(dy, w, out=None, resid=None, **tile):
     return gemm(dy, True, w, False, M, K, N, out, resid=resid, **tile)
 
 
-def linear_wgrad(dy, x, out, accumulate=False, splits=1, workspace=None, **tile):
-    """dW (=|+=) dy.T @ x in f32 (dy [M,N], x [M,K], out [N,K]) — nn.Linear weight gradient."""
+def linear_wgrad_workspace_bytes(M: int, N: int, K: int, splits: int) -> int:
+    return int(call("vpt_linear_wgrad_workspace_bytes", M, N, K, splits))
+
+
+def linear_wgrad(dy, x, out, accumulate=False, splits=1, workspace=None, bias_out=None, geometry=0, ring_grid=0):
+    """dW (=|+=) dy.T @ x in f32 (dy [M,N], x [M,K], out [N,K]) — nn.Linear weight gradient — and, with
+    bias_out [N] f32, the bias gradient (=|+=) column sums of dy in the same ring GEMM (vpt_linear_wgrad)."""
     M, N = dy.shape
     K = x.shape[1]
-    return gemm(dy, False, x, False, N, K, M, out, out_mode=OUT_F32_ACC if accumulate else OUT_F32,
-                splits=splits, workspace=workspace, **tile)
+    _chk(dy, BF16, "dy")
+    _chk(x, BF16, "x")
+    _chk(out, F32, "out")
+    if bias_out is not None:
+        _chk(bias_out, F32, "bias_out")
+        if not bias_out.is_contiguous() or bias_out.numel() != N:
+            raise ValueError("bias_out must be a contiguous [N] f32 tensor")
+    need = linear_wgrad_workspace_bytes(M, N, K, splits)
+    if workspace is None or workspace.numel() * workspace.element_size() < need:
+        workspace = torch.empty((need + 3) // 4, dtype=F32, device=dy.device)
+
+    def run():
+        call("vpt_linear_wgrad", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(), out.stride(0),
+             _p(bias_out), M, N, K, int(accumulate), splits, workspace.data_ptr(), int(geometry), int(ring_grid),
+             stream())
+    pr = PROBES.get("gemm")
+    if pr is None:
+        run()
+    else:
+        pr.record(2.0 * M * N * K, run, key=f"wgrad M{N} N{K} K{M} s{splits}{' +b' if bias_out is not None else ''}")
+    return out
 
 
 def linear_swiglu(x, w12, b12, x12, h):
