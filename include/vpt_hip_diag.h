@@ -25,6 +25,8 @@ int vpt_gemm_set_geometry(int geo);
 int vpt_gemm_set_debug(unsigned long long* buf);
 /* Persistent ring grid override (0 = per-call / default). */
 int vpt_gemm_set_ring_grid(int blocks);
+/* Ring epilogue stagger in 10-ns ticks: half the blocks start that much later (0 = off, production). */
+int vpt_gemm_set_stagger(int ticks);
 /* Forward lazy-rescale threshold in log2 units (default 8; 0 = rescale whenever the row max grows). */
 int vpt_attn_set_rescale_threshold(float tau);
 /* Attention kernel variant: 0 = production (split dK/dV + dQ kernels); 13 = fused single-pass backward

@@ -187,8 +187,11 @@ def test_swiglu_fused_epilogues_match_unfused(ops, M):
     assert torch.equal(x12, x12_u)
     assert torch.equal(h, h_u)
     x12f = x12.float()
+    # torch's bf16 silu (libm expf + IEEE division in f32) vs the kernels' v_exp_f32 + v_rcp_f32 sigmoid: at
+    # most one bf16 ulp apart (csrc/common.h sigmoid_hw), and equal almost everywhere
     h_ref = (torch.nn.functional.silu(x12f[:, :F]).bfloat16().float() * x12f[:, F:]).bfloat16()
-    assert torch.equal(h, h_ref)
+    assert ((h.float() - h_ref.float()).abs() <= h_ref.float().abs() * 2 ** -7 + 1e-30).all()
+    assert (h != h_ref).float().mean().item() < 0.02
     # backward
     dy = rnd(M, D, seed=133)
     w3 = rnd(D, F, scale=0.03, seed=134)

@@ -40,6 +40,33 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
+// Logistic sigmoid on the hardware transcendental units: rcp(1 + 2^(-x log2 e)) = v_exp_f32 + v_rcp_f32
+// (~1 ulp each), instead of libm expf + IEEE division (~30 instructions). Used by the SwiGLU forward and
+// backward (fused GEMM epilogues and the elementwise kernels alike, so the two paths stay bit-identical);
+// against torch's bf16 silu (expf + division in f32) the bf16 results differ by at most one bf16 ulp.
+// Limits: x -> -inf gives 2^inf = inf, rcp(inf) = 0; x -> +inf gives rcp(1) = 1; NaN propagates.
+__device__ __forceinline__ float sigmoid_hw(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
+}
+
+// SwiGLU element math shared by the fused GEMM epilogues (gemm.hip) and the elementwise kernels (misc.hip),
+// with FP contraction off so both compile to the same operations (the two paths are tested bit-identical).
+// Forward: h = bf16(bf16(silu(x1)) * x2) (the reference's silu(x1) * x2 on bf16 tensors, denoiser.py:480-506).
+__device__ __forceinline__ float swiglu_fwd1(float x1, float x2) {
+#pragma clang fp contract(off)
+  const float s = x1 * sigmoid_hw(x1);
+  return bf2f(f2bf(s)) * x2;
+}
+// Backward of one element: dh (bf16 value) -> dx1 = bf16(dh * x2) * silu'(x1), dx2 = dh * bf16(silu(x1)).
+__device__ __forceinline__ void swiglu_bwd1(float gd, float a, float b, float& d1, float& d2) {
+#pragma clang fp contract(off)
+  const float sg = sigmoid_hw(a);
+  const float sv = bf2f(f2bf(a * sg));
+  const float ds = bf2f(f2bf(gd * b));
+  d2 = gd * sv;
+  d1 = ds * (sg * (1.f + a * (1.f - sg)));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

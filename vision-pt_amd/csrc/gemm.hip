@@ -53,6 +53,9 @@ struct GemmArgs {
   // row sums of A over this item's K slice (wgrad direction: the bias gradient sum_t dY[t][m]), f32 at
   // rsum[split * M + m]; ring kernel (RS instantiation) only
   float* rsum;
+  // ring kernel: start delay (s_memrealtime ticks, 10 ns) of the blocks with bit 3 of blockIdx set, so
+  // that half the CUs reach their (HBM-bound) epilogues while the other half run K loops (0 = off)
+  int stagger;
 };
 
 // ---- LDS images -----------------------------------------------------------------------------
@@ -626,9 +629,19 @@ __device__ __forceinline__ int ring_stores(const GemmArgs& g) {
   if (g.sw == 2) return 32;  // dx1, dx2 per lane, fragment and half
   return g.out_mode == OUT_BF16 ? 16 : 32;
 }
-__device__ __forceinline__ float silu_ref(float x) { return x / (1.f + expf(-x)); }
 __device__ __forceinline__ int stg_off(int row, int col) {
   return row * 256 + (((col >> 2) ^ (row & 1)) << 4) + ((col & 3) << 2);
+}
+
+// A 16-B buffer store whose data registers the next instruction may not overwrite: the store reads them
+// after issue, and hipcc (ROCm 7.2, gfx950) emitted the SwiGLU-backward epilogue's first store followed
+// directly by a VALU write of its data registers, with no wait state -- the stored dwords came out corrupted.
+// The scheduling barrier pins the pad right behind the store (tools/isa_store_hazard.py checks the .s).
+__device__ __forceinline__ void store_b128_padded(u32x4 v, __amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 0);
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 1");
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 template <int EPI, int I0, int I1>
@@ -666,18 +679,10 @@ __device__ __forceinline__ void epilogue_ring(const GemmArgs& g, const floatx4 (
         unpack8(make_uint4(a4[0], a4[1], a4[2], a4[3]), a);
         unpack8(make_uint4(b4[0], b4[1], b4[2], b4[3]), b);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const float gd = bf2f(f2bf(o[q]));  // dh is a bf16 tensor in the reference
-          const float sg = 1.f / (1.f + expf(-a[q]));
-          const float sv = bf2f(f2bf(a[q] * sg));
-          const float ds = bf2f(f2bf(gd * b[q]));
-          d2[q] = gd * sv;
-          d1[q] = ds * (sg * (1.f + a[q] * (1.f - sg)));
-        }
+        for (int q = 0; q < 8; ++q) swiglu_bwd1(bf2f(f2bf(o[q])), a[q], b[q], d1[q], d2[q]);  // dh: a bf16 tensor
         const uint4 w1 = pack8(d1), w2 = pack8(d2);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{w1.x, w1.y, w1.z, w1.w}, e.rs, (int)e.voff, soff, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{w2.x, w2.y, w2.z, w2.w}, e.rs,
-                                               (int)(e.col_ok ? e.voff + g.N * 2 : e.voff), soff, 0);
+        store_b128_padded(u32x4{w1.x, w1.y, w1.z, w1.w}, e.rs, (int)e.voff, soff);
+        store_b128_padded(u32x4{w2.x, w2.y, w2.z, w2.w}, e.rs, (int)(e.col_ok ? e.voff + g.N * 2 : e.voff), soff);
       } else if (g.out_mode == OUT_BF16) {
         if (EPI == EPI_RESID) {
           // reference semantics: residual + bf16(linear output), rounded again to bf16. Out-of-range rows /
@@ -746,7 +751,7 @@ __device__ __forceinline__ void epilogue_ring_swf(const GemmArgs& g, const float
     for (int e = 0; e < 8; ++e) {
       x1[e] = bf2f(f2bf(x1[e] * g.alpha + b1[e]));
       x2[e] = bf2f(f2bf(x2[e] * g.alpha + b2[e]));
-      hv[e] = bf2f(f2bf(silu_ref(x1[e]))) * x2[e];
+      hv[e] = swiglu_fwd1(x1[e], x2[e]);
     }
     const int soff = i * 16 * (int)g.ldc * 2, soffh = i * 16 * (int)g.ldc2 * 2;
     const uint4 w1 = pack8(x1), w2 = pack8(x2), wh = pack8(hv);
@@ -796,6 +801,15 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
   ring_issue<AK, BK_, SW>(g, it, 0, lds0, wid, lane);
   if (it.nk > 1) ring_issue<AK, BK_, SW>(g, it, 1, lds0, wid, lane);
   if (it.nk > 2) ring_issue<AK, BK_, SW>(g, it, 2, lds0, wid, lane);
+  // Epilogue de-synchronisation: with every block on the same item length all 256 CUs reach their store
+  // (and residual / x12 load) bursts together, which then run at the chip's HBM rate while no MFMA works.
+  // Delaying half the blocks by about half an epilogue (wave-uniform spin on the 100 MHz real-time
+  // counter, the first tiles already in flight) makes the two halves alternate: one half's epilogue
+  // traffic overlaps the other half's K loop.
+  if (g.stagger > 0 && ((blockIdx.x >> 3) & 1)) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)g.stagger) __builtin_amdgcn_s_sleep(2);
+  }
   int pend = 0;  // epilogue stores younger than this item's pre-issued tiles 0-2 (0 on the first item)
   int kth = 0;   // items done by this block (TL stamps)
 
@@ -979,6 +993,21 @@ int launch(const GemmArgs& g, int splits, hipStream_t s) {
   return VPT_OK;
 }
 
+// Epilogue stagger (GemmArgs::stagger, 10-ns ticks; diagnostic build only). Measured at the JiT-B/16 B=8
+// shapes with 200-1500 ticks (profiles/r02/r02q_gemm_stagger_ab.json): no gain on any shape, larger delays
+// only add their own length, i.e. the epilogues are not a chip-wide synchronized HBM burst. Off in
+// production.
+#ifdef VPT_DIAG
+int g_stagger_override = 0;  // vpt_gemm_set_stagger
+#endif
+inline int ring_stagger() {
+#ifdef VPT_DIAG
+  return g_stagger_override;
+#else
+  return 0;
+#endif
+}
+
 template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false, bool STAMP = false, bool TL = false, int SW = 0>
 int launch_ring(const GemmArgs& g, int splits, hipStream_t s) {
   constexpr int LDS = RSTAGES * 2 * 256 * RBK * 2;  // the epilogue stages through ring stage 3
@@ -986,25 +1015,28 @@ int launch_ring(const GemmArgs& g, int splits, hipStream_t s) {
   const int rg = g.ring_grid > 0 ? g.ring_grid : kRingGrid;
   const int grid = items < rg ? items : rg;
   const int epi = SW ? EPI_PLAIN : epi_mode(g);
+  GemmArgs ga = g;
+  ga.stagger = ring_stagger();
+  const GemmArgs& gl = ga;
   if (!AK && !SW && g.rsum) {  // fused bias gradient (wgrad direction)
     if (epi == EPI_ACC)
       hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, 0, EPI_ACC, true>), dim3(grid), dim3(512), LDS,
-                         s, g);
+                         s, gl);
     else
       hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, 0, EPI_PLAIN, true>), dim3(grid), dim3(512),
-                         LDS, s, g);
+                         LDS, s, gl);
   } else if (epi == EPI_RESID)
     hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, SW, SW ? 0 : EPI_RESID>), dim3(grid), dim3(512),
-                       LDS, s, g);
+                       LDS, s, gl);
   else if (epi == EPI_SWB)
     hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, SW, SW ? 0 : EPI_SWB>), dim3(grid), dim3(512),
-                       LDS, s, g);
+                       LDS, s, gl);
   else if (epi == EPI_ACC)
     hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, SW, SW ? 0 : EPI_ACC>), dim3(grid), dim3(512),
-                       LDS, s, g);
+                       LDS, s, gl);
   else
     hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, SW, EPI_PLAIN>), dim3(grid), dim3(512), LDS, s,
-                       g);
+                       gl);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
@@ -1187,6 +1219,12 @@ extern "C" int vpt_gemm_set_geometry(int geo) {
 extern "C" int vpt_gemm_set_ring_grid(int blocks) {
   VPT_CHECK_ARG(blocks >= 0 && blocks <= 65536, "vpt_gemm_set_ring_grid: 0..65536");
   g_ring_grid_override = blocks;
+  return VPT_OK;
+}
+
+// Ring epilogue stagger in 10-ns ticks (0 = off, the production setting).
+extern "C" int vpt_gemm_set_stagger(int ticks) {
+  g_stagger_override = ticks;
   return VPT_OK;
 }
 

@@ -328,7 +328,7 @@ __global__ void swiglu_fwd_kernel(const bf16_t* __restrict__ x12, long M, int F,
   unpack8(*reinterpret_cast<const uint4*>(x12 + row * 2 * F + ch * 8), a);
   unpack8(*reinterpret_cast<const uint4*>(x12 + row * 2 * F + F + ch * 8), b);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) o[e] = bf2f(f2bf(silu_f(a[e]))) * b[e];
+  for (int e = 0; e < 8; ++e) o[e] = swiglu_fwd1(a[e], b[e]);
   *reinterpret_cast<uint4*>(h + row * F + ch * 8) = pack8(o);
 }
 
@@ -344,13 +344,7 @@ __global__ void swiglu_bwd_kernel(const bf16_t* __restrict__ dh, const bf16_t* _
   unpack8(*reinterpret_cast<const uint4*>(x12 + row * 2 * F + F + ch * 8), b);
   unpack8(*reinterpret_cast<const uint4*>(dh + row * F + ch * 8), g);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float sg = 1.f / (1.f + expf(-a[e]));
-    const float s = bf2f(f2bf(a[e] * sg));
-    const float ds = bf2f(f2bf(g[e] * b[e]));
-    d2[e] = g[e] * s;
-    d1[e] = ds * (sg * (1.f + a[e] * (1.f - sg)));
-  }
+  for (int e = 0; e < 8; ++e) swiglu_bwd1(g[e], a[e], b[e], d1[e], d2[e]);
   *reinterpret_cast<uint4*>(dx12 + row * 2 * F + ch * 8) = pack8(d1);
   *reinterpret_cast<uint4*>(dx12 + row * 2 * F + F + ch * 8) = pack8(d2);
 }

@@ -21,6 +21,9 @@ LIB_DIAG = PKG_ROOT / "lib" / "libvpt_hip_diag.so"
 ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+# Per-unit extra flags. gemm.hip: no SLP packing of the epilogues' f32 math into v_pk_*_f32 (packed f32 ops
+# beside MFMAs cost issue cycles: guide, 'price of one filler beside MFMAs').
+UNIT_FLAGS = {"gemm.hip": ["-fno-slp-vectorize"]}
 
 
 def _needs(obj: Path, deps: list[Path]) -> bool:
@@ -34,7 +37,8 @@ def _compile(src: Path, diag: bool = False) -> Path:
     obj = (BUILD_DIAG if diag else BUILD) / (src.stem + ".o")
     deps = [src] + sorted(CSRC.glob("*.h"))
     if _needs(obj, deps):
-        cmd = [HIPCC, *CFLAGS, *(["-DVPT_DIAG"] if diag else []), "-c", str(src), "-o", str(obj)]
+        cmd = [HIPCC, *CFLAGS, *UNIT_FLAGS.get(src.name, []), *(["-DVPT_DIAG"] if diag else []), "-c", str(src), "-o",
+               str(obj)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr[-4000:]}")

@@ -89,6 +89,7 @@ SIGNATURES: dict[str, list] = {
 # when VPT_DIAG=1 (tools/), never by the product path.
 DIAG_SIGNATURES: dict[str, list] = {
     "vpt_gemm_set_geometry": [I],
+    "vpt_gemm_set_stagger": [I],
     "vpt_gemm_set_debug": [P],
     "vpt_gemm_set_ring_grid": [I],
     "vpt_attn_set_rescale_threshold": [F],
