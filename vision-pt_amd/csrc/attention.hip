@@ -354,13 +354,12 @@ __global__ void attn_bwd_pre_kernel(AttnArgs g, int H, long rows_total) {
 // ------------------------------------------------------------------ backward dK, dV
 // ABL (timing-only ablations, wrong results): 1 = no next-tile staging (global -> regs -> LDS) in
 // the loop, 2 = transposed fragment reads replaced by row reads.
+// Body of one dK/dV block (key block bx of head hd, batch b); lds = [buf][Q / dO] tiles, lstat = [buf][lse / delta].
 template <int ABL, int NW>
-__global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
-  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];     // [buf][Q / dO]
-  __shared__ __attribute__((aligned(16))) float lstat[2][2][64];     // [buf][lse / delta]
+__device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int b, char (&lds)[2][2][8192],
+                                          float (&lstat)[2][2][64]) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
-  const int b = blockIdx.z, hd = blockIdx.y;
-  const int k0 = blockIdx.x * (32 * NW) + wid * 32;
+  const int k0 = bx * (32 * NW) + wid * 32;
   const bf16_t* Q = g.q.p + b * g.q.sb + hd * g.q.sh;
   const bf16_t* dO = g.dO.p + b * g.dO.sb + hd * g.dO.sh;
   const float* LSE = g.lse + b * g.l_sb + hd * g.l_sh;
@@ -516,14 +515,19 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
   store_T(g.dk, (long)b * g.dk.sb + hd * g.dk.sh, dkT, 0.69314718055994531f, key, g.nk, lane, kmasked);
 }
 
-// ------------------------------------------------------------------ backward dQ
 template <int ABL, int NW>
-__global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dq_kernel(AttnArgs g) {
-  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];  // [buf][K / V]
-  extern __shared__ __attribute__((aligned(16))) float kbl[];   // key bias of keys kb0.. (fill_key_bias)
+__global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];     // [buf][Q / dO]
+  __shared__ __attribute__((aligned(16))) float lstat[2][2][64];     // [buf][lse / delta]
+  dkdv_body<ABL, NW>(g, blockIdx.x, blockIdx.y, blockIdx.z, lds, lstat);
+}
+
+// ------------------------------------------------------------------ backward dQ
+// Body of one dQ block (query block bx of head hd, batch b); lds = [buf][K / V] tiles, kbl = key bias of keys kb0..
+template <int ABL, int NW>
+__device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b, char (&lds)[2][2][8192], float* kbl) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
-  const int b = blockIdx.z, hd = blockIdx.y;
-  const int q0 = blockIdx.x * (32 * NW) + wid * 32;
+  const int q0 = bx * (32 * NW) + wid * 32;
   const int qrow = q0 + (lane & 31);
   const bf16_t* K = g.k.p + b * g.k.sb + hd * g.k.sh;
   const bf16_t* V = g.v.p + b * g.v.sb + hd * g.v.sh;
@@ -595,6 +599,33 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dq_kernel(AttnArgs g) {
     if (ABL != 1) cur ^= 1;
   }
   store_T(g.dq, (long)b * g.dq.sb + hd * g.dq.sh, dqT, g.scale, qrow, g.n, lane, false);
+}
+
+template <int ABL, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dq_kernel(AttnArgs g) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];  // [buf][K / V]
+  extern __shared__ __attribute__((aligned(16))) float kbl[];   // key bias of keys kb0.. (fill_key_bias)
+  dq_body<ABL, NW>(g, blockIdx.x, blockIdx.y, blockIdx.z, lds, kbl);
+}
+
+// The production backward as ONE launch over both block kinds: the dK/dV blocks first (the longer ones),
+// then the dQ blocks. Each kind alone is 3,168 equal blocks at B=8 1024^2 on 512 block slots (2 per CU):
+// 6.19 waves of work run as 7, twice. In one grid the dQ blocks start on the slots the dK/dV tail frees,
+// so the pair runs in ~(work of both) / slots instead of two rounded-up launches.
+__global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs g, int nkb, int nqb, int B) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];
+  __shared__ __attribute__((aligned(16))) float lstat[2][2][64];
+  extern __shared__ __attribute__((aligned(16))) float kbl[];
+  const int nk_blocks = nkb * g.H * B;
+  int bid = blockIdx.x;
+  if (bid < nk_blocks) {
+    const int bx = bid % nkb, r = bid / nkb;
+    dkdv_body<8, 4>(g, bx, r % g.H, r / g.H, lds, lstat);
+  } else {
+    bid -= nk_blocks;
+    const int bx = bid % nqb, r = bid / nqb;
+    dq_body<0, 4>(g, bx, r % g.H, r / g.H, lds, kbl);
+  }
 }
 
 #ifdef VPT_DIAG
@@ -1201,7 +1232,8 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
     return VPT_OK;
   }
 #endif
-  // production: the split dK/dV pass (explicitly ordered body) + the dQ pass. The fused single pass
+  // production: the split dK/dV pass (explicitly ordered body) + the dQ pass, launched as one grid
+  // (attn_bwd_kernel: dK/dV blocks, then dQ blocks). The fused single pass
   // (attn_bwd_fused_kernel, diagnostic variant 13) does 5 products instead of 7 but its f32 dQ atomics
   // run at the chip-wide atomic rate (~1.3 TB/s: 3.4 GB per launch at B=8 1024^2, 128-key blocks):
   // measured 2.66 ms vs 1.55 ms for this pair (1.14 ms with the atomics removed).
@@ -1224,9 +1256,8 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
     return VPT_OK;
   }
 #endif
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<8, 4>), dim3((nk + 127) / 128, H, B), dim3(256), 0, s, g);
-  VPT_LAUNCH_CHECK();
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 4>), dim3((n + 127) / 128, H, B), dim3(256), key_bias_lds_bytes(g), s, g);
+  const int nkb = (nk + 127) / 128, nqb = (n + 127) / 128;
+  hipLaunchKernelGGL(attn_bwd_kernel, dim3((nkb + nqb) * H * B), dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
