@@ -21,7 +21,8 @@ import sys
 OPS = {
     "gemm": (("gemm_ring_kernel", "gemm_bf16_kernel", "splitk_reduce_kernel"), ("gemm_ring_kernel", "gemm_bf16_kernel")),
     "attn_fwd": (("attn_fwd_kernel",), ("attn_fwd_kernel",)),
-    "attn_bwd": (("attn_bwd_pre_kernel", "attn_bwd_dkdv_kernel", "attn_bwd_dq_kernel"), ("attn_bwd_dkdv_kernel",)),
+    "attn_bwd": (("attn_bwd_pre_kernel", "attn_bwd_kernel", "attn_bwd_dkdv_kernel", "attn_bwd_dq_kernel"),
+                 ("attn_bwd_kernel", "attn_bwd_dkdv_kernel")),
 }
 
 
