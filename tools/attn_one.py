@@ -18,6 +18,7 @@ from vpt import ops  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--time", action="store_true", help="print median ms per forward / backward launch (JSON)")
     args = ap.parse_args()
     dev = "cuda"
     B, H, n = 8, 12, 4170
@@ -37,12 +38,31 @@ def main():
     dv = torch.empty(B * rows, D, dtype=torch.bfloat16, device=dev)
     q4, k4, v4 = (ops._t4(qkv, B, rows, H, c) for c in (0, D, 2 * D))
     o4 = ops._t4(o, B, rows, H)
+    fwd = lambda: ops.attn_fwd(q4, k4, v4, o4, lse, kb, B, H, rows, n, n_dense)  # noqa: E731
+    bwd = lambda: ops.attn_bwd(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, kb,  # noqa: E731
+                               ops._t4(dqk, B, rows, H, 0), ops._t4(dqk, B, rows, H, D), ops._t4(dv, B, rows, H),
+                               B, H, rows, n, n_dense)
+    if not args.time:
+        for _ in range(args.iters):
+            fwd()
+            bwd()
+        torch.cuda.synchronize()
+        print("ok")
+        return
+    import json
+    import statistics
+    res = {"fwd": [], "bwd": []}
     for _ in range(args.iters):
-        ops.attn_fwd(q4, k4, v4, o4, lse, kb, B, H, rows, n, n_dense)
-        ops.attn_bwd(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, kb, ops._t4(dqk, B, rows, H, 0),
-                     ops._t4(dqk, B, rows, H, D), ops._t4(dv, B, rows, H), B, H, rows, n, n_dense)
-    torch.cuda.synchronize()
-    print("ok")
+        for k, fn in (("fwd", fwd), ("bwd", bwd)):
+            fn()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(10):
+                fn()
+            e.record()
+            torch.cuda.synchronize()
+            res[k].append(s.elapsed_time(e) / 10)
+    print(json.dumps({k: round(statistics.median(v), 4) for k, v in res.items()}))
 
 
 if __name__ == "__main__":

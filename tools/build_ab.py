@@ -1,0 +1,41 @@
+"""Builds libvpt_hip.so from csrc/ at another git revision into vision-pt_amd/lib/ab/<name>.so, for same-box
+A/B timing (VPT_LIB_AB=<path> makes vpt load it instead of the production library).
+
+  python tools/build_ab.py REV NAME [--diag]
+"""
+import os
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "vision-pt_amd"))
+from vpt import _build  # noqa: E402
+
+
+def main():
+    rev, name = sys.argv[1], sys.argv[2]
+    diag = "--diag" in sys.argv
+    out = ROOT / "vision-pt_amd" / "lib" / "ab" / f"{name}.so"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    with tempfile.TemporaryDirectory() as td:
+        td = Path(td)
+        files = subprocess.run(["git", "-C", str(ROOT), "ls-tree", "--name-only", rev, "vision-pt_amd/csrc/"],
+                               capture_output=True, text=True, check=True).stdout.split()
+        for f in files:
+            data = subprocess.run(["git", "-C", str(ROOT), "show", f"{rev}:{f}"], capture_output=True, check=True).stdout
+            (td / Path(f).name).write_bytes(data)
+        objs = []
+        for src in sorted(td.glob("*.hip")):
+            obj = td / (src.stem + ".o")
+            cmd = [_build.HIPCC, *_build.CFLAGS, *_build.UNIT_FLAGS.get(src.name, []), *(["-DVPT_DIAG"] if diag else []),
+                   "-c", str(src), "-o", str(obj)]
+            subprocess.run(cmd, check=True)
+            objs.append(str(obj))
+        subprocess.run([_build.HIPCC, "-shared", "-fPIC", f"--offload-arch={_build.ARCH}", *objs, "-o", str(out)], check=True)
+    print(out)
+
+
+if __name__ == "__main__":
+    main()

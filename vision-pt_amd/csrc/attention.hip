@@ -113,6 +113,45 @@ __device__ __forceinline__ void dma_rows(char* lds, const void* head, long sr, i
     dma_x4(head, (uint32_t)(((long)r * sr + c * 8) * 2), lds_addr(lds + q * 1024));
   }
 }
+// dma_rows with the LDS tile given as a byte address (lds_tile, wave-uniform) and a fast path for full
+// tiles (r0 + 64 <= n): the row advance goes into the scalar base (head + r0 rows) and the per-lane offsets
+// (row * sr + chunk) * 2 come precomputed from a RowPlan (loop-invariant registers), so no clamp, 64-bit
+// multiply, generic-to-LDS conversion or readfirstlane is issued per piece; only the last, partial tile takes
+// the clamped path.
+template <int NW>
+struct RowPlan {
+  uint32_t voff[8 / NW];
+  uint32_t wq;  // this wave's first piece within a tile image (bytes)
+};
+template <int NW>
+__device__ __forceinline__ RowPlan<NW> row_plan(long sr, int wid, int lane) {
+  RowPlan<NW> p;
+#pragma unroll
+  for (int i = 0; i < 8 / NW; ++i) {
+    const int q = (8 / NW) * wid + i, row = 8 * q + (lane >> 3);
+    const int c = (lane & 7) ^ sigma(row);
+    p.voff[i] = (uint32_t)((row * (int)sr + c * 8) * 2);
+  }
+  p.wq = __builtin_amdgcn_readfirstlane((uint32_t)((8 / NW) * wid * 1024));
+  return p;
+}
+template <int NW>
+__device__ __forceinline__ void dma_rows_at(uint32_t lds_tile, const void* head, long sr, int r0, int n,
+                                            const RowPlan<NW>& p, int wid, int lane) {
+  if (r0 + 64 <= n) {
+    const void* base = (const char*)head + (long)r0 * sr * 2;
+#pragma unroll
+    for (int i = 0; i < 8 / NW; ++i) dma_x4(base, p.voff[i], lds_tile + p.wq + i * 1024);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8 / NW; ++i) {
+      const int q = (8 / NW) * wid + i, row = 8 * q + (lane >> 3);
+      const int c = (lane & 7) ^ sigma(row);
+      const int r = min(r0 + row, n - 1);
+      dma_x4(head, (uint32_t)(((long)r * sr + c * 8) * 2), lds_tile + p.wq + i * 1024);
+    }
+  }
+}
 // 64 f32 statistics (rows r0..r0+63, clamped to n-1) -> lds, one 256-B piece.
 __device__ __forceinline__ void dma_stat(float* lds, const void* head, int r0, int n, int lane) {
   dma_x1(head, (uint32_t)(min(r0 + lane, n - 1) * 4), lds_addr(lds));
@@ -242,8 +281,10 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnArgs g) {
   const void* Ku = uniform_ptr(K);
   const void* Vu = uniform_ptr(V);
   fill_key_bias<NW>(kbl, g, b, tid);
-  dma_rows<NW>(lds[0][0], Ku, g.k.sr, 0, g.nk, wid, lane);
-  dma_rows<NW>(lds[0][1], Vu, g.v.sr, 0, g.nk, wid, lane);
+  const uint32_t lb = lds_addr(&lds[0][0][0]);  // [buf][K / V] tiles of 8 KB
+  const RowPlan<NW> pk = row_plan<NW>(g.k.sr, wid, lane), pv = row_plan<NW>(g.v.sr, wid, lane);
+  dma_rows_at<NW>(lb, Ku, g.k.sr, 0, g.nk, pk, wid, lane);
+  dma_rows_at<NW>(lb + 8192, Vu, g.v.sr, 0, g.nk, pv, wid, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -252,8 +293,8 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnArgs g) {
     const int kv0 = t * 64;
     const bool more = t + 1 < nt;
     if (more) {  // next K/V tile by LDS-DMA into the other buffer, in flight during this tile
-      dma_rows<NW>(lds[cur ^ 1][0], Ku, g.k.sr, kv0 + 64, g.nk, wid, lane);
-      dma_rows<NW>(lds[cur ^ 1][1], Vu, g.v.sr, kv0 + 64, g.nk, wid, lane);
+      dma_rows_at<NW>(lb + (cur ^ 1) * 16384, Ku, g.k.sr, kv0 + 64, g.nk, pk, wid, lane);
+      dma_rows_at<NW>(lb + (cur ^ 1) * 16384 + 8192, Vu, g.v.sr, kv0 + 64, g.nk, pv, wid, lane);
     }
     const char* lk = lds[cur][0];
     const char* lv = lds[cur][1];
@@ -381,9 +422,11 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
   const void* Lu = uniform_ptr(LSE);
   const void* Eu = uniform_ptr(DEL);
   // Q / dO tiles and their lse / delta rows by LDS-DMA (waves 0 and 1 also move one stats piece each).
+  const uint32_t lb = lds_addr(&lds[0][0][0]);  // [buf][Q / dO] tiles of 8 KB
+  const RowPlan<NW> pq = row_plan<NW>(g.q.sr, wid, lane), pd0 = row_plan<NW>(g.dO.sr, wid, lane);
   auto stage = [&](int buf, int r0) {
-    dma_rows<NW>(lds[buf][0], Qu, g.q.sr, r0, g.n, wid, lane);
-    dma_rows<NW>(lds[buf][1], Du, g.dO.sr, r0, g.n, wid, lane);
+    dma_rows_at<NW>(lb + buf * 16384, Qu, g.q.sr, r0, g.n, pq, wid, lane);
+    dma_rows_at<NW>(lb + buf * 16384 + 8192, Du, g.dO.sr, r0, g.n, pd0, wid, lane);
     if (wid == 0) dma_stat(lstat[buf][0], Lu, r0, g.n, lane);
     else if (wid == 1) dma_stat(lstat[buf][1], Eu, r0, g.n, lane);
   };
@@ -548,8 +591,10 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
   const void* Ku = uniform_ptr(K);
   const void* Vu = uniform_ptr(V);
   fill_key_bias<NW>(kbl, g, b, tid);
-  dma_rows<NW>(lds[0][0], Ku, g.k.sr, 0, g.nk, wid, lane);
-  dma_rows<NW>(lds[0][1], Vu, g.v.sr, 0, g.nk, wid, lane);
+  const uint32_t lb = lds_addr(&lds[0][0][0]);  // [buf][K / V] tiles of 8 KB
+  const RowPlan<NW> pk = row_plan<NW>(g.k.sr, wid, lane), pv = row_plan<NW>(g.v.sr, wid, lane);
+  dma_rows_at<NW>(lb, Ku, g.k.sr, 0, g.nk, pk, wid, lane);
+  dma_rows_at<NW>(lb + 8192, Vu, g.v.sr, 0, g.nk, pv, wid, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -558,8 +603,8 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
     const int kv0 = t * 64;
     const bool more = ABL != 1 && t + 1 < nt;
     if (more) {
-      dma_rows<NW>(lds[cur ^ 1][0], Ku, g.k.sr, kv0 + 64, g.nk, wid, lane);
-      dma_rows<NW>(lds[cur ^ 1][1], Vu, g.v.sr, kv0 + 64, g.nk, wid, lane);
+      dma_rows_at<NW>(lb + (cur ^ 1) * 16384, Ku, g.k.sr, kv0 + 64, g.nk, pk, wid, lane);
+      dma_rows_at<NW>(lb + (cur ^ 1) * 16384 + 8192, Vu, g.v.sr, kv0 + 64, g.nk, pv, wid, lane);
     }
     const char* lk = lds[cur][0];
     const char* lv = lds[cur][1];

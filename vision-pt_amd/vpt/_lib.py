@@ -130,6 +130,9 @@ def _load(path: Path, diag: bool = False) -> C.CDLL:
 
 DIAG = os.environ.get("VPT_DIAG", "0") == "1"
 LIB_PATH = LIB_DIAG if DIAG else LIB
+# developer A/B hook (tools/build_ab.py): load a library built from another revision of csrc/ instead
+if os.environ.get("VPT_LIB_AB"):
+    LIB_PATH = Path(os.environ["VPT_LIB_AB"])
 lib = _load(LIB_PATH, DIAG)
 
 
