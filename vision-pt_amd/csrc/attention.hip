@@ -411,6 +411,10 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
   load_row_frags(kf, g.k.p + b * g.k.sb + hd * g.k.sh, g.k.sr, key, g.nk, lane);
   load_row_frags(vf, g.v.p + b * g.v.sb + hd * g.v.sh, g.v.sr, key, g.nk, lane);
   const bool kmasked = key_bias(g, b, key) == kNegInf;
+  // Retire those loads here, visibly to hipcc's wait placement: otherwise its wait for them sits at the
+  // first MFMA inside the tile loop, runs every iteration, and -- vmcnt retiring in order -- also drains the
+  // next tile's LDS-DMA issued just before it (the asm DMAs are invisible to the compiler).
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
 
   floatx16 dvT[2], dkT[2];
 #pragma unroll
