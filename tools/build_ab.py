@@ -3,15 +3,27 @@ A/B timing (VPT_LIB_AB=<path> makes vpt load it instead of the production librar
 
   python tools/build_ab.py REV NAME [--diag]
 """
-import os
+import importlib.util
 import subprocess
 import sys
 import tempfile
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-sys.path.insert(0, str(ROOT / "vision-pt_amd"))
-from vpt import _build  # noqa: E402
+
+
+def _build_module(rev: str, td: Path):
+    """vpt/_build.py as of `rev` (its compiler flags, per-unit flags included)."""
+    src = subprocess.run(["git", "-C", str(ROOT), "show", f"{rev}:vision-pt_amd/vpt/_build.py"], capture_output=True,
+                         check=True).stdout
+    path = td / "_build_rev.py"
+    path.write_bytes(src)
+    spec = importlib.util.spec_from_file_location("_build_rev", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    if not hasattr(mod, "UNIT_FLAGS"):
+        mod.UNIT_FLAGS = {}
+    return mod
 
 
 def main():
@@ -21,6 +33,7 @@ def main():
     out.parent.mkdir(parents=True, exist_ok=True)
     with tempfile.TemporaryDirectory() as td:
         td = Path(td)
+        _build = _build_module(rev, td)
         files = subprocess.run(["git", "-C", str(ROOT), "ls-tree", "--name-only", rev, "vision-pt_amd/csrc/"],
                                capture_output=True, text=True, check=True).stdout.split()
         for f in files:
