@@ -18,7 +18,8 @@ extern "C" {
 
 /* GEMM tile geometry override: 0 = automatic; 128, 256; 2561 = ring unstaggered, 2562 = 256x256
  * 2-stage (A/B); 2563/2564 = timing-only ablations of the ring (WRONG results); 2565 = DMA in the
- * MFMA phase; 2566 / 2567 = stamped / timeline ring builds (need vpt_gemm_set_debug). */
+ * MFMA phase; 2566 / 2567 = stamped / timeline ring builds (need vpt_gemm_set_debug); 2568 = ring without
+ * its epilogue (timing only, WRONG results; accumulators kept live so the MFMAs are not dead code). */
 int vpt_gemm_set_geometry(int geo);
 /* u64 buffer receiving per-wave K-step segment cycle sums (2566: [256][8][8]) or realtime stamps
  * (2567: [grid][4][4]); nullptr disables. */

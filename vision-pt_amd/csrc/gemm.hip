@@ -694,19 +694,19 @@ __device__ __forceinline__ void epilogue_ring(const GemmArgs& g, const floatx4 (
           for (int q = 0; q < 8; ++q) o[q] = bf2f(f2bf(o[q])) + rv[q];
         }
         const uint4 w = pack8(o);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{w.x, w.y, w.z, w.w}, e.rs, (int)e.voff, soff, 0);
+        store_b128_padded(u32x4{w.x, w.y, w.z, w.w}, e.rs, (int)e.voff, soff);
       } else {
         if (EPI == EPI_ACC) {
           const u32x4 a0 = pre.v[4 * il + 2 * p], a1 = pre.v[4 * il + 2 * p + 1];
 #pragma unroll
           for (int q = 0; q < 4; ++q) { o[q] += __uint_as_float(a0[q]); o[4 + q] += __uint_as_float(a1[q]); }
         }
-        __builtin_amdgcn_raw_buffer_store_b128(
+        store_b128_padded(
             u32x4{__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3])}, e.rs,
-            (int)e.voff, soff, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(
+            (int)e.voff, soff);
+        store_b128_padded(
             u32x4{__float_as_uint(o[4]), __float_as_uint(o[5]), __float_as_uint(o[6]), __float_as_uint(o[7])}, e.rs,
-            (int)e.voff, soff + 16, 0);
+            (int)e.voff, soff + 16);
       }
     }
   }
@@ -755,9 +755,9 @@ __device__ __forceinline__ void epilogue_ring_swf(const GemmArgs& g, const float
     }
     const int soff = i * 16 * (int)g.ldc * 2, soffh = i * 16 * (int)g.ldc2 * 2;
     const uint4 w1 = pack8(x1), w2 = pack8(x2), wh = pack8(hv);
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4{w1.x, w1.y, w1.z, w1.w}, rs, (int)vx, soff, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4{w2.x, w2.y, w2.z, w2.w}, rs, (int)(vx + F * 2), soff, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4{wh.x, wh.y, wh.z, wh.w}, rh, (int)vh, soffh, 0);
+    store_b128_padded(u32x4{w1.x, w1.y, w1.z, w1.w}, rs, (int)vx, soff);
+    store_b128_padded(u32x4{w2.x, w2.y, w2.z, w2.w}, rs, (int)(vx + F * 2), soff);
+    store_b128_padded(u32x4{wh.x, wh.y, wh.z, wh.w}, rh, (int)vh, soffh);
   }
 }
 
@@ -955,7 +955,16 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
       if (nx.nk > 1) ring_issue<AK, BK_, SW>(g, nx, 1, lds0, wid, lane);
       if (nx.nk > 2) ring_issue<AK, BK_, SW>(g, nx, 2, lds0, wid, lane);
     }
-    if (SW) {
+    if (ABL == 3) {
+      // diagnostic timing ablation (wrong results): no epilogue, but the accumulators stay live (a store
+      // no real run takes) so the K loop's MFMAs are not dead code
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+      if (s == 1.2345e37f) reinterpret_cast<float*>(g.C)[threadIdx.x] = s;
+    } else if (SW) {
       epilogue_ring_swf(g, acc, stg, lane, it, wm, wn, bias8, bias8b);
     } else if (GF == 2) {
       epilogue_ring<EPI, 0, 2>(g, acc, stg, lane, ea, bias8, pre);
@@ -979,7 +988,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
     // X_0, which every wave reaches only after its staging reads (raw_barrier: lgkmcnt(0) first).
     item = next;
     it = nx;
-    pend = S;  // the epilogue's S stores are younger than the next item's pre-issued tiles 0-2
+    pend = ABL == 3 ? 0 : S;  // the epilogue's S stores are younger than the next item's pre-issued tiles 0-2
   }
 }
 
@@ -1054,6 +1063,7 @@ int launch_geo(const GemmArgs& g, int splits, int geo, hipStream_t s) {
   if (geo == 2565) return launch_ring<AK, BK_, true, 0, true>(g, splits, s);  // DMA in the MFMA phase
   if (AK && BK_ && geo == 2566 && g.dbg) return launch_ring<AK, BK_, true, 0, false, true>(g, splits, s);  // stamps
   if (AK && BK_ && geo == 2567 && g.dbg) return launch_ring<AK, BK_, true, 0, false, false, true>(g, splits, s);
+  if (geo == 2568) return launch_ring<AK, BK_, true, 3>(g, splits, s);  // no epilogue (wrong results)
   if (geo == 2562) return launch<AK, BK_, 256, 256, 2, 4>(g, splits, s);  // 2-stage BK=64 T256 (A/B only)
 #endif
   return launch<AK, BK_, 128, 128, 2, 2>(g, splits, s);
@@ -1209,8 +1219,8 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
 #ifdef VPT_DIAG
 // ---- diagnostic build only (libvpt_hip_diag.so, include/vpt_hip_diag.h): process-wide switches ----
 extern "C" int vpt_gemm_set_geometry(int geo) {
-  VPT_CHECK_ARG(geo == 0 || geo == 128 || geo == 256 || (geo >= 2561 && geo <= 2567),
-                "vpt_gemm_set_geometry: 0, 128, 256 or 2561-2567");
+  VPT_CHECK_ARG(geo == 0 || geo == 128 || geo == 256 || (geo >= 2561 && geo <= 2568),
+                "vpt_gemm_set_geometry: 0, 128, 256 or 2561-2568");
   g_geo_override = geo;
   return VPT_OK;
 }
