@@ -1570,36 +1570,44 @@ namespace {
 constexpr int LKC = 128;         // K chunk of W staged per step (lora_proj)
 constexpr int LKP = LKC + 8;     // padded LDS row (bf16): conflict-free b128 row reads
 
-// One wave per 16 rows (64-thread workgroups, M/16 of them): 128-k chunks with the activation fragments of
-// LPD chunks in flight in registers (a 4-deep ring), so the memory latency is paid once, not per chunk.
+// Four waves per 16 rows (LKS-wave workgroups, M/16 of them), each taking every LKS-th 128-k chunk with the
+// activation fragments of its next LPD chunks in flight in registers (a 4-deep ring), so the memory latency
+// is paid once, not per chunk; the LKS partial sums meet in LDS and wave 0 adds them in wave order
+// (deterministic). (One wave per 16 rows left M = 4096 launches at one wave per CU: 12 us, latency-bound.)
 // W = down [16][K]: B fragments straight from global memory (L2-resident, prefetched with the chunk);
 // W = up [K][16]: each chunk transposed through the wave's LDS image.
 constexpr int LPD = 4;
-__global__ __launch_bounds__(64) void lora_proj_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W,
-                                                       int w_kmajor, bf16_t* __restrict__ Y, long ldy, int M, int K,
-                                                       float alpha) {
-  __shared__ __attribute__((aligned(16))) bf16_t ws[16 * LKP];
-  const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
+constexpr int LKS = 4;
+__global__ __launch_bounds__(64 * LKS) void lora_proj_kernel(const bf16_t* __restrict__ X, long ldx,
+                                                             const bf16_t* __restrict__ W, int w_kmajor,
+                                                             bf16_t* __restrict__ Y, long ldy, int M, int K, float alpha) {
+  __shared__ __attribute__((aligned(16))) bf16_t wsa[LKS][16 * LKP];
+  __shared__ __attribute__((aligned(16))) floatx4 red[LKS][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
+  bf16_t* ws = wsa[wid];
   const int row = blockIdx.x * 16 + j;
   const bf16_t* xr = X + (long)min(row, M - 1) * ldx + 8 * g;
   const bf16_t* wr = W + (long)j * K + 8 * g;  // down: row j
   const int nch = K / LKC;
+  const int ncw = (nch - wid + LKS - 1) / LKS;  // chunks wid, wid + LKS, ... of this wave
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
   uint4 xb[LPD][LKC / 32], wb[LPD][LKC / 32];
 #pragma unroll
   for (int u = 0; u < LPD; ++u)
-    if (u < nch) {
+    if (u < ncw) {
+      const int c = wid + LKS * u;
 #pragma unroll
       for (int s = 0; s < LKC / 32; ++s) {
-        xb[u][s] = *reinterpret_cast<const uint4*>(xr + u * LKC + 32 * s);
-        if (w_kmajor) wb[u][s] = *reinterpret_cast<const uint4*>(wr + u * LKC + 32 * s);
+        xb[u][s] = *reinterpret_cast<const uint4*>(xr + c * LKC + 32 * s);
+        if (w_kmajor) wb[u][s] = *reinterpret_cast<const uint4*>(wr + c * LKC + 32 * s);
       }
     }
-  for (int c0 = 0; c0 < nch; c0 += LPD) {
+  for (int t0 = 0; t0 < ncw; t0 += LPD) {
 #pragma unroll
     for (int u = 0; u < LPD; ++u) {
-      const int c = c0 + u;
-      if (c < nch) {
+      const int t = t0 + u;
+      if (t < ncw) {
+        const int c = wid + LKS * t;
         if (!w_kmajor) {  // up [K][16]: 128 rows of 32 B, two per lane, transposed into [16][k]
           __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -1623,16 +1631,22 @@ __global__ __launch_bounds__(64) void lora_proj_kernel(const bf16_t* __restrict_
                                      : as_frag(*reinterpret_cast<const uint4*>(&ws[j * LKP + 32 * s + 8 * g]));
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(xb[u][s]), bf, acc, 0, 0, 0);
         }
-        if (c + LPD < nch) {
+        if (t + LPD < ncw) {
+          const int cn = c + LKS * LPD;
 #pragma unroll
           for (int s = 0; s < LKC / 32; ++s) {
-            xb[u][s] = *reinterpret_cast<const uint4*>(xr + (c + LPD) * LKC + 32 * s);
-            if (w_kmajor) wb[u][s] = *reinterpret_cast<const uint4*>(wr + (c + LPD) * LKC + 32 * s);
+            xb[u][s] = *reinterpret_cast<const uint4*>(xr + cn * LKC + 32 * s);
+            if (w_kmajor) wb[u][s] = *reinterpret_cast<const uint4*>(wr + cn * LKC + 32 * s);
           }
         }
       }
     }
   }
+  red[wid][lane] = acc;
+  __syncthreads();
+  if (wid != 0) return;
+#pragma unroll
+  for (int w = 1; w < LKS; ++w) acc += red[w][lane];
   // D[m][j]: lane holds rows 4g..4g+3 of the wave's 16, column j = lane & 15
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -1730,7 +1744,7 @@ extern "C" int vpt_lora_proj(const void* X, long ldx, const void* W, int w_kmajo
   VPT_CHECK_ARG(X && W && Y, "vpt_lora_proj: null pointer");
   VPT_CHECK_ARG(r == 16, "vpt_lora_proj: rank 16 (the C5 configuration) only");
   VPT_CHECK_ARG(M > 0 && K > 0 && K % LKC == 0 && ldx % 8 == 0, "vpt_lora_proj: K % 128 == 0, 16-B leading dim");
-  hipLaunchKernelGGL(lora_proj_kernel, dim3((M + 15) / 16), dim3(64), 0, (hipStream_t)stream, (const bf16_t*)X, ldx,
+  hipLaunchKernelGGL(lora_proj_kernel, dim3((M + 15) / 16), dim3(64 * LKS), 0, (hipStream_t)stream, (const bf16_t*)X, ldx,
                      (const bf16_t*)W, w_kmajor, (bf16_t*)Y, ldy, M, K, alpha);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
