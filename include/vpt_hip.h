@@ -235,6 +235,20 @@ long vpt_lora_wgrad_workspace(int M, int N);
 int vpt_lora_wgrad2(const void* dY, long lddy, const void* dS, long ldds, float* g_up, int n_out, const void* X,
                     long ldx, const void* vS, long ldvs, float* g_down, int n_in, int M, int accumulate, float alpha,
                     void* ws_up, void* ws_down, void* stream);
+/* vpt_lora_wgrad2 in two steps, so that one launch reduces the adapter gradients of many targets:
+ * _partial writes both gradients' split-M f32 slabs into ws_up / ws_down (vpt_lora_wgrad_workspace bytes each;
+ * they must stay untouched until the reduce has run), vpt_lora_wgrad_splits(M, N) = the slabs of a width-N
+ * gradient, and vpt_lora_wgrad_reduce_batch applies g (+)= alpha * (sum of the slabs in split order) for up
+ * to 32 jobs in one launch (trans = 1: g stored [16][n], as g_down). Same results as vpt_lora_wgrad2. */
+typedef struct {
+  const float* part;
+  float* g;
+  int n, splits, trans, reserved;
+} VptLoraReduceJob;
+int vpt_lora_wgrad_splits(int M, int N);
+int vpt_lora_wgrad2_partial(const void* dY, long lddy, const void* dS, long ldds, int n_out, const void* X, long ldx,
+                            const void* vS, long ldvs, int n_in, int M, void* ws_up, void* ws_down, void* stream);
+int vpt_lora_wgrad_reduce_batch(const VptLoraReduceJob* jobs, int njobs, float alpha, int accumulate, void* stream);
 /* SpatialTransformer (src/models/sdxl/denoiser.py:283-365) around the transformer blocks:
  * GroupNorm(G, C, eps) on NCHW bf16 [B][C][HW] (f32 statistics mean / rstd [B*G] saved for the backward;
  * output NCHW bf16), its input gradient (affine weights frozen under QLoRA; dres: + a second NCHW gradient),

@@ -22,6 +22,7 @@
 // LDS (f32, 64 rows at a time) so bias / residual / SiLU and stores are 8-16 B per lane. Optional
 // split-K writes f32 partial slabs, summed in a fixed order by splitk_reduce_kernel.
 #include "common.h"
+#include "../../include/vpt_hip.h"  // C-ABI types (VptLoraReduceJob)
 
 namespace {
 
@@ -1737,6 +1738,27 @@ __global__ void lora_wgrad_reduce_kernel(LoraWgradJob j0, LoraWgradJob j1, float
   float* d = jb.G + (jb.trans ? (long)j * jb.N + n : (long)i);
   *d = (accumulate ? *d : 0.f) + alpha * sum;
 }
+// Batched form of lora_wgrad_reduce_kernel: blockIdx.y selects one of up to kLoraRedJobs (part, G) jobs, so
+// one launch finishes the adapter gradients of a whole transformer block (the per-target reduce launches
+// cost more than their few MB of traffic).
+constexpr int kLoraRedJobs = 32;
+struct LoraRedBatch {
+  const float* part[kLoraRedJobs];
+  float* g[kLoraRedJobs];
+  int n[kLoraRedJobs], splits[kLoraRedJobs], trans[kLoraRedJobs];
+};
+__global__ void lora_wgrad_reduce_batch_kernel(LoraRedBatch b, float alpha, int accumulate) {
+  const int jb = blockIdx.y;
+  const int N = b.n[jb], splits = b.splits[jb];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // element (n, j) of [N][16]
+  if (i >= N * 16) return;
+  const float* p = b.part[jb] + i;
+  float sum = 0.f;
+  for (int z = 0; z < splits; ++z) sum += p[(long)z * N * 16];  // split order: as lora_wgrad_reduce_kernel
+  const int n = i >> 4, j = i & 15;
+  float* d = b.g[jb] + (b.trans[jb] ? (long)j * N + n : (long)i);
+  *d = (accumulate ? *d : 0.f) + alpha * sum;
+}
 }  // namespace
 
 extern "C" int vpt_lora_proj(const void* X, long ldx, const void* W, int w_kmajor, void* Y, long ldy, int M, int K, int r,
@@ -1772,12 +1794,17 @@ static LoraWgradJob lora_job(const void* X, long ldx, const void* S, long lds_, 
   return j;
 }
 
+// Split-M slabs a wgrad of M rows and N columns writes (the `splits` of its vpt_lora_wgrad_reduce_batch job).
+extern "C" int vpt_lora_wgrad_splits(int M, int N) {
+  return M > 0 && N > 0 ? lora_job(nullptr, 0, nullptr, 0, nullptr, 0, M, N, nullptr).splits : 0;
+}
+
 // Both adapter gradients of one LoRA Linear in two launches (slabs, then the ordered sum):
 //   G_up [N_out][16] (+)= alpha * dY[M][N_out]^T . dS[M][16]
 //   G_down [16][N_in] (+)= alpha * X[M][N_in]^T . vS[M][16]     (ws_up / ws_down: lora_wgrad_workspace bytes)
-extern "C" int vpt_lora_wgrad2(const void* dY, long lddy, const void* dS, long ldds, float* g_up, int n_out,
-                               const void* X, long ldx, const void* vS, long ldvs, float* g_down, int n_in, int M,
-                               int accumulate, float alpha, void* ws_up, void* ws_down, void* stream) {
+static int lora_wgrad2_impl(const void* dY, long lddy, const void* dS, long ldds, float* g_up, int n_out,
+                            const void* X, long ldx, const void* vS, long ldvs, float* g_down, int n_in, int M,
+                            int accumulate, float alpha, void* ws_up, void* ws_down, bool deferred, void* stream) {
   VPT_CHECK_ARG(dY && dS && g_up && X && vS && g_down && ws_up && ws_down, "vpt_lora_wgrad2: null pointer");
   VPT_CHECK_ARG(M > 0 && n_out % 64 == 0 && n_in % 64 == 0 && lddy % 8 == 0 && ldx % 8 == 0 && ldds % 8 == 0 &&
                     ldvs % 8 == 0, "vpt_lora_wgrad2: widths % 64, 16-B leading dims");
@@ -1787,8 +1814,43 @@ extern "C" int vpt_lora_wgrad2(const void* dY, long lddy, const void* dS, long l
   const int gx = max(n_out, n_in) / 64, gy = max(j0.splits, j1.splits);
   hipLaunchKernelGGL(lora_wgrad_kernel, dim3(gx, gy, 2), dim3(256), 0, s, j0, j1, M);
   VPT_LAUNCH_CHECK();
+  if (deferred) return VPT_OK;
   hipLaunchKernelGGL(lora_wgrad_reduce_kernel, dim3((max(n_out, n_in) * 16 + 255) / 256, 2), dim3(256), 0, s, j0, j1,
                      alpha, accumulate);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_lora_wgrad2(const void* dY, long lddy, const void* dS, long ldds, float* g_up, int n_out,
+                               const void* X, long ldx, const void* vS, long ldvs, float* g_down, int n_in, int M,
+                               int accumulate, float alpha, void* ws_up, void* ws_down, void* stream) {
+  return lora_wgrad2_impl(dY, lddy, dS, ldds, g_up, n_out, X, ldx, vS, ldvs, g_down, n_in, M, accumulate, alpha, ws_up,
+                          ws_down, false, stream);
+}
+
+extern "C" int vpt_lora_wgrad2_partial(const void* dY, long lddy, const void* dS, long ldds, int n_out, const void* X,
+                                       long ldx, const void* vS, long ldvs, int n_in, int M, void* ws_up, void* ws_down,
+                                       void* stream) {
+  // g_up / g_down are only read by the reduce: any non-null placeholders pass the argument check
+  float* const placeholder = reinterpret_cast<float*>(ws_up);
+  return lora_wgrad2_impl(dY, lddy, dS, ldds, placeholder, n_out, X, ldx, vS, ldvs, placeholder, n_in, M, 1, 1.f, ws_up,
+                          ws_down, true, stream);
+}
+
+extern "C" int vpt_lora_wgrad_reduce_batch(const VptLoraReduceJob* jobs, int njobs, float alpha, int accumulate,
+                                           void* stream) {
+  VPT_CHECK_ARG(jobs && njobs > 0 && njobs <= kLoraRedJobs, "vpt_lora_wgrad_reduce_batch: 1..32 jobs");
+  LoraRedBatch b = {};
+  int nmax = 0;
+  for (int i = 0; i < njobs; ++i) {
+    VPT_CHECK_ARG(jobs[i].part && jobs[i].g && jobs[i].n > 0 && jobs[i].splits > 0,
+                  "vpt_lora_wgrad_reduce_batch: bad job");
+    b.part[i] = jobs[i].part; b.g[i] = jobs[i].g;
+    b.n[i] = jobs[i].n; b.splits[i] = jobs[i].splits; b.trans[i] = jobs[i].trans;
+    nmax = max(nmax, jobs[i].n);
+  }
+  hipLaunchKernelGGL(lora_wgrad_reduce_batch_kernel, dim3((nmax * 16 + 255) / 256, njobs), dim3(256), 0,
+                     (hipStream_t)stream, b, alpha, accumulate);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

@@ -74,6 +74,9 @@ SIGNATURES: dict[str, list] = {
     "vpt_lora_proj": [P, L, P, I, P, L, I, I, I, F, P],
     "vpt_lora_wgrad_workspace": [I, I],
     "vpt_lora_wgrad2": [P, L, P, L, P, I, P, L, P, L, P, I, I, I, F, P, P, P],
+    "vpt_lora_wgrad_splits": [I, I],
+    "vpt_lora_wgrad2_partial": [P, L, P, L, I, P, L, P, L, I, I, P, P, P],
+    "vpt_lora_wgrad_reduce_batch": [P, I, F, I, P],
     "vpt_ema_update": [P, P, L, F, I, P],
     "vpt_gemm_nf4": [P, L, P, P, P, P, P, L, I, P, L, P, L, I, P, L, I, I, I, P, P, L, I, F, P],
     "vpt_nf4_quantize": [P, L, P, P, P, P, P, P, P],
@@ -111,7 +114,7 @@ _RESTYPES = {
     "vpt_build_info": C.c_char_p,
 }
 # Entry points that return a value (size / count / string) rather than a status code.
-_VALUE_FNS = {"vpt_lora_wgrad_workspace", "vpt_gemm_workspace_bytes", "vpt_linear_wgrad_workspace_bytes", "vpt_attn_fused_workspace_bytes", "vpt_cover_resize_crop_workspace", "vpt_gemm_swiglu_bwd_workspace", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
+_VALUE_FNS = {"vpt_lora_wgrad_workspace", "vpt_lora_wgrad_splits", "vpt_gemm_workspace_bytes", "vpt_linear_wgrad_workspace_bytes", "vpt_attn_fused_workspace_bytes", "vpt_cover_resize_crop_workspace", "vpt_gemm_swiglu_bwd_workspace", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
               "vpt_colsum_blocks", "vpt_attn_q_scale", "vpt_last_error_string", "vpt_abi_version", "vpt_build_info"}
 
 

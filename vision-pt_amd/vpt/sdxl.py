@@ -233,7 +233,12 @@ class SDXLTransformerBlock:
         return y
 
     def backward(self, dy: torch.Tensor):
-        """Returns (dx, dctx); accumulates every adapter's g_down / g_up (norms and NF4 bases frozen)."""
+        """Returns (dx, dctx); accumulates every adapter's g_down / g_up (norms and NF4 bases frozen). The ten
+        targets' adapter-gradient reduces run as one batched launch at the end (ops.lora_wgrad_batch)."""
+        with ops.lora_wgrad_batch():
+            return self._backward(dy)
+
+    def _backward(self, dy: torch.Tensor):
         st, L = self._st, self.lin
         B, n, nc = st["B"], st["n"], st["nc"]
         m1, m2, m3 = st["m"]
