@@ -34,13 +34,15 @@ def main():
     with tempfile.TemporaryDirectory() as td:
         td = Path(td)
         _build = _build_module(rev, td)
-        files = subprocess.run(["git", "-C", str(ROOT), "ls-tree", "--name-only", rev, "vision-pt_amd/csrc/"],
-                               capture_output=True, text=True, check=True).stdout.split()
+        # csrc/ and include/ at their repository paths (units include ../../include/vpt_hip.h)
+        files = subprocess.run(["git", "-C", str(ROOT), "ls-tree", "--name-only", rev, "vision-pt_amd/csrc/",
+                                "include/"], capture_output=True, text=True, check=True).stdout.split()
         for f in files:
             data = subprocess.run(["git", "-C", str(ROOT), "show", f"{rev}:{f}"], capture_output=True, check=True).stdout
-            (td / Path(f).name).write_bytes(data)
+            (td / f).parent.mkdir(parents=True, exist_ok=True)
+            (td / f).write_bytes(data)
         objs = []
-        for src in sorted(td.glob("*.hip")):
+        for src in sorted((td / "vision-pt_amd" / "csrc").glob("*.hip")):
             obj = td / (src.stem + ".o")
             cmd = [_build.HIPCC, *_build.CFLAGS, *_build.UNIT_FLAGS.get(src.name, []), *(["-DVPT_DIAG"] if diag else []),
                    "-c", str(src), "-o", str(obj)]

@@ -1656,7 +1656,7 @@ __global__ __launch_bounds__(64 * LKS) void lora_proj_kernel(const bf16_t* __res
   }
 }
 
-constexpr int LMC = 32;  // m rows per wgrad step
+constexpr int LMC = 128;  // m rows per wgrad stage (4 MFMA k-steps of 32 between two barriers)
 
 // One wgrad job: G (+)= alpha * X[M][N]^T . S[M][16] (trans: G stored [16][N]); split over gridDim.y.
 struct LoraWgradJob {
@@ -1667,64 +1667,54 @@ struct LoraWgradJob {
   int N, trans, mchunk, splits;
 };
 
+// The MFMA operands run along m, the row index of both X and S: the tiles are staged row-major as loaded
+// (one 16-B LDS store per chunk) and read back transposed by ds_read_b64_tr_b16 (lane i of a 16-lane group
+// gets column i of 4 rows), 128 rows per stage with the next stage's loads in flight in registers.
+constexpr int LXS = 72;  // X stage row stride (bf16): 64 columns + 16 B padding (spreads the tr reads' banks)
+constexpr int LSS = 24;  // S stage row stride (bf16): 16 columns + 16 B
 __global__ __launch_bounds__(256) void lora_wgrad_kernel(LoraWgradJob j0, LoraWgradJob j1, int M) {
   const LoraWgradJob jb = blockIdx.z ? j1 : j0;
   if ((int)blockIdx.x >= jb.N / 64 || (int)blockIdx.y >= jb.splits) return;
-  __shared__ __attribute__((aligned(16))) bf16_t xt[64 * (LMC + 8)];  // [n][m]
-  __shared__ __attribute__((aligned(16))) bf16_t st[16 * (LMC + 8)];  // [j][m]
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4;
+  __shared__ __attribute__((aligned(16))) bf16_t xt[LMC * LXS];  // [m][n]
+  __shared__ __attribute__((aligned(16))) bf16_t st[LMC * LSS];  // [m][j]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   const int n0 = blockIdx.x * 64;
   const int mb = blockIdx.y * jb.mchunk, me = min(M, mb + jb.mchunk);
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-  // the global reads of LPD steps are in flight in registers (a 4-deep ring): one latency per chunk, not per step
-  const int mr = tid >> 3, c = tid & 7;   // X tile: 32 rows x 64 n, one 16-B chunk per thread
-  const int sm = tid >> 1, hh = tid & 1;  // S tile: 32 rows x 16 j, threads 0..63
-  auto ldx_ = [&](int m0) {
-    const int m = m0 + mr;
-    return m < me ? *reinterpret_cast<const uint4*>(jb.X + (long)m * jb.ldx + n0 + c * 8) : make_uint4(0, 0, 0, 0);
-  };
-  auto lds_ = [&](int m0) {
-    return (tid < 64 && m0 + sm < me) ? *reinterpret_cast<const uint4*>(jb.S + (long)(m0 + sm) * jb.lds + hh * 8)
-                                      : make_uint4(0, 0, 0, 0);
-  };
-  uint4 xv[LPD], sv[LPD];
+  const int mr = tid >> 3, c = tid & 7;   // X: rows mr + 32u (u = 0..3), 16-B chunk c of the 64 columns
+  const int sm = tid >> 1, hh = tid & 1;  // S: row sm, 16-B half hh of the 16 columns
+  auto load = [&](int m0, uint4 (&xv)[4], uint4& sv) {
 #pragma unroll
-  for (int u = 0; u < LPD; ++u) { xv[u] = ldx_(mb + u * LMC); sv[u] = lds_(mb + u * LMC); }
-  for (int q0 = mb; q0 < me; q0 += LPD * LMC) {
-#pragma unroll
-    for (int u = 0; u < LPD; ++u) {
-      const int m0 = q0 + u * LMC;
-      if (m0 < me) {
-        {
-          const uint32_t w[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            xt[(c * 8 + 2 * e) * (LMC + 8) + mr] = (bf16_t)(w[e] & 0xffff);
-            xt[(c * 8 + 2 * e + 1) * (LMC + 8) + mr] = (bf16_t)(w[e] >> 16);
-          }
-          if (tid < 64) {
-            const uint32_t q[4] = {sv[u].x, sv[u].y, sv[u].z, sv[u].w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              st[(hh * 8 + 2 * e) * (LMC + 8) + sm] = (bf16_t)(q[e] & 0xffff);
-              st[(hh * 8 + 2 * e + 1) * (LMC + 8) + sm] = (bf16_t)(q[e] >> 16);
-            }
-          }
-        }
-        xv[u] = ldx_(m0 + LPD * LMC);  // refill the ring slot LPD steps ahead
-        sv[u] = lds_(m0 + LPD * LMC);
-        __syncthreads();
-        const bf16x8 a = as_frag(*reinterpret_cast<const uint4*>(&xt[(wid * 16 + (lane & 15)) * (LMC + 8) + 8 * g]));
-        const bf16x8 b = as_frag(*reinterpret_cast<const uint4*>(&st[(lane & 15) * (LMC + 8) + 8 * g]));
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
-        __syncthreads();
-      }
+    for (int u = 0; u < 4; ++u) {
+      const int m = m0 + mr + 32 * u;
+      xv[u] = m < me ? *reinterpret_cast<const uint4*>(jb.X + (long)m * jb.ldx + n0 + c * 8) : make_uint4(0, 0, 0, 0);
     }
+    sv = m0 + sm < me ? *reinterpret_cast<const uint4*>(jb.S + (long)(m0 + sm) * jb.lds + hh * 8) : make_uint4(0, 0, 0, 0);
+  };
+  uint4 xv[4], sv;
+  load(mb, xv, sv);
+  for (int m0 = mb; m0 < me; m0 += LMC) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) *reinterpret_cast<uint4*>(&xt[(mr + 32 * u) * LXS + c * 8]) = xv[u];
+    *reinterpret_cast<uint4*>(&st[sm * LSS + hh * 8]) = sv;
+    if (m0 + LMC < me) load(m0 + LMC, xv, sv);  // next stage in flight during this one
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < LMC / 32; ++kk) {
+      // A = X^T rows n = 16 wid + (lane & 15), k = m (8g .. 8g+7 of this 32); B = S, columns j = lane & 15
+      const int r0 = 32 * kk + 8 * g + q;
+      const uint2 a0 = lds_read_tr16((const VPT_LDS void*)(VPT_LDS char*)&xt[r0 * LXS + 16 * wid + 4 * p]);
+      const uint2 a1 = lds_read_tr16((const VPT_LDS void*)(VPT_LDS char*)&xt[(r0 + 4) * LXS + 16 * wid + 4 * p]);
+      const uint2 b0 = lds_read_tr16((const VPT_LDS void*)(VPT_LDS char*)&st[r0 * LSS + 4 * p]);
+      const uint2 b1 = lds_read_tr16((const VPT_LDS void*)(VPT_LDS char*)&st[(r0 + 4) * LSS + 4 * p]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag2(a0, a1), as_frag2(b0, b1), acc, 0, 0, 0);
+    }
+    __syncthreads();
   }
   // D[n][j]: rows n = n0 + 16 wid + 4g + r, column j = lane & 15 -> part[split][n][j]
-  float* p = jb.part + ((long)blockIdx.y * jb.N + n0 + wid * 16 + 4 * g) * 16 + (lane & 15);
+  float* pp = jb.part + ((long)blockIdx.y * jb.N + n0 + wid * 16 + 4 * g) * 16 + (lane & 15);
 #pragma unroll
-  for (int r = 0; r < 4; ++r) p[r * 16] = acc[r];
+  for (int r = 0; r < 4; ++r) pp[r * 16] = acc[r];
 }
 
 // G (+)= alpha * (sum of the split slabs in split order): deterministic; blockIdx.y selects the job.
