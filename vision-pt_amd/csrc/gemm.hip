@@ -1489,6 +1489,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nf4_kernel(GemmArgs g, Nf4Args f)
     if (more) {
       glds_tile<true, 128, 4>(nb, tile_ptr<true>(g.A, g.lda, m0, (kt + 1) * BK), g.lda, m0, g.M, BK, wid, lane);
       if (ABL < 2) nr = nf4_load<BKMAJ>(g, f, n0, (kt + 1) * BK, tid);
+    } else if (f.A2) {
+      // the LoRA K-extension tile (k in [0, r) of (A2, B2)) goes out under the last K step's MFMAs, into
+      // the idle stage, instead of as an exposed load after the loop
+      glds_tile<true, 128, 4>(nb, tile_ptr<true>(f.A2, f.lda2, m0, 0), f.lda2, m0, g.M, f.r, wid, lane);
+      glds_tile<BKMAJ, 128, 4>(nb + G::A_BYTES, tile_ptr<BKMAJ>(f.B2, f.ldb2, n0, 0), f.ldb2, n0, g.N, f.r, wid, lane);
     }
     mma_tile<true, BKMAJ, G>(smem + cur * G::STAGE, acc, wm, wn, lane);
     if (more && ABL == 0) nf4_store<BKMAJ>(nb + G::A_BYTES, nr, lut, c2, off, tid);
@@ -1497,12 +1502,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nf4_kernel(GemmArgs g, Nf4Args f)
     __syncthreads();
     cur ^= 1;
   }
-  if (f.A2) {  // LoRA K-extension: k in [0, r) of (A2, B2), zero-filled to 64
+  if (f.A2) {  // LoRA K-extension: k in [0, r) of (A2, B2) (loaded in the last K step), zero-filled to 64
     char* st = smem + cur * G::STAGE;
-    glds_tile<true, 128, 4>(st, tile_ptr<true>(f.A2, f.lda2, m0, 0), f.lda2, m0, g.M, f.r, wid, lane);
-    glds_tile<BKMAJ, 128, 4>(st + G::A_BYTES, tile_ptr<BKMAJ>(f.B2, f.ldb2, n0, 0), f.ldb2, n0, g.N, f.r, wid, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
     zero_k_tail<true, 128, 256>(st, f.r, tid);
     zero_k_tail<BKMAJ, 128, 256>(st + G::A_BYTES, f.r, tid);
     __syncthreads();
