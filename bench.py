@@ -7,9 +7,11 @@ bucketing (BASELINE.json config 3; config 4 when launched with N>1 ranks).
          --master-port P bench.py --gpus N --steps K --warmup W
 
 One step per rank = one batch of B=8 images of one bucket (5 buckets {1024x1024, 960x1088,
-1088x960, 896x1152, 1152x896}, round-robin in a seeded order): noise + patchify, JiT forward, x-loss,
-backward, RCCL all-reduce of the f32 gradients (N>1, bucketed, overlapped with backward), fused
-RAdamScheduleFree step — no work skipped. Synthetic data resident in HBM (no decoder), random-init
+1088x960, 896x1152, 1152x896}; each epoch's bucket batches in one seeded shuffled order shared by all ranks,
+rank r taking entries r, r+N, ... as accelerate's prepare_data_loader does): noise + patchify, JiT forward,
+x-loss, backward, RCCL all-reduce of the gradients (N>1: bf16 wire, per-block buckets launched as the
+backward completes them), fused RAdamScheduleFree step per bucket on a side stream as each reduction lands
+— no work skipped. `--workload c2`: BASELINE config 2 (512^2, B=16); `--workload c5`: config 5. Synthetic data resident in HBM (no decoder), random-init
 weights of the JiT_B_16_Config architecture, class-conditional context (V=10,000, 64 tokens, valid
 length U[8,64], CFG drop p=0.1). Prints ONE JSON line on rank 0.
 """
@@ -30,22 +32,41 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "train images/sec (whole node), JiT 1024² bucketed, 1/2/4/8 MI355X"
+METRIC_C2 = "train images/sec, JiT-B/16 512² single-bucket, 1 MI355X"
 BUCKETS = [(1024, 1024), (960, 1088), (1088, 960), (896, 1152), (1152, 896)]  # (W, H)
+BUCKETS_C2 = [(512, 512)]
 N_CLASSES = 10_000
 N_CTX = 64
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)
 PEAK_HBM_GBS = 8000.0
 
 
-def measured_traffic(op: str):
-    """HBM bytes per launch of `op` from the committed rocprofv3 PMC summary (tools/round_profile.sh ->
-    tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE passes, gfx950 read correction), or None."""
-    path = os.path.join(ROOT, "profiles", "traffic_latest.json")
+def measured_traffic(op: str, workload: str = "c3"):
+    """HBM bytes per launch of `op` from the committed rocprofv3 PMC summary of this workload
+    (profiles/traffic_latest.json = the c3 headline; profiles/traffic_<workload>.json otherwise;
+    tools/round_profile.sh -> tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE passes, gfx950 read
+    correction), or None when no summary of this workload is committed."""
+    name = "traffic_latest.json" if workload == "c3" else f"traffic_{workload}.json"
+    path = os.path.join(ROOT, "profiles", name)
     try:
         d = json.load(open(path))
-        return d[op]["hbm_bytes_per_launch"], f"profiles/traffic_latest.json ({d.get('_tag', '?')})"
+        return d[op]["hbm_bytes_per_launch"], f"profiles/{name} ({d.get('_tag', '?')})"
     except (OSError, KeyError, ValueError):
         return None, None
+
+
+def shared_order(n_buckets: int, steps: int, world: int, rank: int, seed: int = 7) -> list[int]:
+    """Per-step bucket index of this rank: accelerate's prepare_data_loader over a shuffled bucket-batch list
+    (vpt.data.BucketLoader.order): every rank draws the SAME seeded permutation of each epoch's bucket batches
+    (n_buckets per rank per epoch) and takes entries rank, rank + world, ... -- so ranks hold DIFFERENT
+    buckets in the same step (the 4032-4170-token skew is inside the timed region, as in training)."""
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    while len(out) < steps:
+        epoch = [i % n_buckets for i in range(n_buckets * world)]
+        perm = torch.randperm(len(epoch), generator=g).tolist()
+        out += [epoch[perm[j]] for j in range(rank, len(epoch), world)]
+    return out[:steps]
 
 
 def train_flops_per_image(np_: int, D=768, F=2048, depth=12, cs=4, bd=128) -> float:
@@ -58,10 +79,10 @@ def train_flops_per_image(np_: int, D=768, F=2048, depth=12, cs=4, bd=128) -> fl
     return 3.0 * f
 
 
-def make_batches(B: int, device, seed: int):
+def make_batches(B: int, device, seed: int, buckets=BUCKETS):
     g = torch.Generator(device="cpu").manual_seed(seed)
     out = []
-    for (W, H) in BUCKETS:
+    for (W, H) in buckets:
         img = (torch.rand(B, 3, H, W, generator=g) * 2 - 1).half().to(device)
         lens = torch.randint(8, N_CTX + 1, (B,), generator=g)
         ids = torch.randint(0, N_CLASSES, (B, N_CTX), generator=g)
@@ -74,7 +95,7 @@ def make_batches(B: int, device, seed: int):
     return out
 
 
-def cpu_baseline(budget_s: float = 20.0):
+def cpu_baseline(budget_s: float = 20.0, buckets=BUCKETS, max_steps: int = 4):
     """Times the CPU oracle (oracle/jit_oracle.py, a parity-pinned fp32 restatement of the
     reference step; AdamW stands in for schedulefree which is not installed) on host cores."""
     from oracle import jit_oracle as O
@@ -98,18 +119,33 @@ def cpu_baseline(budget_s: float = 20.0):
         opt.step()
         opt.zero_grad()
 
-    one(*BUCKETS[0])  # warm-up at the sample's own size (allocator, threads)
+    one(*buckets[0])  # warm-up at the sample's own size (allocator, threads)
     n, t0 = 0, time.perf_counter()
     while True:
-        W, H = BUCKETS[n % len(BUCKETS)]
+        W, H = buckets[n % len(buckets)]
         one(W, H)
         n += 1
-        if time.perf_counter() - t0 > budget_s or n >= 4:
+        if time.perf_counter() - t0 > budget_s or n >= max_steps:
             break
     dt = time.perf_counter() - t0
+    area = "1024^2-area buckets" if buckets is BUCKETS else f"{buckets[0][0]}x{buckets[0][1]}"
     return dict(value=round(n / dt, 5), unit="img/s", cores=threads, kind="port",
-                sample=f"{n} JiT-B/16 training steps (B=1, 1024^2-area buckets, fp32, AdamW) on the CPU oracle, "
+                sample=f"{n} JiT-B/16 training steps (B=1, {area}, fp32, AdamW) on the CPU oracle, "
                        f"{dt:.1f} s, torch threads={threads}")
+
+
+def roofline_entry(name: str, st: dict, workload: str = "c3"):
+    """MFMA roofline of one probed kernel: algorithmic FLOPs / mean launch time vs the bf16 peak, with the PMC
+    HBM bytes per launch (profiles/traffic_*.json) against the launch's compulsory bytes."""
+    traffic, src = measured_traffic(name, workload)
+    comp = st["mean_compulsory_bytes"]
+    return {"bound": "mfma", "kernel": name, "achieved": round(st["tflops"], 2), "peak": PEAK_BF16_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(st["tflops"] / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+            "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": src,
+            "compulsory_bytes_per_launch": round(comp), "traffic_over_compulsory":
+                round(traffic / comp, 2) if (traffic and comp) else None,
+            "algorithmic_gflop_per_launch": round(st["mean_gflop"], 3), "mean_launch_ms": round(st["mean_ms"], 4),
+            "launches_probed": st["launches"]}
 
 
 def main():
@@ -117,16 +153,24 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: 8 for c3, 16 for c2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--breakdown", default=None, help="write per-shape GEMM probe totals (JSON) to this file")
     ap.add_argument("--grad-ckpt", action="store_true",
                     help="gradient checkpointing on (denoiser.py:945-967): keep block inputs, recompute in backward")
-    ap.add_argument("--workload", default="c3", choices=["c3", "c5"],
-                    help="c3: JiT-B/16 1024^2 bucketed (the headline); c5: SDXL QLoRA transformer stacks")
+    ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
+                    help="optimizer per gradient bucket on a side stream as each all-reduce lands (auto: N > 1; "
+                         "at N = 1 one launch after the backward measured faster: 166.9 vs 166.0 img/s, r03d)")
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c5"],
+                    help="c3: JiT-B/16 1024^2 bucketed (the headline); c2: JiT-B/16 512^2 B=16; "
+                         "c5: SDXL QLoRA transformer stacks")
     args = ap.parse_args()
     if args.workload == "c5":
         return bench_c5(args)
+    c2 = args.workload == "c2"
+    buckets = BUCKETS_C2 if c2 else BUCKETS
+    if args.batch is None:
+        args.batch = 16 if c2 else 8
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -148,22 +192,24 @@ def main():
     trainer.engine.set_gradient_checkpointing(args.grad_ckpt)
     opt = RAdamScheduleFreeFlat(trainer.engine.params, trainer.engine.grads, lr=1e-4)
     opt.train()
-    # bf16 wire: the reference's DDP all-reduces the bf16 .grad tensors of its bf16 parameters
-    sync = GradSync(trainer.engine.grads, grad_buckets(trainer.engine.layout, cfg.depth), wire="bf16")
+    # per-block buckets: all-reduced (bf16 wire, as the reference's DDP reduces its bf16 .grad tensors) the
+    # moment the backward completes them and stepped by the optimizer on a side stream as each reduction lands
+    overlap = args.overlap == "on" or (args.overlap == "auto" and world > 1)
+    sync = GradSync(trainer.engine.grads, grad_buckets(trainer.engine.layout, cfg.depth), wire="bf16",
+                    overlap=overlap)
     losslog = LossLog(device)
-    batches = make_batches(args.batch, device, seed=100 + rank)
-    order = torch.randperm(len(BUCKETS), generator=torch.Generator().manual_seed(7)).tolist()
+    batches = make_batches(args.batch, device, seed=100 + rank, buckets=buckets)
+    n_probe = len(buckets)
+    order = shared_order(len(buckets), args.warmup + args.steps + n_probe, world, rank)
 
     def step(i):
-        b = batches[order[i % len(order)]]
-        trainer.step(b["images"], b["ids"], b["mask"], b["original_size"], b["target_size"], b["crop_coords"],
-                     on_ready=sync.launch if world > 1 else None)
+        b = batches[order[i]]
         s = opt.begin_step()
-        if world > 1:
-            sync.launch_rest()
-            sync.finish(lambda lo, hi, sc, g: opt.apply_range(s, lo, hi, sc, g))
-        else:
-            opt.apply_range(s, 0, opt.params.numel())
+        sync.arm(lambda lo, hi, sc, g, **kw: opt.apply_range(s, lo, hi, sc, g, **kw))
+        trainer.step(b["images"], b["ids"], b["mask"], b["original_size"], b["target_size"], b["crop_coords"],
+                     on_ready=sync.launch)
+        sync.launch_rest()
+        sync.finish()
         opt.end_step(s)
         losslog.push(trainer._loss)  # the reference's per-step loss gather (2-float all-reduce, read later)
 
@@ -188,7 +234,7 @@ def main():
     while losslog.pending:
         loss = losslog.pop()  # the last timed step's loss, averaged over ranks
 
-    # ---- probe pass (after the timed region): one round of the 5 buckets with HIP events around every
+    # ---- probe pass (after the timed region): one round of the buckets with HIP events around every
     # launch of the MFMA ops (algorithmic FLOPs) and the memory-bound ops (algorithmic HBM bytes)
     mfma_ops = ("attn_fwd", "attn_bwd", "gemm")
     hbm_ops = ("rmsnorm_fwd", "rmsnorm_bwd", "qknorm_rope_fwd", "qknorm_rope_bwd", "patchify",
@@ -197,7 +243,6 @@ def main():
     ops.PROBES.update(probes)
     for p in probes.values():
         p.active = True
-    n_probe = len(BUCKETS)
     for i in range(args.warmup + args.steps, args.warmup + args.steps + n_probe):
         step(i)
     torch.cuda.synchronize()
@@ -207,50 +252,55 @@ def main():
 
     imgs = args.batch * args.steps * world
     value = imgs / dt
-    # dominant kernel = the probed op with the largest total time inside the timed region
     stats, hbm = {}, {}
     for k in mfma_ops:
         n, ms, fl = probes[k].summary()
         stats[k] = dict(launches=n, mean_ms=ms, total_ms=n * ms, tflops=(fl / (ms * 1e-3) / 1e12) if ms else 0.0,
-                        mean_gflop=fl / 1e9)
+                        mean_gflop=fl / 1e9, mean_compulsory_bytes=probes[k].mean_bytes())
     for k in hbm_ops:
         n, ms, nb = probes[k].summary()
         gbs = nb / (ms * 1e-3) / 1e9 if ms else 0.0
         hbm[k] = dict(launches=n, mean_ms=round(ms, 4), mean_mb=round(nb / 1e6, 3), gb_s=round(gbs, 1),
                       frac=round(gbs / PEAK_HBM_GBS, 3))
+    gemm_keys = probes["gemm"].by_key()
     if args.breakdown and rank == 0:
         rows = {k: dict(launches=n, ms_per_step=round(t / n_probe, 4), tflops=round(w / (t * 1e-3) / 1e12, 1))
-                for k, (n, t, w) in probes["gemm"].by_key().items()}
+                for k, (n, t, w) in gemm_keys.items()}
         rows = dict(sorted(rows.items(), key=lambda kv: -kv[1]["ms_per_step"]))
         json.dump(rows, open(args.breakdown, "w"), indent=1)
-    dom = max(stats, key=lambda k: stats[k]["total_ms"])
-    ach = stats[dom]["tflops"]
-    traffic, traffic_src = measured_traffic(dom)
-    np_avg = sum((W // 16) * (H // 16) for W, H in BUCKETS) / len(BUCKETS)
+    # headline roofline = the single kernel with the largest time per step: attn_fwd / attn_bwd are one kernel
+    # each; the GEMMs are compared shape by shape (the largest GEMM shape's total); the others sit beside it
+    single = {k: stats[k]["total_ms"] for k in ("attn_fwd", "attn_bwd")}
+    single["gemm"] = max((t for _, t, _ in gemm_keys.values()), default=0.0)
+    dom = max(single, key=single.get)
+    np_avg = sum((W // 16) * (H // 16) for W, H in buckets) / len(buckets)
     step_tflop = train_flops_per_image(np_avg) * args.batch / 1e12
+    wl = ("JiT-B/16 (JiT_B_16_Config) training step, 512^2 single bucket (BASELINE config 2)" if c2 else
+          "JiT-B/16 (JiT_B_16_Config) training step, 1024^2 area, 5 aspect-ratio buckets, rank-interleaved "
+          "shared shuffled order")
     result = {
-        "metric": METRIC, "value": round(value, 3), "unit": "img/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (HBM-resident, random-init weights)",
-        "config": {"workload": "JiT-B/16 (JiT_B_16_Config) training step, 1024^2 area, 5 aspect-ratio buckets round-robin",
-                   "model": "JiT-B/16", "per_gpu_batch": args.batch, "global_batch": args.batch * world,
-                   "seq_len": "4042-4170 tokens", "buckets_wh": BUCKETS, "parallelism": f"dp{world}",
-                   "loss_target": "image", "optimizer": "RAdamScheduleFree (fused HIP)",
-                   "grad_allreduce": "bf16 wire, per-block buckets overlapped with backward" if world > 1 else None, "grad_checkpointing": bool(args.grad_ckpt)},
-        "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-                     "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
-                     "algorithmic_gflop_per_launch": round(stats[dom]["mean_gflop"], 3),
-                     "mean_launch_ms": round(stats[dom]["mean_ms"], 4)},
+        "metric": METRIC_C2 if c2 else METRIC, "value": round(value, 3), "unit": "img/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (HBM-resident, random-init weights)",
+        "config": {"workload": wl, "model": "JiT-B/16", "per_gpu_batch": args.batch, "global_batch": args.batch * world,
+                   "seq_len": "1034-1098 tokens" if c2 else "4042-4170 tokens", "buckets_wh": buckets,
+                   "parallelism": f"dp{world}", "loss_target": "image", "optimizer": "RAdamScheduleFree (fused HIP)",
+                   "optimizer_overlap": "per bucket on a side stream during backward" if overlap else
+                   "one launch after the backward",
+                   "grad_allreduce": "bf16 wire, per-block buckets overlapped with backward" if world > 1 else None,
+                   "grad_checkpointing": bool(args.grad_ckpt)},
+        "roofline": roofline_entry(dom, stats[dom], args.workload),
+        "roofline_others": {k: roofline_entry(k, stats[k], args.workload) for k in mfma_ops if k != dom},
         "kernels": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in stats.items()},
         "hbm_kernels": hbm,
         "probe_pass": f"{n_probe} steps after the timed region, HIP events on the launching stream",
-        "model_tflops_per_gpu": round(step_tflop * args.steps / (dt) , 2),
+        "model_tflops_per_gpu": round(step_tflop * args.steps / (dt), 2),
         "mfu": round(step_tflop * args.steps / dt / PEAK_BF16_TFLOPS, 4),
         "final_loss": round(loss, 5),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline()
+        result["cpu_baseline"] = cpu_baseline(buckets=buckets)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -259,51 +309,65 @@ def main():
 
 
 def bench_c5(args):
-    """BASELINE config 5 on one GPU: the SDXL QLoRA step over the UNet's 11 SpatialTransformers (70 blocks,
-    700 LoRA r=16 targets, NF4 bases dequantised inside the GEMMs) at the 1024^2 stage shapes, batch 4
-    (configs/sdxl/flow_match/config.yml), RAdamScheduleFree on the adapters (vpt/sdxl_train.py). The UNet's
-    conv / ResNet path, VAE and text encoders are outside SURVEY §8 and not executed (synthetic stage inputs)."""
+    """BASELINE config 5 on one GPU: the SDXL flow-matching QLoRA step (train/sdxl/flow_match.py:109-174) at
+    1024^2 (latents 4 x 128 x 128), batch 4 (configs/sdxl/flow_match/config.yml): t ~ scale_shift_sigmoid,
+    noising, the UNet's 11 SpatialTransformers (70 blocks, 700 LoRA r=16 targets, NF4 bases dequantised inside
+    the GEMMs) inside a frozen skeleton of the UNet's topology (its ResNet / conv path is outside SURVEY §8),
+    velocity MSE, backward, RAdamScheduleFree on the adapters (vpt/sdxl_flow.py)."""
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         raise SystemExit("--workload c5 is a 1-GPU configuration")
     torch.cuda.set_device(0)
     from vpt import ops
-    from vpt.sdxl_train import SDXLStacksQLoRA
+    from vpt.sdxl_flow import SDXLFlowMatchQLoRA
     B = 4
-    m = SDXLStacksQLoRA(B=B, device="cuda", seed=0)
-    xs, ctx, gs = m.make_inputs(seed=1)
+    m = SDXLFlowMatchQLoRA(B=B, device="cuda", seed=0)
+    lat, ctx, pooled, sizes = m.make_inputs(seed=1)
     for _ in range(args.warmup):
-        m.step(xs, ctx, gs)
+        m.step(lat, ctx, pooled, sizes)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        m.step(xs, ctx, gs)
+        m.step(lat, ctx, pooled, sizes)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    # probe pass after the timed region: NF4 GEMM launches timed with HIP events on the launching stream
-    pr = ops.KernelProbe("gemm_nf4")
-    ops.PROBES["gemm_nf4"] = pr
-    pr.active = True
-    m.step(xs, ctx, gs)
+    loss = m.loss.item()
+    # probe pass after the timed region: NF4 GEMM and attention launches timed with HIP events
+    probes = {k: ops.KernelProbe(k) for k in ("gemm_nf4", "attn_fwd", "attn_bwd", "gemm")}
+    ops.PROBES.update(probes)
+    for p in probes.values():
+        p.active = True
+    m.step(lat, ctx, pooled, sizes)
     torch.cuda.synchronize()
-    pr.active = False
+    for p in probes.values():
+        p.active = False
     ops.PROBES.clear()
-    n, ms, fl = pr.summary()
+    kern = {}
+    for k, pr in probes.items():
+        n, ms, fl = pr.summary()
+        kern[k] = dict(launches=n, mean_ms=round(ms, 4), total_ms=round(n * ms, 3),
+                       tflops=round(fl / (ms * 1e-3) / 1e12, 2) if ms else 0.0)
+    n, ms, fl = probes["gemm_nf4"].summary()
     tf = fl / (ms * 1e-3) / 1e12 if ms else 0.0
     step_tf = m.flops_per_step() / 1e12
     res = {
-        "metric": "train images/sec, SDXL QLoRA r=16 transformer stacks (NF4 bases, 1024^2 stage shapes), 1 MI355X",
+        "metric": "train images/sec, SDXL QLoRA r=16 flow-matching step (1024^2, latents 4x128x128), 1 MI355X",
         "value": round(B * args.steps / dt, 3), "unit": "img/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "bf16 (NF4 weights)", "data": "synthetic stage activations / context / output grads, random-init weights",
-        "config": {"workload": "BASELINE config 5 transformer part: 11 SpatialTransformers (70 blocks, 700 LoRA targets), "
-                               "context 231x2048, UNet conv/ResNet path, VAE and text encoders not executed",
+        "dtype": "bf16 (NF4 weights)", "data": "synthetic latents / text context / pooled output, random-init weights",
+        "config": {"workload": "BASELINE config 5: t ~ scale_shift_sigmoid(-0.8, 0.8), z = t x + (1 - t) eps, "
+                               "v = UNet(z, 1000 t, ctx 231x2048, pooled, sizes), loss = mse(v, eps - x); the UNet's "
+                               "11 SpatialTransformers (70 blocks, 700 LoRA targets) with the reference's "
+                               "conditioning path, its ResNet / conv / resample path replaced by frozen "
+                               "pixel-(un)shuffle + Linear maps (outside SURVEY §8); VAE and text encoders not run",
                    "global_batch": B, "lora_rank": 16, "lora_alpha": 1.0, "adapter_params": m.n_adapter_params(),
+                   "loss": "flow-matching velocity MSE (loss_with_predicted_velocity)",
                    "optimizer": "RAdamScheduleFree (fused HIP)"},
         "roofline": {"bound": "mfma", "kernel": "gemm_nf4", "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(tf / PEAK_BF16_TFLOPS, 4), "traffic": None,
                      "mean_launch_ms": round(ms, 4), "launches_per_step": n},
+        "kernels": kern,
         "model_tflops_per_step": round(step_tf, 3), "model_tflops_per_s": round(step_tf * args.steps / dt, 2),
-        "mfu": round(step_tf * args.steps / dt / PEAK_BF16_TFLOPS, 4),
+        "mfu": round(step_tf * args.steps / dt / PEAK_BF16_TFLOPS, 4), "final_loss": round(loss, 5),
     }
     print(json.dumps(res), flush=True)
 

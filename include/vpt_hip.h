@@ -183,11 +183,21 @@ int vpt_cast_f32_bf16(const float* in, long n, void* out, void* stream);
  * src/trainer/common.py:276-285,382-388). */
 int vpt_radam_sf_step(void* y, const void* grad, int grad_bf16, float* z, float* v, long n, float beta2,
                       float bias_correction2, float eps, float ckp1, float adaptive_y_lr, float lr, float decay,
-                      float grad_scale, int adam, void* stream);
+                      float grad_scale, int adam, const float* clip_coef, float clip_value, void* stream);
+/* Gradient clipping (src/models/for_training.py:98-109 after_backward: accelerator.clip_grad_norm_ /
+ * clip_grad_value_, src/config.py:74-75): the step above multiplies g by *clip_coef (device scalar; null =
+ * none) and then clamps it to [-clip_value, clip_value] (0 = none). The global norm is taken over all
+ * (all-reduced, mean) gradient buckets: vpt_grad_sumsq writes vpt_grad_norm_blocks() partial sums of
+ * (scale * g)^2 of one bucket into part; vpt_clip_coef sums n partials in a fixed order and writes
+ * coef = min(1, max_norm / (norm + 1e-6)) (torch.nn.utils.clip_grad_norm_) and, if norm_out, the norm. */
+int vpt_grad_norm_blocks(void);
+int vpt_grad_sumsq(const void* g, int g_bf16, long n, float scale, float* part, void* stream);
+int vpt_clip_coef(const float* part, int n, float max_norm, float* coef, float* norm_out, void* stream);
 int vpt_sf_lerp(void* y, const float* z, long n, float w, void* stream);
 /* EMA copy of the flat bf16 parameters (swa_utils.AveragedModel(get_ema_avg_fn(decay)), use_buffers=False;
- * src/trainer/common.py:211-216, 385-386): first = 1 copies, else ema = bf16(bf16(d*ema) + bf16((1-d)*p)). */
-int vpt_ema_update(void* ema, const void* param, long n, float decay, int first, void* stream);
+ * src/trainer/common.py:211-216, 385-386): first = 1 copies, else ema = bf16(bf16(d*ema) + bf16(omd*p)); omd = the caller's
+ * f32 rounding of (1 - decay) formed in double (torch rounds the Python scalar 1 - decay, not 1 - f32(decay)). */
+int vpt_ema_update(void* ema, const void* param, long n, float decay, float one_minus_decay, int first, void* stream);
 int vpt_sf_init(const void* y, float* z, float* v, long n, void* stream);
 
 
@@ -258,6 +268,25 @@ int vpt_groupnorm_fwd(const void* x, const void* w, const void* b, void* y, floa
 int vpt_groupnorm_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const void* w,
                       const void* dres, void* dx, int B, int C, int G, long HW, void* stream);
 int vpt_transpose_add(const void* src, const void* add, void* dst, int B, int R, int S, void* stream);
+/* SDXL flow-matching step around the UNet (train/sdxl/flow_match.py:109-174):
+ * vpt_flow_noise     prepare_scaled_noised_latents (src/modules/loss/flow_match.py:60-74) on bf16 latents x
+ *                    [B][n_per_sample]: eps = bf16(bf16(randn) * noise_scale) from a counter RNG (seed), or the
+ *                    caller's eps_in; z = t x + (1 - t) eps (clean_at_zero: (1 - t) x + t eps), f32 math,
+ *                    bf16 out; t [B] f32 in (0, 1). eps_out receives the generated noise (needed by the loss).
+ * vpt_velocity_loss  loss_with_predicted_velocity (flow_match.py:85-96): *loss = mean((v - bf16(eps - x))^2)
+ *                    (f32, fixed-order block sums in part[vpt_velocity_loss_blocks()]); dv (optional) =
+ *                    bf16(2 (v - target) / n), the gradient of the mean. n % 8 == 0.
+ * vpt_sinusoid_embed get_timestep_embedding(vals, dim, flip_sin_to_cos=True, downscale_freq_shift=0)
+ *                    (src/modules/timestep/embedding.py:10-62 via src/models/sdxl/denoiser.py:1117-1123) -> bf16.
+ * vpt_space_to_depth NCHW bf16 [B][C][H][W] -> token-major [B][(H/r)(W/r)][C r r] (feature (c r + i) r + j =
+ *                    pixel_unshuffle order); inverse = 1 maps tokens back to NCHW (pixel_shuffle), its adjoint. */
+int vpt_flow_noise(const void* x, const float* t, long n_per_sample, int B, float noise_scale, int clean_at_zero,
+                   unsigned long long seed, const void* eps_in, void* z, void* eps_out, void* stream);
+int vpt_velocity_loss_blocks(void);
+int vpt_velocity_loss(const void* v, const void* x, const void* eps, long n, void* dv, float* part, float* loss,
+                      void* stream);
+int vpt_sinusoid_embed(const float* vals, int R, int dim, void* out, void* stream);
+int vpt_space_to_depth(const void* src, void* dst, int B, int C, int H, int W, int r, int inverse, void* stream);
 /* Elementwise bf16: out = a + b (residual sums), out = s * a (LoRA scale gradient); n % 8 == 0. */
 int vpt_add_bf16(const void* a, const void* b, long n, void* out, void* stream);
 int vpt_scale_bf16(const void* a, long n, float s, void* out, void* stream);

@@ -223,3 +223,67 @@ def spatial_forward(x, ctx, w, heads, depth, rank, alpha, head_dim=64, groups=32
         h = block_forward(h, ctx, wb, heads, rank, alpha, head_dim)
     h = F.linear(h, w["proj_out.weight"], w["proj_out.bias"])
     return h.reshape(B, H, W, C).permute(0, 3, 1, 2) + x
+
+
+# ---------------------------------------------------------------------------- flow-matching step (config 5)
+def sinusoid(t: torch.Tensor, dim: int, max_period: int = 10000) -> torch.Tensor:
+    """get_timestep_embedding(t, dim, flip_sin_to_cos=True, downscale_freq_shift=0)
+    (src/modules/timestep/embedding.py:10-62, called at src/models/sdxl/denoiser.py:1117-1123)."""
+    half = dim // 2
+    expo = -math.log(max_period) * torch.arange(0, half, dtype=torch.float32) / half
+    emb = t[:, None].float() * torch.exp(expo)[None, :]
+    return torch.cat([torch.cos(emb), torch.sin(emb)], dim=-1)
+
+
+def flow_match_loss(latents, t, eps, ctx, pooled, sizes, sk, stacks, rank, alpha, noise_scale=1.0):
+    """SDXLForFlowMatchingTraining.train_step (train/sdxl/flow_match.py:109-174) in fp32 on the skeleton UNet of
+    vpt/sdxl_flow.py (the §8 transformer stacks, the reference's conditioning MLPs and emb_layers adds; frozen
+    pixel-(un)shuffle + Linear maps in place of the conv / ResNet / resample path, skips as additions):
+      z = t x + (1 - t) eps (prepare_scaled_noised_latents, flow_match.py:60-74), model timestep t * 1000,
+      loss = mse(v, eps - x) (loss_with_predicted_velocity, flow_match.py:85-96).
+    sk: the skeleton's weights {t1, t2, l1, l2, e_in, e_down, e_up, m_in, m_down, m_up, m_out} as (W, b|None);
+    stacks: 11 (weights, heads, depth) in SDXL order (2 + 2 down, mid, 3 + 3 up)."""
+    B, _, L, _ = latents.shape
+    x = latents.float()
+    tt = t.float().view(B, 1, 1, 1)
+    z = tt * x + (1 - tt) * eps.float() * noise_scale
+
+    def lin(name, h, bias=True):
+        W, b = sk[name]
+        return F.linear(h, W, b if bias else None)
+
+    temb = lin("t2", F.silu(lin("t1", sinusoid(t * 1000.0, 320))))
+    add = sinusoid(sizes.reshape(-1).float(), 256).reshape(B, -1)
+    glob = lin("l2", F.silu(lin("l1", torch.cat([pooled.float(), add], 1)))) + temb
+    sg = F.silu(glob)
+    eA, eB, eU = lin("e_in", sg), lin("e_down", sg), lin("e_up", sg)
+
+    def st(i, h):
+        w, heads, depth = stacks[i]
+        return spatial_forward(h, ctx, w, heads, depth, rank, alpha)
+
+    def tok_lin(name, h_nchw, r, emb=None):
+        """pixel_unshuffle(h, r) -> tokens -> Linear (+ per-sample emb) -> NCHW at the unshuffled size."""
+        u = F.pixel_unshuffle(h, r) if r > 1 else h
+        Bn, Cf, Hh, Ww = u.shape
+        y = lin(name, u.permute(0, 2, 3, 1).reshape(Bn, Hh * Ww, Cf), bias=True)
+        if emb is not None:
+            y = y + emb[:, None, :]
+        return y.reshape(Bn, Hh, Ww, -1).permute(0, 3, 1, 2)
+
+    x64 = tok_lin("m_in", z, 2, eA)
+    e0 = st(0, x64)
+    e1 = st(1, e0)
+    x32 = tok_lin("m_down", e1, 2, eB)
+    d0 = st(2, x32)
+    d1 = st(3, d0)
+    m = st(4, d1)
+    u0 = st(5, m + d1)
+    u1 = st(6, u0 + d0)
+    u2 = st(7, u1 + x32)
+    y64 = F.pixel_shuffle(tok_lin("m_up", u2, 1, eU), 2)
+    v0 = st(8, y64 + e1)
+    v1 = st(9, v0 + e0)
+    v2 = st(10, v1 + x64)
+    v = F.pixel_shuffle(tok_lin("m_out", v2, 1), 2)
+    return F.mse_loss(v, eps.float() * noise_scale - x), v

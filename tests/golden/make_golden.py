@@ -30,6 +30,9 @@ Fixtures:
                          flux_shift samplers (two latent shapes, two global-RNG seeds, non-default kwargs).
   init.safetensors       JiT.initialize_weights + ClassEncoder.initialize_weights on the micro config: per
                          parameter the kind (normal / ones / zeros), mean, std, numel.
+  ref_bf16_error.safetensors  the reference's own bf16-autocast step vs its fp32 step on the GPU parity
+                         test's cases (micro, C1, JiT-B/16 256^2 B=2 and 1024^2 B=1): per-parameter gradient
+                         rel-L2, prediction and loss rel (`make_golden.py bf16err`).
   sampler.safetensors    JiTModel.generate (src/models/jit/pipeline.py:378-488) on the micro config,
                          float32 execution, class context, 4 Euler steps, 2 x 64x48: starting noise,
                          token ids/masks and the final image for four cases (CFG 2.0; no CFG; CFG 3.0
@@ -423,9 +426,84 @@ def init_fixture(R, meta):
               metadata=dict(meta, names=json.dumps(names)))
 
 
+def run_reference_bf16(R, oc: OracleConfig, weights, batch, loss_target):
+    """The reference as its trainer runs it (SURVEY gotcha #5): bf16 weights, forward and backward under
+    bf16 autocast (accelerate mixed_precision=bf16, src/trainer/common.py:322), fp16 images, fp32 loss."""
+    model = R.den.Denoiser(ref_config(R, oc))
+    sd = {k: v for k, v in weights.items() if not k.startswith("class_encoder.")}
+    model.load_state_dict(sd, strict=True)
+    model = model.to(torch.bfloat16)
+    model.train()
+    emb = weights["class_encoder.embedding.weight"].clone().to(torch.bfloat16).requires_grad_(True)
+    x, t = batch["image"], batch["t"]
+    orig = torch.randn_like
+    torch.randn_like = lambda ten, *a, **k: batch["noise"].to(ten.dtype)
+    try:
+        z, _ = R.fm.prepare_scaled_noised_latents(latents=x, timestep=t, noise_scale=1.0)
+    finally:
+        torch.randn_like = orig
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        ctx = F.embedding(batch["ids"], emb, padding_idx=emb.shape[0] - 1)
+        pred = model(image=z, timestep=t.to(torch.bfloat16), context=ctx, original_size=batch["original_size"],
+                     target_size=batch["target_size"], crop_coords=batch["crop_coords"], context_mask=batch["mask"])
+        assert loss_target == "image"
+        loss = F.mse_loss(pred, x)
+    loss.backward()
+    grads = {n: p.grad.detach().float().clone() for n, p in model.named_parameters()}
+    grads["class_encoder.embedding.weight"] = emb.grad.detach().float().clone()
+    return loss.detach().float(), pred.detach().float(), grads
+
+
+def bf16_error_fixture(R, meta):
+    """How far the REFERENCE's own bf16-autocast training step is from its fp32 step, per parameter gradient
+    (whole-tensor rel-L2), prediction and loss -- on the exact cases tests/test_parity_gpu.py runs. The GPU
+    parity test holds the HIP step to SURVEY §8(c)'s bar, except on a parameter where the reference's own bf16
+    step is already further than that bar from fp32."""
+    from oracle.jit_oracle import jit_b16
+    cases = {"micro": (micro_config(), 20, 1, dict(B=2, H=64, W=48, n_ctx=8, seed=2)),
+             "c1": (c1_config(), 1000, 3, dict(B=4, H=256, W=256, n_ctx=64, seed=4, padded_rows=(1, 3))),
+             "jitb16-256x256-B2": (jit_b16(), 1000, 11, dict(B=2, H=256, W=256, n_ctx=64, seed=12)),
+             "jitb16-1024x1024-B1": (jit_b16(), 1000, 11, dict(B=1, H=1024, W=1024, n_ctx=64, seed=12))}
+    # every other GPU parity case the CPU's memory holds (B = 8 at 1024^2 does not: the parity test bounds it
+    # with the largest per-parameter entry over the five 1024^2 B = 2 buckets)
+    for (H, W, B) in [(1024, 1024, 2), (1088, 960, 2), (960, 1088, 2), (896, 1152, 2), (1152, 896, 2), (512, 512, 16)]:
+        cases[f"jitb16-{W}x{H}-B{B}"] = (jit_b16(), 1000, 11, dict(B=B, H=H, W=W, n_ctx=64, seed=12))
+    only = os.environ.get("BF16ERR_CASES")
+    if only:
+        cases = {k: v for k, v in cases.items() if k in only.split(",")}
+    path = os.path.join(HERE, "ref_bf16_error.safetensors")
+    out, names = {}, {}
+    if os.path.exists(path):  # incremental: keep the cases already computed
+        from safetensors import safe_open
+        from safetensors.torch import load_file
+        with safe_open(path, "pt") as f:
+            names = json.loads(f.metadata()["names"])
+        out = dict(load_file(path))
+    for case, (oc, V, wseed, bk) in cases.items():
+        if case in names:
+            continue
+        w = make_weights(oc, seed=wseed, n_classes=V)
+        kw = {k: v for k, v in bk.items() if k not in ("B", "H", "W", "n_ctx", "seed")}
+        batch = make_batch(oc, bk["B"], bk["H"], bk["W"], bk["n_ctx"], V, seed=bk["seed"], **kw)
+        l32, p32, _, g32 = run_reference(R, oc, w, batch, "image")
+        l16, p16, g16 = run_reference_bf16(R, oc, w, batch, "image")
+        order = sorted(g32)
+        names[case] = order
+        rels = [((g16[n] - g32[n].float()).norm() / g32[n].float().norm().clamp_min(1e-30)).item() for n in order]
+        out[f"{case}/grad_rel"] = torch.tensor(rels, dtype=torch.float64)
+        out[f"{case}/pred_rel"] = ((p16 - p32).norm() / p32.norm()).double().reshape(1)
+        out[f"{case}/loss_rel"] = ((l16 - l32).abs() / l32).double().reshape(1)
+        print(case, "pred", out[f"{case}/pred_rel"].item(), "loss", out[f"{case}/loss_rel"].item(),
+              "worst grad", max(zip(rels, order)), flush=True)
+        save_file(out, path, metadata=dict(meta, names=json.dumps(names)))
+
+
 def main():
     R = import_reference()
     meta = {"torch": torch.__version__, "threads": str(torch.get_num_threads()), "reference": REF}
+    if len(sys.argv) > 1 and sys.argv[1] == "bf16err":
+        bf16_error_fixture(R, meta)
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "sampler":
         sampler_fixture(R, meta)
         print("sampler", os.path.getsize(os.path.join(HERE, "sampler.safetensors")))

@@ -132,3 +132,162 @@ def test_two_rank_gradient_mean_equals_single_rank_big_batch(wire):
         assert first is None
         assert abs(second - (l0 + l1) / 2) < 1e-6 * abs(l0 + l1)
         assert abs(third - 3 * (l0 + l1) / 2) < 1e-6 * abs(l0 + l1)
+
+
+# ----------------------------------------------------------------------- overlap, clipping, sharded order
+def _grad_worker(rank, world, port, q, mode):
+    """Each rank holds its own flat gradient over the micro layout; GradSync reduces the mean, lands every
+    bucket as it is launched (overlap) or at finish (serial), with optional global-norm / value clipping; the
+    callback applies the clip exactly as the optimizer kernel does (g * scale * coef, then clamp)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from vpt.ddp import GradSync, grad_buckets
+    from vpt.params import ParamLayout
+    cfg = _vcfg(GC.micro_config())
+    lay = ParamLayout(cfg, 20)
+    g = torch.Generator().manual_seed(100 + rank)
+    grads = torch.randn(lay.total, generator=g) * (1.0 + rank)
+    mine = grads.clone()  # the all-reduce sums in place
+    overlap, norm, value, accum = mode
+    sync = GradSync(grads, grad_buckets(lay, cfg.depth), overlap=overlap, clip_grad_norm=norm, clip_grad_value=value)
+    out = torch.full_like(grads, float("nan"))
+    order = []
+
+    def apply(lo, hi, sc, gr, clip_coef=None, clip_value=None):
+        order.append((lo, hi))
+        e = gr.float() * sc
+        if clip_coef is not None:
+            e = e * clip_coef
+        if clip_value:
+            e = e.clamp(-clip_value, clip_value)
+        out[lo:hi] = e
+
+    sync.arm(apply, 1.0 / accum)
+    landed_during_backward = []
+    for name, _, _ in sync.buckets[:-2]:  # the engine's on_ready calls, in completion order
+        sync.launch(name)
+        landed_during_backward.append(len(order))
+    sync.launch_rest()
+    sync.finish()
+    q.put((rank, mine.numpy(), out.numpy(), order, landed_during_backward,
+           sync.norm.item() if norm is not None else None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _spawn(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q, *args)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(out, key=lambda t: t[0])
+
+
+@pytest.mark.parametrize("mode", [(True, None, None, 1), (False, None, None, 1), (True, 1.0, None, 2),
+                                  (False, 1.0, None, 1), (True, None, 0.05, 1), (True, 0.5, 0.02, 2)],
+                         ids=["overlap", "serial", "overlap-clipnorm-accum2", "serial-clipnorm", "overlap-clipvalue",
+                              "overlap-clipnorm-clipvalue-accum2"])
+def test_two_rank_overlap_and_clipping_match_reference_semantics(mode):
+    """World 2 over gloo: the mean gradient (SUM all-reduce x 1/world x 1/accum) with after_backward's
+    clip_grad_norm_ then clip_grad_value_ (src/models/for_training.py:98-109) equals torch's own clipping of
+    the mean gradient; with overlap every bucket is stepped as it is launched (none left for finish() except
+    the two launched after the backward), unless global-norm clipping needs every bucket first."""
+    overlap, norm, value, accum = mode
+    res = [(r[0], torch.from_numpy(r[1]), torch.from_numpy(r[2]), *r[3:]) for r in _spawn(_grad_worker, 2, mode)]
+    g_mean = (res[0][1] + res[1][1]) / 2 / accum
+    ref = g_mean.clone()
+    p = torch.nn.Parameter(torch.zeros_like(ref))
+    p.grad = ref
+    if norm is not None:
+        tn = torch.nn.utils.clip_grad_norm_([p], norm)
+        assert abs(res[0][5] - tn.item()) <= 1e-4 * tn.item()  # f32 sums in another order
+    if value is not None:
+        torch.nn.utils.clip_grad_value_([p], value)
+    for r in range(2):
+        out, order, landed = res[r][2], res[r][3], res[r][4]
+        assert torch.allclose(out, p.grad, rtol=1e-5, atol=1e-7), (r, (out - p.grad).abs().max())
+        spans = sorted(order)
+        assert spans[0][0] == 0 and all(a[1] == b[0] for a, b in zip(spans, spans[1:]))  # each bucket once
+        if overlap and norm is None:
+            assert landed == list(range(1, len(landed) + 1))  # stepped during the backward, bucket by bucket
+        else:
+            assert all(n == 0 for n in landed)  # nothing stepped before finish()
+    assert torch.equal(res[0][2], res[1][2])
+
+
+def test_bench_shared_order_is_rank_interleaved():
+    """bench.py's bucket schedule = accelerate prepare_data_loader over one shared seeded shuffle: the ranks'
+    per-step draws interleave one permutation per epoch (so ranks hold different buckets in the same step), and
+    world 1 is the plain per-epoch shuffle (every bucket once per epoch)."""
+    import bench
+    steps, nb = 20, 5
+    for world in (1, 2, 4):
+        per = [bench.shared_order(nb, steps, world, r) for r in range(world)]
+        for e in range(steps // nb):
+            merged = [per[j % world][e * nb + j // world] for j in range(nb * world)]
+            assert sorted(merged) == sorted(i % nb for i in range(nb * world))  # one epoch = the shuffled list
+        if world == 1:
+            assert all(per[0].count(b) == steps // nb for b in range(nb))
+    two = [bench.shared_order(nb, steps, 2, r) for r in range(2)]
+    assert any(a != b for a, b in zip(*two))  # different buckets on the two ranks in some step
+
+
+def _save_worker(rank, world, port, q, tmp):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import types
+    from vpt.trainer import JiTTrainLoop, SafetensorsSaver
+    from vpt.params import ParamLayout
+    cfg = _vcfg(GC.micro_config())
+    lay = ParamLayout(cfg, 20)
+    eng = types.SimpleNamespace(layout=lay, params=torch.full((lay.total,), float(rank)))
+    loop = JiTTrainLoop.__new__(JiTTrainLoop)  # only the save path (no engine / optimizer needed)
+    loop.trainer = types.SimpleNamespace(engine=eng)
+    loop.savers = [SafetensorsSaver("jit", tmp)]
+    loop.ema_savers, loop.ema, loop.saved = [], None, []
+    loop._save(1, 4)
+    q.put((rank, list(loop.saved)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_checkpoint_saved_by_rank0_only(tmp_path):
+    """common.py:390-423: wait_for_everyone, save on the main process only, wait_for_everyone."""
+    from safetensors.torch import load_file
+    res = _spawn(_save_worker, 2, str(tmp_path))
+    assert len(res[0][1]) == 1 and res[1][1] == []
+    files = sorted(os.listdir(tmp_path))
+    assert files == ["jit_00001e_000004s.safetensors"]
+    sd = load_file(os.path.join(tmp_path, files[0]))
+    assert all(float(v.float().abs().max()) == 0.0 for v in sd.values())  # rank 0's replica
+
+
+def test_integration_md_optimizer_callback_matches_gradsync():
+    """The INTEGRATION.md §3 snippet's callback is called by GradSync with the arguments it passes (the round-2
+    example had a 3-parameter lambda for a 4-argument call)."""
+    import re
+    import types
+    from vpt.ddp import GradSync, grad_buckets
+    from vpt.params import ParamLayout
+    text = open(os.path.join(os.path.dirname(os.path.dirname(__file__)), "INTEGRATION.md")).read()
+    lam = re.search(r"sync\.arm\((lambda [^\n]*\))\)\n", text).group(1)
+    calls = []
+    opt = types.SimpleNamespace(apply_range=lambda s, lo, hi, sc, g, **kw: calls.append((lo, hi, sc, kw)))
+    fn = eval(lam, {"opt": opt, "s": {}})
+    cfg = _vcfg(GC.micro_config())
+    lay = ParamLayout(cfg, 20)
+    for clip in ({}, {"clip_grad_norm": 1.0, "clip_grad_value": 0.5}):
+        calls.clear()
+        sync = GradSync(torch.randn(lay.total), grad_buckets(lay, cfg.depth), **clip)
+        sync.arm(fn)
+        for n, _, _ in sync.buckets:
+            sync.launch(n)
+        sync.finish()
+        assert sum(hi - lo for lo, hi, _, _ in calls) == lay.total
+        assert all(set(kw) == ({"clip_coef", "clip_value"} if clip else set()) for *_, kw in calls)

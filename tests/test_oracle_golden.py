@@ -155,3 +155,23 @@ def test_rope_out_of_range_bucket_raises():
     """SURVEY gotcha #8: buckets wider than 2048 px overflow rope_axes_lens=128."""
     with pytest.raises(IndexError):
         O.rope_freqs(O.jit_b16(), 2368 // 16, 448 // 16, 64)
+
+
+def test_reference_bf16_error_fixture_covers_every_parameter():
+    """ref_bf16_error.safetensors (the reference's own bf16-autocast step vs its fp32 step, which the GPU parity
+    bar falls back to on the cancelling key-path gradients) names every gradient of each case's model."""
+    import json
+    from safetensors import safe_open
+    from safetensors.torch import load_file
+    path = os.path.join(os.path.dirname(__file__), "golden", "ref_bf16_error.safetensors")
+    with safe_open(path, "pt") as f:
+        names = json.loads(f.metadata()["names"])
+    fx = load_file(path)
+    cfgs = {"micro": (GC.micro_config(), 20), "c1": (GC.c1_config(), 1000), "jitb16-256x256-B2": (O.jit_b16(), 1000),
+            "jitb16-1024x1024-B1": (O.jit_b16(), 1000)}
+    for case, (oc, V) in cfgs.items():
+        w = O.make_weights(oc, seed=1, n_classes=V)
+        assert sorted(names[case]) == sorted(w), case
+        r = fx[f"{case}/grad_rel"]
+        assert r.numel() == len(w) and bool((r > 0).all()) and bool((r < 0.1).all())
+        assert fx[f"{case}/loss_rel"].item() < 1e-4 and fx[f"{case}/pred_rel"].item() < 3e-2

@@ -341,17 +341,21 @@ def test_lora_skinny_kernels_vs_torch(ops, M, K, N):
     assert rel(g_down, -0.5 + 3.0 * vs.float().t() @ x.float()) < 1e-5
     ops.lora_wgrad2(dy, ds, g_up, x, vs, g_down, accumulate=False)
     assert rel(g_up, dy.float().t() @ ds.float()) < 1e-5 and rel(g_down, vs.float().t() @ x.float()) < 1e-5
-    # batched reduces (lora_wgrad_batch: split-M slabs per target, one reduce launch for all): bit-identical,
-    # for 17 targets (34 jobs: two launches) and with a flush forced by a change of alpha
-    gu = [torch.full((N, 16), 0.25, device=DEV) for _ in range(18)]
-    gd = [torch.full((16, K), -0.5, device=DEV) for _ in range(18)]
+    # batched reduces (lora_wgrad_batch: split-M slabs per target, one reduce launch per 32 jobs): bit-identical
+    # to the per-target path, over 52 targets with distinct inputs (4 flushes: workspace names are re-issued
+    # after each, so a slab still pending reduction must never be handed out again) and a flush forced by a
+    # change of alpha
+    T = 52
+    dss = [ds.roll(i, 0) for i in range(T)]
+    vss = [vs.roll(-i, 0) for i in range(T)]
+    gu = [torch.full((N, 16), 0.25, device=DEV) for _ in range(T)]
+    gd = [torch.full((16, K), -0.5, device=DEV) for _ in range(T)]
     with ops.lora_wgrad_batch():
-        for i in range(17):
-            ops.lora_wgrad2(dy, ds, gu[i], x, vs, gd[i], accumulate=True, alpha=3.0)
-        ops.lora_wgrad2(dy, ds, gu[17], x, vs, gd[17], accumulate=False)
-    ref_u, ref_d = torch.full((N, 16), 0.25, device=DEV), torch.full((16, K), -0.5, device=DEV)
-    ops.lora_wgrad2(dy, ds, ref_u, x, vs, ref_d, accumulate=True, alpha=3.0)
-    for i in range(17):
+        for i in range(T - 1):
+            ops.lora_wgrad2(dy, dss[i], gu[i], x, vss[i], gd[i], accumulate=True, alpha=3.0)
+        ops.lora_wgrad2(dy, dss[T - 1], gu[T - 1], x, vss[T - 1], gd[T - 1], accumulate=False)
+    for i in range(T):
+        ref_u, ref_d = torch.full((N, 16), 0.25, device=DEV), torch.full((16, K), -0.5, device=DEV)
+        last = i == T - 1
+        ops.lora_wgrad2(dy, dss[i], ref_u, x, vss[i], ref_d, accumulate=not last, alpha=1.0 if last else 3.0)
         assert torch.equal(gu[i], ref_u) and torch.equal(gd[i], ref_d), i
-    ops.lora_wgrad2(dy, ds, ref_u, x, vs, ref_d, accumulate=False)
-    assert torch.equal(gu[17], ref_u) and torch.equal(gd[17], ref_d)

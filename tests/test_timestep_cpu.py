@@ -40,6 +40,14 @@ def test_sampler_rejects_foreign_kwargs():
         sample_timestep((4, 3, 8, 8), "cpu", "bogus")
 
 
+def test_uniform_ignores_kwargs_like_the_dispatcher():
+    # sampling.py:183-184 calls uniform_rand(latents_shape, device) without **kwargs
+    from vpt.timestep import sample_timestep
+    a = sample_timestep((5, 3, 8, 8), "cpu", "uniform", generator=torch.Generator().manual_seed(1), sigmoid_scale=2.0)
+    b = sample_timestep((5, 3, 8, 8), "cpu", "uniform", generator=torch.Generator().manual_seed(1))
+    assert torch.equal(a, b) and a.shape == (5,)
+
+
 def test_scale_shift_sigmoid_distribution():
     # JiT's sampler (config.yml timestep_sampling): logit-normal with mean -0.8, std 0.8
     t = sample_timestep((200000, 3, 8, 8), "cpu", "scale_shift_sigmoid", generator=torch.Generator().manual_seed(1))

@@ -75,17 +75,19 @@ def test_train_loop_saving_ema_and_optimizer_modes(tmp_path):
     assert loop.ema.n_averaged == 4
 
 
-def test_ema_kernel_matches_bf16_reference_arithmetic():
+@pytest.mark.parametrize("decay", [0.9, 0.9999])
+def test_ema_kernel_matches_bf16_reference_arithmetic(decay):
+    """0.9999 is the reference default (src/config.py ema_decay): torch rounds the Python double 1 - decay."""
     from vpt import ops
     g = torch.Generator(device=DEV).manual_seed(3)
     p = torch.randn(100003, device=DEV, generator=g).bfloat16()
     ema = torch.empty_like(p)
-    ops.ema_update(ema, p, 0.9, True)
+    ops.ema_update(ema, p, decay, True)
     assert torch.equal(ema, p)
     ref = ema.clone()
     for _ in range(3):
         p = (p.float() + 0.1 * torch.randn(p.shape, device=DEV, generator=g)).bfloat16()
-        ops.ema_update(ema, p, 0.9, False)
-        ref = 0.9 * ref + (1 - 0.9) * p  # get_ema_avg_fn on bf16 tensors (swa_utils)
+        ops.ema_update(ema, p, decay, False)
+        ref = decay * ref + (1 - decay) * p  # get_ema_avg_fn on bf16 tensors (swa_utils)
     torch.cuda.synchronize()
     assert torch.equal(ema, ref)

@@ -431,6 +431,8 @@ __global__ void cast_f32_bf16_kernel(const float* __restrict__ in, long n, bf16_
 struct SfScalars {
   float beta2, bias_correction2, eps, ckp1, adaptive_y_lr, lr, decay, grad_scale;
   int adam;
+  const float* clip_coef;  // device scalar (global-norm clip coefficient) or null
+  float clip_value;        // clamp(g, -clip_value, clip_value) when > 0
 };
 // GB: the gradient arrives as bf16 (the all-reduced bf16 wire buffer, vpt.ddp.GradSync wire="bf16").
 template <bool GB>
@@ -440,6 +442,9 @@ __global__ void radam_sf_step_kernel(bf16_t* __restrict__ y, const void* __restr
   if (i >= n) return;
   float g = (GB ? bf2f(reinterpret_cast<const bf16_t*>(grad)[i]) : reinterpret_cast<const float*>(grad)[i]) *
             s.grad_scale;
+  // after_backward (for_training.py:98-109): clip_grad_norm_ then clip_grad_value_ on the (mean) gradient
+  if (s.clip_coef) g *= *s.clip_coef;
+  if (s.clip_value > 0.f) g = fminf(fmaxf(g, -s.clip_value), s.clip_value);
   float vv = v[i] * s.beta2 + (1.f - s.beta2) * g * g;
   v[i] = vv;
   if (s.adam) g = g / (sqrtf(vv / s.bias_correction2) + s.eps);
@@ -703,16 +708,72 @@ extern "C" int vpt_cast_f32_bf16(const float* in, long n, void* out, void* strea
 
 extern "C" int vpt_radam_sf_step(void* y, const void* grad, int grad_bf16, float* z, float* v, long n, float beta2,
                                  float bias_correction2, float eps, float ckp1, float adaptive_y_lr, float lr,
-                                 float decay, float grad_scale, int adam, void* stream) {
-  VPT_CHECK_ARG(y && grad && z && v && n >= 0, "vpt_radam_sf_step: bad args");
+                                 float decay, float grad_scale, int adam, const float* clip_coef, float clip_value,
+                                 void* stream) {
+  VPT_CHECK_ARG(y && grad && z && v && n >= 0 && clip_value >= 0.f, "vpt_radam_sf_step: bad args");
   if (n == 0) return VPT_OK;
-  SfScalars s{beta2, bias_correction2, eps, ckp1, adaptive_y_lr, lr, decay, grad_scale, adam};
+  SfScalars s{beta2, bias_correction2, eps, ckp1, adaptive_y_lr, lr, decay, grad_scale, adam, clip_coef, clip_value};
   if (grad_bf16)
     hipLaunchKernelGGL(radam_sf_step_kernel<true>, grid1(n), dim3(256), 0, (hipStream_t)stream, (bf16_t*)y, grad, z, v,
                        n, s);
   else
     hipLaunchKernelGGL(radam_sf_step_kernel<false>, grid1(n), dim3(256), 0, (hipStream_t)stream, (bf16_t*)y, grad, z,
                        v, n, s);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+// ---------------------------------------------------------------- gradient clipping (global L2 norm)
+// Per-bucket partial sums of squares: block j of kGradNormBlocks grid-strides over the bucket and writes
+// its sum to part[j] (fixed assignment and order -> deterministic; no atomics).
+constexpr int kGradNormBlocks = 256;
+template <bool GB>
+__global__ void grad_sumsq_kernel(const void* __restrict__ g, long n, float scale, float* __restrict__ part) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float x = (GB ? bf2f(reinterpret_cast<const bf16_t*>(g)[i]) : reinterpret_cast<const float*>(g)[i]) * scale;
+    s += x * x;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+// coef = min(1, max_norm / (sqrt(sum of all partials) + 1e-6)) (torch.nn.utils.clip_grad_norm_), one block;
+// norm_out (optional) receives the total norm.
+__global__ void clip_coef_kernel(const float* __restrict__ part, int n, float max_norm, float* __restrict__ coef,
+                                 float* __restrict__ norm_out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += part[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float norm = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
+    *coef = fminf(max_norm / (norm + 1e-6f), 1.f);
+    if (norm_out) *norm_out = norm;
+  }
+}
+
+extern "C" int vpt_grad_norm_blocks(void) { return kGradNormBlocks; }
+
+extern "C" int vpt_grad_sumsq(const void* g, int g_bf16, long n, float scale, float* part, void* stream) {
+  VPT_CHECK_ARG(g && part && n >= 0, "vpt_grad_sumsq: bad args");
+  if (g_bf16)
+    hipLaunchKernelGGL(grad_sumsq_kernel<true>, dim3(kGradNormBlocks), dim3(256), 0, (hipStream_t)stream, g, n, scale,
+                       part);
+  else
+    hipLaunchKernelGGL(grad_sumsq_kernel<false>, dim3(kGradNormBlocks), dim3(256), 0, (hipStream_t)stream, g, n, scale,
+                       part);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_clip_coef(const float* part, int n, float max_norm, float* coef, float* norm_out, void* stream) {
+  VPT_CHECK_ARG(part && coef && n > 0 && max_norm > 0.f, "vpt_clip_coef: bad args");
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, part, n, max_norm, coef, norm_out);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
@@ -725,11 +786,13 @@ extern "C" int vpt_sf_lerp(void* y, const float* z, long n, float w, void* strea
   return VPT_OK;
 }
 
-extern "C" int vpt_ema_update(void* ema, const void* param, long n, float decay, int first, void* stream) {
-  VPT_CHECK_ARG(ema && param && decay >= 0.f && decay <= 1.f, "vpt_ema_update: bad args");
+extern "C" int vpt_ema_update(void* ema, const void* param, long n, float decay, float one_minus_decay, int first,
+                              void* stream) {
+  VPT_CHECK_ARG(ema && param && decay >= 0.f && decay <= 1.f && one_minus_decay >= 0.f && one_minus_decay <= 1.f,
+                "vpt_ema_update: bad args");
   if (n == 0) return VPT_OK;
   hipLaunchKernelGGL(ema_update_kernel, grid1(n), dim3(256), 0, (hipStream_t)stream, (bf16_t*)ema,
-                     (const bf16_t*)param, n, decay, (float)(1.0 - (double)decay), first);
+                     (const bf16_t*)param, n, decay, one_minus_decay, first);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

@@ -57,7 +57,10 @@ SIGNATURES: dict[str, list] = {
     "vpt_embed_gather": [P, P, L, I, P, P],
     "vpt_embed_scatter_add": [P, P, L, I, LL, P, P],
     "vpt_cast_f32_bf16": [P, L, P, P],
-    "vpt_radam_sf_step": [P, P, I, P, P, L, F, F, F, F, F, F, F, F, I, P],
+    "vpt_radam_sf_step": [P, P, I, P, P, L, F, F, F, F, F, F, F, F, I, P, F, P],
+    "vpt_grad_norm_blocks": [],
+    "vpt_grad_sumsq": [P, I, L, F, P, P],
+    "vpt_clip_coef": [P, I, F, P, P, P],
     "vpt_sf_lerp": [P, P, L, F, P],
     "vpt_sf_init": [P, P, P, L, P],
     "vpt_copy_rows": [P, L, I, I, I, P, L, I, I, I, P],
@@ -77,10 +80,15 @@ SIGNATURES: dict[str, list] = {
     "vpt_lora_wgrad_splits": [I, I],
     "vpt_lora_wgrad2_partial": [P, L, P, L, I, P, L, P, L, I, I, P, P, P],
     "vpt_lora_wgrad_reduce_batch": [P, I, F, I, P],
-    "vpt_ema_update": [P, P, L, F, I, P],
+    "vpt_ema_update": [P, P, L, F, F, I, P],
     "vpt_gemm_nf4": [P, L, P, P, P, P, P, L, I, P, L, P, L, I, P, L, I, I, I, P, P, L, I, F, P],
     "vpt_nf4_quantize": [P, L, P, P, P, P, P, P, P],
     "vpt_add_bf16": [P, P, L, P, P],
+    "vpt_flow_noise": [P, P, L, I, F, I, U64, P, P, P, P],
+    "vpt_velocity_loss_blocks": [],
+    "vpt_velocity_loss": [P, P, P, L, P, P, P, P],
+    "vpt_sinusoid_embed": [P, I, I, P, P],
+    "vpt_space_to_depth": [P, P, I, I, I, I, I, I, P],
     "vpt_scale_bf16": [P, L, F, P, P],
     "vpt_cover_resize_crop_workspace": [I, I, I, I, I, I, I],
     "vpt_cover_resize_crop": [P, I, I, I, I, I, I, I, I, P, P, P],
@@ -114,7 +122,7 @@ _RESTYPES = {
     "vpt_build_info": C.c_char_p,
 }
 # Entry points that return a value (size / count / string) rather than a status code.
-_VALUE_FNS = {"vpt_lora_wgrad_workspace", "vpt_lora_wgrad_splits", "vpt_gemm_workspace_bytes", "vpt_linear_wgrad_workspace_bytes", "vpt_attn_fused_workspace_bytes", "vpt_cover_resize_crop_workspace", "vpt_gemm_swiglu_bwd_workspace", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
+_VALUE_FNS = {"vpt_grad_norm_blocks", "vpt_velocity_loss_blocks", "vpt_lora_wgrad_workspace", "vpt_lora_wgrad_splits", "vpt_gemm_workspace_bytes", "vpt_linear_wgrad_workspace_bytes", "vpt_attn_fused_workspace_bytes", "vpt_cover_resize_crop_workspace", "vpt_gemm_swiglu_bwd_workspace", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
               "vpt_colsum_blocks", "vpt_attn_q_scale", "vpt_last_error_string", "vpt_abi_version", "vpt_build_info"}
 
 
@@ -133,9 +141,6 @@ def _load(path: Path, diag: bool = False) -> C.CDLL:
 
 DIAG = os.environ.get("VPT_DIAG", "0") == "1"
 LIB_PATH = LIB_DIAG if DIAG else LIB
-# developer A/B hook (tools/build_ab.py): load a library built from another revision of csrc/ instead
-if os.environ.get("VPT_LIB_AB"):
-    LIB_PATH = Path(os.environ["VPT_LIB_AB"])
 lib = _load(LIB_PATH, DIAG)
 
 

@@ -21,6 +21,8 @@ reduces the f32 gradients (2x the bytes; exact up to summation order).
 
 from __future__ import annotations
 
+import contextlib
+
 import torch
 import torch.distributed as dist
 
@@ -52,18 +54,72 @@ def grad_buckets(layout: ParamLayout, depth: int) -> list[tuple[str, int, int]]:
 
 
 class GradSync:
-    def __init__(self, grads: torch.Tensor, buckets: list[tuple[str, int, int]], group=None, wire: str = "f32"):
+    """Bucketed gradient all-reduce with the optimizer step overlapped (SURVEY §8(e) "Overlap").
+
+    Per step: `arm(apply_fn)` before the backward, `launch(name)` from the engine's on_ready as each bucket's
+    last gradient kernel is enqueued, `launch_rest()` after it, `finish()` before the next forward.
+
+    apply_fn(lo, hi, grad_scale, grad, **clip) steps parameters [lo, hi) from `grad` (the reduced f32 slice of
+    the gradient buffer or the bf16 wire slice); with clipping configured it also receives clip_coef (device
+    f32 scalar) and clip_value (RAdamScheduleFreeFlat.apply_range takes both).
+
+    overlap=True: each bucket is stepped on a side stream the moment its reduction lands (world 1: the
+    moment its gradients are written), i.e. during the rest of the backward; finish() joins the side stream
+    into the current one (CPU / gloo: the same order, blocking). Safe because a bucket's parameters are never read again in this backward once its
+    gradients are complete (the dgrad GEMMs of block i precede on_ready(block i)).
+
+    clip_grad_norm (after_backward, src/models/for_training.py:98-109): the global L2 norm of the mean
+    gradient needs every bucket, so landing buckets only contribute partial sums of squares (side stream);
+    finish() forms the coefficient on the device (no host sync) and steps every bucket with it.
+    clip_grad_value: a clamp inside the optimizer kernel, so it keeps the overlap."""
+
+    def __init__(self, grads: torch.Tensor, buckets: list[tuple[str, int, int]], group=None, wire: str = "f32",
+                 overlap: bool = True, clip_grad_norm: float | None = None, clip_grad_value: float | None = None):
         if wire not in ("f32", "bf16"):
             raise ValueError(f"wire dtype must be 'f32' or 'bf16', got {wire!r}")
         self.grads = grads
         self.buckets = buckets
         self.index = {n: (lo, hi) for n, lo, hi in buckets}
+        self.slot = {n: i for i, (n, _, _) in enumerate(buckets)}
+        spans = sorted((lo, hi) for _, lo, hi in buckets)
+        if any(a[1] != b[0] for a, b in zip(spans, spans[1:])):
+            raise ValueError("gradient buckets must tile one contiguous range")
+        self.buckets_span = (spans[0][0], spans[-1][1])
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self.wire = wire
+        self.cuda = grads.is_cuda
         self.comm = torch.empty(grads.numel(), dtype=torch.bfloat16, device=grads.device) \
             if wire == "bf16" and self.world > 1 else None
+        self.overlap = overlap  # land (reduce-wait + step) each bucket as it is launched
+        self.side = torch.cuda.Stream(device=grads.device) if (self.cuda and overlap) else None
+        self.configure_clipping(clip_grad_norm, clip_grad_value)
         self.works: dict[str, object] = {}
+        self.landed: list[str] = []
+        self.apply_fn = None
+        self.scale = 1.0 / self.world
+
+    def configure_clipping(self, clip_grad_norm: float | None = None, clip_grad_value: float | None = None):
+        if clip_grad_norm is not None:
+            if clip_grad_norm <= 0:
+                raise ValueError("clip_grad_norm must be > 0")
+            self.nb = ops_norm_blocks() if self.cuda else 1
+            self.part = torch.zeros(len(self.buckets) * self.nb, dtype=torch.float32, device=self.grads.device)
+            self.coef = torch.ones(1, dtype=torch.float32, device=self.grads.device)
+            self.norm = torch.zeros(1, dtype=torch.float32, device=self.grads.device)  # last step's total norm
+        if clip_grad_value is not None and clip_grad_value <= 0:
+            raise ValueError("clip_grad_value must be > 0")
+        self.clip_norm, self.clip_value = clip_grad_norm, clip_grad_value
+
+    # ------------------------------------------------------------------ per step
+    def arm(self, apply_fn, grad_scale: float = 1.0):
+        """Registers this step's optimizer callback before the backward (enables the overlap). grad_scale
+        multiplies the summed gradient (e.g. 1 / gradient_accumulation_steps); the 1 / world mean is added."""
+        self.apply_fn = apply_fn
+        self.scale = grad_scale / self.world
+
+    def _src(self, lo: int, hi: int) -> torch.Tensor:
+        return self.comm[lo:hi] if self.comm is not None else self.grads[lo:hi]
 
     def _to_wire(self, lo: int, hi: int) -> torch.Tensor:
         src, dst = self.grads[lo:hi], self.comm[lo:hi]
@@ -75,29 +131,103 @@ class GradSync:
         return dst
 
     def launch(self, name: str):
-        if self.world == 1:
+        if name in self.works or name in self.landed:
             return
         lo, hi = self.index[name]
-        buf = self._to_wire(lo, hi) if self.comm is not None else self.grads[lo:hi]
-        self.works[name] = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        if self.world > 1:
+            buf = self._to_wire(lo, hi) if self.comm is not None else self.grads[lo:hi]
+            self.works[name] = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        else:
+            self.works[name] = None
+        if self.apply_fn is not None and self.overlap:
+            self._land(name)
 
     def launch_rest(self):
         for n, _, _ in self.buckets:
-            if n not in self.works:
-                self.launch(n)
+            self.launch(n)
 
-    def finish(self, apply_fn):
-        """For every bucket in completion order: make the current stream wait for its reduction,
-        then apply_fn(lo, hi, grad_scale, grad) with grad = the reduced buffer of [lo, hi) (f32 slice of
-        the gradient buffer, or the bf16 wire slice)."""
-        scale = 1.0 / self.world
-        for n, lo, hi in self.buckets:
-            w = self.works.pop(n, None)
+    def _clip_kw(self) -> dict:
+        kw = {}
+        if self.clip_norm is not None:
+            kw["clip_coef"] = self.coef
+        if self.clip_value is not None:
+            kw["clip_value"] = self.clip_value
+        return kw
+
+    def _sumsq(self, name: str, src: torch.Tensor, scale: float):
+        i = self.slot[name]
+        part = self.part[i * self.nb:(i + 1) * self.nb]
+        if src.is_cuda:
+            from . import ops
+            ops.grad_sumsq(src, scale, part)
+        else:
+            part.copy_((src.float() * scale).pow(2).sum().reshape(1))
+
+    def _land(self, name: str):
+        """The bucket's reduction has been enqueued: step it (or, with global-norm clipping, take its sum of
+        squares) behind that reduction -- on the side stream when overlapping, else on the current stream."""
+        w = self.works.pop(name)
+        lo, hi = self.index[name]
+        scale = self.scale
+        src = self._src(lo, hi)
+        if self.side is not None:
+            self.side.wait_stream(torch.cuda.current_stream(self.grads.device))  # gradients / wire cast written
+            ctx = torch.cuda.stream(self.side)
+        else:
+            ctx = contextlib.nullcontext()
+        with ctx:
             if w is not None:
-                w.wait()
-            src = self.comm[lo:hi] if self.comm is not None else self.grads[lo:hi]
-            apply_fn(lo, hi, scale, src)
+                w.wait()  # stream-ordered on the GPU (the side / current stream waits the collective); blocking on gloo
+            if self.clip_norm is not None:
+                self._sumsq(name, src, scale)
+            else:
+                self.apply_fn(lo, hi, scale, src, **self._clip_kw())
+        self.landed.append(name)
+
+    def finish(self, apply_fn=None, grad_scale: float = 1.0):
+        """Completes the step: every bucket not yet landed is landed now (serial path), global-norm clipping
+        forms its coefficient and steps every bucket, and the current stream waits for the side stream.
+        `apply_fn` (if given) replaces the armed callback -- the serial form finish(fn) without arm()."""
+        if apply_fn is not None:
+            self.apply_fn = apply_fn
+            self.scale = grad_scale / self.world
+        if self.apply_fn is None:
+            raise RuntimeError("GradSync.finish: no optimizer callback (arm() or finish(apply_fn))")
+        if self.world == 1 and not self.overlap and self.clip_norm is None and not self.landed:
+            # one process, serial: the buckets tile the flat buffer, so ONE optimizer launch covers them all
+            lo, hi = self.buckets_span
+            self.apply_fn(lo, hi, self.scale, self.grads[lo:hi], **self._clip_kw())
+            self.works.clear()
+            self.apply_fn = None
+            return
+        for n, _, _ in self.buckets:
+            if n not in self.landed and n not in self.works:
+                self.launch(n)  # (lands it as well when overlapping)
+        for n, _, _ in self.buckets:
+            if n in self.works:
+                self._land(n)
+        if self.clip_norm is not None:
+            ctx = torch.cuda.stream(self.side) if self.side is not None else contextlib.nullcontext()
+            scale = self.scale
+            with ctx:
+                if self.part.is_cuda:
+                    from . import ops
+                    ops.clip_coef(self.part, self.clip_norm, self.coef, self.norm)
+                else:
+                    self.norm.copy_(self.part.sum().sqrt().reshape(1))
+                    self.coef.copy_((self.clip_norm / (self.norm + 1e-6)).clamp(max=1.0))
+                for n, lo, hi in self.buckets:
+                    self.apply_fn(lo, hi, scale, self._src(lo, hi), **self._clip_kw())
+        if self.side is not None:
+            torch.cuda.current_stream(self.grads.device).wait_stream(self.side)
         self.works.clear()
+        self.landed = []
+        self.apply_fn = None
+
+
+def ops_norm_blocks() -> int:
+    from . import ops
+    return ops.grad_norm_blocks()
 
 
 class LossLog:

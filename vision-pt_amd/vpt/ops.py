@@ -34,9 +34,11 @@ class KernelProbe:
     def __init__(self, op: str):
         self.op = op
         self.records: list[tuple] = []
+        self.nbytes: list[float] = []
         self.active = False
 
-    def record(self, flops: float, fn, key=None):
+    def record(self, flops: float, fn, key=None, nbytes: float = 0.0):
+        """nbytes: compulsory HBM bytes of the launch (operands read once, results written once)."""
         if not self.active:
             return fn()
         s = torch.cuda.Event(enable_timing=True)
@@ -45,7 +47,11 @@ class KernelProbe:
         r = fn()
         e.record()
         self.records.append((s, e, flops, key))
+        self.nbytes.append(nbytes)
         return r
+
+    def mean_bytes(self) -> float:
+        return sum(self.nbytes) / len(self.nbytes) if self.nbytes else 0.0
 
     def summary(self):
         """(launches, mean ms per launch, mean algorithmic FLOPs per launch)."""
@@ -118,7 +124,9 @@ def gemm(a, a_kmajor: bool, b, b_kmajor: bool, M: int, N: int, K: int, out, *, b
         run()
     else:
         pr.record(2.0 * M * N * K, run, key=f"{'fwd' if a_kmajor and b_kmajor else 'dgrad' if a_kmajor else 'wgrad'}"
-                  f" M{M} N{N} K{K} s{splits}")
+                  f" M{M} N{N} K{K} s{splits}",
+                  nbytes=2.0 * (M + N) * K + M * N * (2 if out_mode == OUT_BF16 else 4 if out_mode == OUT_F32 else 8)
+                  + (2.0 * M * N if resid is not None else 0.0))
     return out
 
 
@@ -169,7 +177,8 @@ def linear_wgrad(dy, x, out, accumulate=False, splits=1, workspace=None, bias_ou
     if pr is None:
         run()
     else:
-        pr.record(2.0 * M * N * K, run, key=f"wgrad M{N} N{K} K{M} s{splits}{' +b' if bias_out is not None else ''}")
+        pr.record(2.0 * M * N * K, run, key=f"wgrad M{N} N{K} K{M} s{splits}{' +b' if bias_out is not None else ''}",
+                  nbytes=2.0 * M * (N + K) + N * K * (8 if accumulate else 4))
     return out
 
 
@@ -187,7 +196,8 @@ def linear_swiglu(x, w12, b12, x12, h):
     if pr is None:
         run()
     else:
-        pr.record(2.0 * M * 2 * F * K, run, key=f"swiglu_fwd M{M} N{2 * F} K{K}")
+        pr.record(2.0 * M * 2 * F * K, run, key=f"swiglu_fwd M{M} N{2 * F} K{K}",
+                  nbytes=2.0 * (M + 2 * F) * K + 2.0 * M * 3 * F)  # x12 and h out
     return x12, h
 
 
@@ -208,7 +218,8 @@ def linear_dgrad_swiglu(dy, w3, x12, dx12, workspace=None):
     if pr is None:
         run()
     else:
-        pr.record(2.0 * M * F * D, run, key=f"swiglu_dgrad M{M} N{F} K{D}")
+        pr.record(2.0 * M * F * D, run, key=f"swiglu_dgrad M{M} N{F} K{D}",
+                  nbytes=2.0 * (M + F) * D + 2.0 * M * 2 * F * 2)  # x12 in, dx12 out
     return dx12
 
 
@@ -326,7 +337,8 @@ def attn_fwd(q, k, v, o, lse, kbias, B, H, rows, n, n_dense, scale=0.125, nk=Non
     pr = PROBES.get("attn_fwd")
     if pr is None:
         return run()
-    return pr.record(4.0 * B * H * n * nk * 64, run)  # QK^T + PV over all (query, key) pairs
+    # compulsory: q, o (n rows), k, v (nk rows) bf16 of 64 dims, -LSE f32
+    return pr.record(4.0 * B * H * n * nk * 64, run, nbytes=B * H * (2.0 * 64 * 2 * (n + nk) + 4.0 * n))
 
 
 def attn_bwd(q, k, v, o, do, lse, delta, kbias, dq, dk, dv, B, H, rows, n, n_dense, scale=0.125, nk=None):
@@ -339,7 +351,8 @@ def attn_bwd(q, k, v, o, do, lse, delta, kbias, dq, dk, dv, B, H, rows, n, n_den
     pr = PROBES.get("attn_bwd")
     if pr is None:
         return run()
-    return pr.record(8.0 * B * H * n * nk * 64, run)  # dV, dP, dK, dQ products (algorithmic 2x forward)
+    # compulsory: q, o, do read + dq written (n rows), k, v read + dk, dv written (nk rows), -LSE / -delta
+    return pr.record(8.0 * B * H * n * nk * 64, run, nbytes=B * H * (2.0 * 64 * 4 * (n + nk) + 12.0 * n))
 
 
 # ----------------------------------------------------------------------------- misc
@@ -459,16 +472,45 @@ def cast_f32_bf16(x, out):
 
 
 def radam_sf_step(y, grad, z, v, *, beta2, bias_correction2, eps, ckp1, adaptive_y_lr, lr, decay, grad_scale,
-                  adam):
-    """grad f32, or bf16 (the all-reduced bf16 wire buffer of vpt.ddp.GradSync)."""
+                  adam, clip_coef=None, clip_value=0.0):
+    """grad f32, or bf16 (the all-reduced bf16 wire buffer of vpt.ddp.GradSync); clip_coef = a device f32
+    scalar multiplying the gradient (global-norm clipping), clip_value > 0 clamps it afterwards."""
     if grad.dtype not in (F32, BF16) or grad.numel() != y.numel():
         raise ValueError("grad must be f32 or bf16 with y's size")
+    if clip_coef is not None:
+        _chk(clip_coef, F32, "clip_coef")
     gb = grad.dtype == BF16
     _launch("radam_sf_step", y.numel() * (22 if gb else 24),  # y bf16, grad, z / v f32 in; y, z, v out
             lambda: call("vpt_radam_sf_step", y.data_ptr(), grad.data_ptr(), int(gb), z.data_ptr(), v.data_ptr(),
                          y.numel(),
                          beta2, bias_correction2, eps, ckp1, adaptive_y_lr, lr, decay, grad_scale, int(adam),
-                         stream()))
+                         _p(clip_coef), float(clip_value or 0.0), stream()))
+
+
+GRAD_NORM_BLOCKS = None
+
+
+def grad_norm_blocks() -> int:
+    global GRAD_NORM_BLOCKS
+    if GRAD_NORM_BLOCKS is None:
+        GRAD_NORM_BLOCKS = int(call("vpt_grad_norm_blocks"))
+    return GRAD_NORM_BLOCKS
+
+
+def grad_sumsq(g, scale, part):
+    """part[grad_norm_blocks()] f32 <- partial sums of (scale * g)^2 (g f32 or bf16)."""
+    if g.dtype not in (F32, BF16):
+        raise ValueError("g must be f32 or bf16")
+    _chk(part, F32, "part")
+    if part.numel() < grad_norm_blocks():
+        raise ValueError("part too small")
+    call("vpt_grad_sumsq", g.data_ptr(), int(g.dtype == BF16), g.numel(), float(scale), part.data_ptr(), stream())
+
+
+def clip_coef(part, max_norm, coef, norm_out=None):
+    """coef (device f32 scalar) <- min(1, max_norm / (sqrt(sum(part)) + 1e-6)); norm_out <- the norm."""
+    _chk(part, F32, "part")
+    call("vpt_clip_coef", part.data_ptr(), part.numel(), float(max_norm), coef.data_ptr(), _p(norm_out), stream())
 
 
 def sf_lerp(y, z, w):
@@ -476,7 +518,10 @@ def sf_lerp(y, z, w):
 
 
 def ema_update(ema, params, decay, first):
-    call("vpt_ema_update", ema.data_ptr(), params.data_ptr(), params.numel(), float(decay), int(first), stream())
+    # (1 - decay) is formed in Python double and only then rounded to f32, as torch rounds the Python scalar
+    # of `(1 - decay) * p` (swa_utils.get_ema_avg_fn); 1 - float32(decay) differs by 1.7e-4 relative at 0.9999
+    call("vpt_ema_update", ema.data_ptr(), params.data_ptr(), params.numel(), float(decay), float(1.0 - decay),
+         int(first), stream())
 
 
 def sf_init(y, z, v):
@@ -544,6 +589,49 @@ def transpose_add(src, B, R, S, add=None, out=None):
     """out[b][s][r] = src[b][r][s] (+ add[b][s][r]) for bf16 src [B, R, S] (R, S multiples of 64)."""
     out = torch.empty(B, S, R, dtype=BF16, device=src.device) if out is None else out
     call("vpt_transpose_add", src.data_ptr(), _p(add), out.data_ptr(), B, R, S, stream())
+    return out
+
+
+# ----------------------------------------------------------------------------- SDXL flow matching
+def flow_noise(x, t, B, z, eps=None, eps_in=None, noise_scale=1.0, clean_at_zero=False, seed=0):
+    """prepare_scaled_noised_latents (src/modules/loss/flow_match.py:60-74) on bf16 latents x [B, ...]:
+    eps = bf16(randn * noise_scale) (counter RNG, or eps_in), z = t x + (1 - t) eps (bf16)."""
+    n = x.numel() // B
+    call("vpt_flow_noise", x.data_ptr(), t.data_ptr(), n, B, float(noise_scale), int(clean_at_zero), int(seed),
+         _p(eps_in), z.data_ptr(), _p(eps), stream())
+    return z
+
+
+_LOSS_PART: dict = {}
+
+
+def velocity_loss(v, x, eps, loss, dv=None):
+    """loss_with_predicted_velocity (flow_match.py:85-96): loss (f32 [1]) = mean((v - (eps - x))^2),
+    dv = d loss / d v (bf16); deterministic block sums."""
+    nb = int(call("vpt_velocity_loss_blocks"))
+    part = _LOSS_PART.get(v.device)
+    if part is None:
+        part = _LOSS_PART[v.device] = torch.empty(nb, dtype=F32, device=v.device)
+    _launch("velocity_loss", v.numel() * (6 + (2 if dv is not None else 0)),
+            lambda: call("vpt_velocity_loss", v.data_ptr(), x.data_ptr(), eps.data_ptr(), v.numel(), _p(dv),
+                         part.data_ptr(), loss.data_ptr(), stream()))
+    return loss
+
+
+def sinusoid_embed(vals, dim, out=None):
+    """get_timestep_embedding(vals, dim, flip_sin_to_cos=True, downscale_freq_shift=0) -> bf16 [R, dim]."""
+    R = vals.numel()
+    out = torch.empty(R, dim, dtype=BF16, device=vals.device) if out is None else out
+    call("vpt_sinusoid_embed", vals.data_ptr(), R, dim, out.data_ptr(), stream())
+    return out
+
+
+def space_to_depth(src, B, C, H, W, r, out=None, inverse=False):
+    """NCHW [B,C,H,W] -> tokens [B, (H/r)(W/r), C r r] (pixel_unshuffle + permute); inverse: tokens -> NCHW."""
+    if out is None:
+        out = torch.empty((B, C, H, W) if inverse else (B, (H // r) * (W // r), C * r * r), dtype=BF16,
+                          device=src.device)
+    call("vpt_space_to_depth", src.data_ptr(), out.data_ptr(), B, C, H, W, r, int(inverse), stream())
     return out
 
 
@@ -634,14 +722,19 @@ class _LoraBatch:
         self.key = None  # (alpha, accumulate) of the pending jobs
         self.nws = 0     # workspaces handed out since the last flush
 
+    def reserve(self, key, njobs):
+        """Called BEFORE a target takes its workspaces: flushes first when its jobs would not fit, so the
+        workspace names handed out after a flush never alias slabs that pending jobs still have to reduce."""
+        if self.jobs and (key != self.key or len(self.jobs) + njobs > 32):
+            self.flush()
+        self.key = key
+
     def ws(self, dev, nbytes):
         self.nws += 1
         return _lora_ws(dev, f"batch{self.nws}", nbytes)
 
-    def add(self, jobs, key):
-        if self.jobs and (key != self.key or len(self.jobs) + len(jobs) > 32):
-            self.flush()
-        self.key = key
+    def add(self, jobs):
+        assert len(self.jobs) + len(jobs) <= 32
         self.jobs.extend(jobs)
 
     def flush(self):
@@ -688,13 +781,13 @@ def lora_wgrad2(dy, ds, g_up, x, vs, g_down, accumulate=True, alpha=1.0):
         return
     for t, dt in ((g_up, F32), (g_down, F32)):
         _chk(t, dt, "adapter grad")
+    b.reserve((float(alpha), int(accumulate)), 2)
     ws_up = b.ws(dy.device, int(lib.vpt_lora_wgrad_workspace(M, n_out)))
     ws_dn = b.ws(dy.device, int(lib.vpt_lora_wgrad_workspace(M, n_in)))
     call("vpt_lora_wgrad2_partial", dy.data_ptr(), dy.stride(0), ds.data_ptr(), ds.stride(0), n_out, x.data_ptr(),
          x.stride(0), vs.data_ptr(), vs.stride(0), n_in, M, ws_up.data_ptr(), ws_dn.data_ptr(), stream())
     b.add([_LoraReduceJob(ws_up.data_ptr(), g_up.data_ptr(), n_out, call("vpt_lora_wgrad_splits", M, n_out), 0, 0),
-           _LoraReduceJob(ws_dn.data_ptr(), g_down.data_ptr(), n_in, call("vpt_lora_wgrad_splits", M, n_in), 1, 0)],
-          (float(alpha), int(accumulate)))
+           _LoraReduceJob(ws_dn.data_ptr(), g_down.data_ptr(), n_in, call("vpt_lora_wgrad_splits", M, n_in), 1, 0)])
 
 
 def nf4_quantize(w, code2, packed, qabsmax, absmax2, offset, scratch):

@@ -96,16 +96,19 @@ class RAdamScheduleFreeFlat:
         return self.scalars()
 
     @torch.no_grad()
-    def apply_range(self, s: dict, lo: int, hi: int, grad_scale: float = 1.0, grad: torch.Tensor | None = None):
+    def apply_range(self, s: dict, lo: int, hi: int, grad_scale: float = 1.0, grad: torch.Tensor | None = None,
+                    clip_coef: torch.Tensor | None = None, clip_value: float | None = None):
         """Steps parameters [lo, hi) from self.grads[lo:hi], or from `grad` (f32 or bf16, the range's
-        all-reduced wire buffer) when given."""
+        all-reduced wire buffer) when given. clip_coef (device f32 scalar) / clip_value: gradient clipping
+        (for_training.py:98-109) applied to grad_scale * grad inside the same kernel."""
         g = self.param_groups[0]
         if hi <= lo:
             return
         src = self.grads[lo:hi] if grad is None else grad
         ops.radam_sf_step(self.params[lo:hi], src, self.z[lo:hi], self.v[lo:hi], beta2=s["beta2"],
                           bias_correction2=s["bc2"], eps=g["eps"], ckp1=s["ckp1"], adaptive_y_lr=s["adaptive_y_lr"],
-                          lr=s["lr"], decay=g["weight_decay"], grad_scale=grad_scale, adam=s["adam"])
+                          lr=s["lr"], decay=g["weight_decay"], grad_scale=grad_scale, adam=s["adam"],
+                          clip_coef=clip_coef, clip_value=clip_value or 0.0)
 
     def end_step(self, s: dict):
         g = self.param_groups[0]

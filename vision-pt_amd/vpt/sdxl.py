@@ -138,8 +138,9 @@ class LoRALinearNF4:
         self._saved = (x, ds) if save else None
         return y
 
-    def backward(self, dy: torch.Tensor) -> torch.Tensor:
-        """Accumulates g_up, g_down; returns dx (bf16)."""
+    def backward(self, dy: torch.Tensor, need_dx: bool = True) -> torch.Tensor | None:
+        """Accumulates g_up, g_down; returns dx (bf16), or None with need_dx=False (an input that needs no
+        gradient, e.g. the frozen text encoder's hidden states under attn2.to_k / to_v)."""
         x, ds = self._saved
         M = x.shape[0]
         r = self.down.shape[0]
@@ -151,6 +152,8 @@ class LoRALinearNF4:
             ops.linear_wgrad(dy, ds, self.g_up, accumulate=True, splits=ops.wgrad_splits(*self.up.shape, M))
             ops.gemm(dy, True, self.up, False, M, r, self.up.shape[0], vs, alpha=self.scale)
             ops.linear_wgrad(vs, x, self.g_down, accumulate=True, splits=ops.wgrad_splits(*self.down.shape, M))
+        if not need_dx:
+            return None
         dx = torch.empty(M, self.base.shape[1], dtype=BF16, device=dy.device)
         if self.fused:
             return ops.gemm_nf4(dy, self.base, False, dx, lora_a=vs, lora_b=self.down)
@@ -232,13 +235,15 @@ class SDXLTransformerBlock:
                         lse1=lse1, q2=q2, k2=k2, v2=v2, o2=o2, lse2=lse2, x12=x12) if save else None
         return y
 
-    def backward(self, dy: torch.Tensor):
+    def backward(self, dy: torch.Tensor, need_dctx: bool = True):
         """Returns (dx, dctx); accumulates every adapter's g_down / g_up (norms and NF4 bases frozen). The ten
-        targets' adapter-gradient reduces run as one batched launch at the end (ops.lora_wgrad_batch)."""
+        targets' adapter-gradient reduces run as one batched launch at the end (ops.lora_wgrad_batch).
+        need_dctx=False: the context needs no gradient (the reference's text-encoder states are produced under
+        no_grad, train/sdxl/flow_match.py:115-124), so the to_k / to_v input-gradient GEMMs are skipped."""
         with ops.lora_wgrad_batch():
-            return self._backward(dy)
+            return self._backward(dy, need_dctx)
 
-    def _backward(self, dy: torch.Tensor):
+    def _backward(self, dy: torch.Tensor, need_dctx: bool = True):
         st, L = self._st, self.lin
         B, n, nc = st["B"], st["n"], st["nc"]
         m1, m2, m3 = st["m"]
@@ -250,7 +255,8 @@ class SDXLTransformerBlock:
         do2 = L["attn2.to_out.0"].backward(dx2)
         dq2, dk2, dv2 = self._attn_bwd(st["q2"], st["k2"], st["v2"], st["o2"], st["lse2"], do2, B, n, nc)
         dh2 = L["attn2.to_q"].backward(dq2)
-        dctx = ops.add_bf16(L["attn2.to_k"].backward(dk2), L["attn2.to_v"].backward(dv2))
+        dck, dcv = L["attn2.to_k"].backward(dk2, need_dctx), L["attn2.to_v"].backward(dv2, need_dctx)
+        dctx = ops.add_bf16(dck, dcv) if need_dctx else None
         dx1 = ops.layernorm_bwd(dh2, st["x1"], m2, r2, self.norm["norm2"][0], dres=dx2)
         do1 = L["attn1.to_out.0"].backward(dx1)
         dq, dk, dv = self._attn_bwd(st["q"], st["k"], st["v"], st["o1"], st["lse1"], do1, B, n, n)
@@ -333,16 +339,17 @@ class SDXLSpatialTransformer:
         self._st = dict(B=B, HW=HW, x=x, mean=mean, rstd=rstd) if save else None
         return y
 
-    def backward(self, dy: torch.Tensor):
-        """dy NCHW [B, C, HW] -> (dx NCHW, dctx [B*nc, context_dim])."""
+    def backward(self, dy: torch.Tensor, need_dctx: bool = True):
+        """dy NCHW [B, C, HW] -> (dx NCHW, dctx [B*nc, context_dim] or None with need_dctx=False)."""
         st = self._st
         B, HW, C, G = st["B"], st["HW"], self.C, self.groups
         du = ops.transpose_add(dy, B, C, HW)                                  # tokens [B, HW, C]
         dt = self.proj_out.backward(du.view(B * HW, C))
         dctx = None
         for blk in reversed(self.blocks):
-            dt, dc = blk.backward(dt)
-            dctx = dc if dctx is None else ops.add_bf16(dctx, dc)
+            dt, dc = blk.backward(dt, need_dctx)
+            if need_dctx:
+                dctx = dc if dctx is None else ops.add_bf16(dctx, dc)
         dtok = self.proj_in.backward(dt)
         dh = ops.transpose_add(dtok.view(B, HW, C), B, HW, C)                 # NCHW
         dx = ops.groupnorm_bwd(dh, st["x"], st["mean"], st["rstd"], self.norm_w, B, C, G, HW, dres=dy)

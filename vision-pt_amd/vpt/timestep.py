@@ -30,7 +30,8 @@ def _time_shift(mu: float, sigma: float, t: torch.Tensor) -> torch.Tensor:
 def sample_timestep(latents_shape, device=None, sampling_type: str = "sigmoid", generator: torch.Generator | None = None,
                     **kw) -> torch.Tensor:
     """t in (0, 1), shape [latents_shape[0]] f32 (sampling.py:170-187; same argument names and defaults).
-    Like the reference, a sampler rejects keyword arguments it does not take."""
+    Like the reference, a sampler rejects keyword arguments it does not take, except "uniform", whose
+    dispatcher call passes none on (sampling.py:170-187), so any are ignored."""
     B = int(latents_shape[0])
 
     def randn():
@@ -55,8 +56,7 @@ def sample_timestep(latents_shape, device=None, sampling_type: str = "sigmoid", 
     if sampling_type == "sigmoid":  # sampling.py:71-82
         a = take("sigmoid_scale")
         return (randn() * a.get("sigmoid_scale", 1.0)).sigmoid()
-    if sampling_type == "uniform":  # sampling.py:85-93
-        take()
+    if sampling_type == "uniform":  # sampling.py:85-93; the dispatcher calls uniform_rand(shape, device): kwargs dropped
         return torch.rand(B, device=device, generator=generator)
     if sampling_type == "scale_shift_sigmoid":  # sampling.py:259-272 (**kwargs swallowed there)
         std, mean = kw.get("std", 0.8), kw.get("mean", -0.8)

@@ -15,6 +15,7 @@ import os
 from typing import Iterable
 
 import torch
+import torch.distributed as dist
 from safetensors.torch import save_file
 
 from . import ops
@@ -123,14 +124,23 @@ class JiTTrainLoop:
     def __init__(self, trainer: JiTTrainer, optimizer: RAdamScheduleFreeFlat, loader: Iterable, tokenizer: ClassTokenizer,
                  num_train_epochs: int = 1, gradient_accumulation_steps: int = 1, saving: SavingStrategy | None = None,
                  savers: list[SafetensorsSaver] | None = None, use_ema: bool = False, ema_decay: float = 0.9999,
-                 sync=None, losslog=None, debug_mode: str | None = None, max_token_length: int | None = None):
+                 sync=None, losslog=None, debug_mode: str | None = None, max_token_length: int | None = None,
+                 clip_grad_norm: float | None = None, clip_grad_value: float | None = None):
         self.trainer, self.optimizer, self.loader, self.tokenizer = trainer, optimizer, loader, tokenizer
         self.epochs, self.accum = num_train_epochs, gradient_accumulation_steps
         self.saving, self.savers = saving, list(savers or [])
         self.ema = ParamEMA(trainer.engine.params, ema_decay) if use_ema else None
         # common.py:162-164: the EMA callbacks are copies with the template prefixed by "ema_"
         self.ema_savers = [SafetensorsSaver(s.name, s.save_dir, "ema_" + s.template) for s in self.savers]
+        if sync is None:  # single process: the same bucketed step (optimizer overlapped with the backward)
+            from .ddp import GradSync, grad_buckets
+            world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+            sync = GradSync(trainer.engine.grads, grad_buckets(trainer.engine.layout, trainer.engine.cfg.depth),
+                            overlap=world > 1)  # one process: one optimizer launch after the backward is faster
+        if clip_grad_norm is not None or clip_grad_value is not None:  # TrainerConfig (src/config.py:74-75)
+            sync.configure_clipping(clip_grad_norm, clip_grad_value)
         self.sync, self.losslog, self.debug_mode = sync, losslog, debug_mode
+        self._sched = None
         self.max_len = max_token_length or trainer.tcfg.max_token_length
         self.losses: list[float] = []
         self.saved: list[str] = []
@@ -138,35 +148,43 @@ class JiTTrainLoop:
     def _step(self, batch, micro: int):
         ids, mask = self.tokenizer.tokenize(batch["caption"], max_length=self.max_len)
         tr = self.trainer
-        on_ready = self.sync.launch if (self.sync is not None and (micro + 1) % self.accum == 0) else None
+        on_ready = None
+        if (micro + 1) % self.accum == 0:  # the synchronising micro-step: reduce + step buckets as they complete
+            opt = self.optimizer
+            s = self._sched = opt.begin_step()
+            self.sync.arm(lambda lo, hi, sc, g, **kw: opt.apply_range(s, lo, hi, sc, g, **kw), 1.0 / self.accum)
+            on_ready = self.sync.launch
         loss, _ = tr.step(batch["image"], ids, mask, batch["original_size"], batch["target_size"],
                           batch["crop_coords_top_left"], on_ready=on_ready, accumulate=micro % self.accum != 0)
         return loss
 
     def _apply_gradients(self):
-        """apply_gradients (common.py:380-388): optimizer step with the 1/accum loss scaling folded into the
-        update's grad_scale (and the DDP mean when synchronising), EMA update; gradients are re-zeroed by the
-        next step's backward."""
-        opt = self.optimizer
-        s = opt.begin_step()
-        if self.sync is not None:
-            self.sync.launch_rest()
-            self.sync.finish(lambda lo, hi, sc, g: opt.apply_range(s, lo, hi, sc / self.accum, g))
-        else:
-            opt.apply_range(s, 0, opt.params.numel(), 1.0 / self.accum)
-        opt.end_step(s)
+        """apply_gradients (common.py:380-388): optimizer step with the 1/accum loss scaling (and the DDP mean)
+        folded into the update's grad_scale, gradient clipping (after_backward) inside it, EMA update;
+        gradients are re-zeroed by the next step's backward."""
+        self.sync.launch_rest()
+        self.sync.finish()
+        self.optimizer.end_step(self._sched)
         if self.ema is not None:
             self.ema.update()
 
     def _save(self, epoch: int, steps: int):
-        meta = {"epoch": str(epoch), "steps": str(steps)}
-        sd = reference_state_dict(self.trainer)
-        for cb in self.savers:
-            self.saved.append(cb.save(sd, epoch, steps, meta))
-        if self.ema is not None:
-            esd = reference_state_dict(self.trainer, self.ema.ema)
-            for cb in self.ema_savers:
-                self.saved.append(cb.save(esd, epoch, steps, meta))
+        """common.py:390-423: wait_for_everyone, save on the main process only, wait_for_everyone (ranks hold
+        identical replicas after the synchronised step, so rank 0's copy is the model)."""
+        ddp = dist.is_available() and dist.is_initialized()
+        if ddp:
+            dist.barrier()
+        if not ddp or dist.get_rank() == 0:
+            meta = {"epoch": str(epoch), "steps": str(steps)}
+            sd = reference_state_dict(self.trainer)
+            for cb in self.savers:
+                self.saved.append(cb.save(sd, epoch, steps, meta))
+            if self.ema is not None:
+                esd = reference_state_dict(self.trainer, self.ema.ema)
+                for cb in self.ema_savers:
+                    self.saved.append(cb.save(esd, epoch, steps, meta))
+        if ddp:
+            dist.barrier()
 
     def train(self):
         current_step = 0
@@ -179,7 +197,9 @@ class JiTTrainLoop:
                 if current_step % self.accum == 0:
                     self._apply_gradients()
                 if self.losslog is not None:
-                    self.losslog.push(loss)
+                    v = self.losslog.push(loss)  # mean over ranks of a step depth-1 pushes ago (or None)
+                    if v is not None:
+                        self.losses.append(v)
                 else:
                     self.losses.append(loss.item())  # the reference's per-step loss.item()
                 if self.saving is not None and self.saving.should_save(epoch, current_step):
@@ -190,4 +210,7 @@ class JiTTrainLoop:
                 self.optimizer.eval()  # after_train_epoch (common.py:281-284)
             if self.debug_mode == "1step":
                 break
+        if self.losslog is not None:
+            while self.losslog.pending:  # the last depth-1 steps' losses
+                self.losses.append(self.losslog.pop())
         return current_step
