@@ -262,7 +262,7 @@ def flow_match_loss(latents, t, eps, ctx, pooled, sizes, sk, stacks, rank, alpha
         w, heads, depth = stacks[i]
         return spatial_forward(h, ctx, w, heads, depth, rank, alpha)
 
-    def tok_lin(name, h_nchw, r, emb=None):
+    def tok_lin(name, h, r, emb=None):
         """pixel_unshuffle(h, r) -> tokens -> Linear (+ per-sample emb) -> NCHW at the unshuffled size."""
         u = F.pixel_unshuffle(h, r) if r > 1 else h
         Bn, Cf, Hh, Ww = u.shape

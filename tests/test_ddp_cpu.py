@@ -83,7 +83,7 @@ def _worker(rank, world, port, q, wire="f32"):
     first = log.push(loss.detach())
     second = log.push(loss.detach() * 3)
     third = log.pop()
-    q.put((rank, out.clone(), applied, (first, second, third, loss.item())))
+    q.put((rank, out.numpy().copy(), applied, (first, second, third, loss.item())))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -102,7 +102,7 @@ def test_two_rank_gradient_mean_equals_single_rank_big_batch(wire):
         p.join(timeout=60)
         assert p.exitcode == 0
     out.sort(key=lambda t: t[0])
-    g0, g1 = out[0][1], out[1][1]
+    g0, g1 = torch.from_numpy(out[0][1]), torch.from_numpy(out[1][1])
     assert torch.equal(g0, g1)  # every rank holds the same averaged gradient
     # reference: one process, whole batch of 4 (mean-of-means == mean because both halves have 2 images)
     from vpt.params import ParamLayout

@@ -562,13 +562,6 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
   store_T(g.dk, (long)b * g.dk.sb + hd * g.dk.sh, dkT, 0.69314718055994531f, key, g.nk, lane, kmasked);
 }
 
-template <int ABL, int NW>
-__global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dkdv_kernel(AttnArgs g) {
-  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];     // [buf][Q / dO]
-  __shared__ __attribute__((aligned(16))) float lstat[2][2][64];     // [buf][lse / delta]
-  dkdv_body<ABL, NW>(g, blockIdx.x, blockIdx.y, blockIdx.z, lds, lstat);
-}
-
 // ------------------------------------------------------------------ backward dQ
 // Body of one dQ block (query block bx of head hd, batch b); lds = [buf][K / V] tiles, kbl = key bias of keys kb0..
 template <int ABL, int NW>
@@ -650,13 +643,6 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
   store_T(g.dq, (long)b * g.dq.sb + hd * g.dq.sh, dqT, g.scale, qrow, g.n, lane, false);
 }
 
-template <int ABL, int NW>
-__global__ __launch_bounds__(64 * NW, 2) void attn_bwd_dq_kernel(AttnArgs g) {
-  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];  // [buf][K / V]
-  extern __shared__ __attribute__((aligned(16))) float kbl[];   // key bias of keys kb0.. (fill_key_bias)
-  dq_body<ABL, NW>(g, blockIdx.x, blockIdx.y, blockIdx.z, lds, kbl);
-}
-
 // The production backward as ONE launch over both block kinds: the dK/dV blocks first (the longer ones),
 // then the dQ blocks. Each kind alone is 3,168 equal blocks at B=8 1024^2 on 512 block slots (2 per CU):
 // 6.19 waves of work run as 7, twice. In one grid the dQ blocks start on the slots the dK/dV tail frees,
@@ -677,478 +663,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs g, int nkb, i
   }
 }
 
-#ifdef VPT_DIAG
-// ------------------------------------------------------------------ backward, 64 rows per wave
-// The 32-row kernels above read the LDS operand tiles (Q / dO rows and transposes for dK/dV; K / V rows
-// and K transposed for dQ) once per 32 rows they own, which at two 4-wave blocks per CU loads the LDS array
-// about as long as the MFMAs run. Here every wave owns TWO 32-row sub-blocks (64 keys for dK/dV, 64
-// queries for dQ): each LDS fragment read feeds both sub-blocks' MFMA chains, halving LDS operand traffic
-// per MFMA. Twice the accumulators (dK/dV: 128 f32 per lane) -> one wave per SIMD (512 registers).
-// Measured SLOWER than the 32-row pair at B=8 1024^2 (profiles/r02/r02i_attn_bwd_rows64_ab.json: dK/dV64
-// 1.91 ms and dQ64 1.84 ms per backward vs 1.58 ms): with one wave per SIMD the compiler-scheduled body
-// exposes the LDS / exp latencies the second wave used to hide, and dQ64 at two waves per SIMD spills.
-// Kept in the diagnostic build for A/B (vpt_attn_set_rows64).
-template <int NW>
-__global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dkdv64_kernel(AttnArgs g) {
-  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];     // [buf][Q / dO]
-  __shared__ __attribute__((aligned(16))) float lstat[2][2][64];     // [buf][lse / delta]
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
-  const int b = blockIdx.z, hd = blockIdx.y;
-  const int k0 = blockIdx.x * (64 * NW) + wid * 64;
-  const bf16_t* Q = g.q.p + b * g.q.sb + hd * g.q.sh;
-  const bf16_t* dO = g.dO.p + b * g.dO.sb + hd * g.dO.sh;
-  const float* LSE = g.lse + b * g.l_sb + hd * g.l_sh;
-  const float* DEL = g.delta_in + b * g.l_sb + hd * g.l_sh;
-
-  bf16x8 kf[2][4], vf[2][4];
-  bool kmasked[2];
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb) {
-    const int key = k0 + 32 * kb + (lane & 31);
-    load_row_frags(kf[kb], g.k.p + b * g.k.sb + hd * g.k.sh, g.k.sr, key, g.nk, lane);
-    load_row_frags(vf[kb], g.v.p + b * g.v.sb + hd * g.v.sh, g.v.sr, key, g.nk, lane);
-    kmasked[kb] = key_bias(g, b, key) == kNegInf;
-  }
-  floatx16 dvT[2][2], dkT[2][2];
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-    for (int db = 0; db < 2; ++db) dvT[kb][db] = dkT[kb][db] = splat16(0.f);
-
-  const int nt = (g.n + 63) / 64;
-  const void* Qu = uniform_ptr(Q);
-  const void* Du = uniform_ptr(dO);
-  const void* Lu = uniform_ptr(LSE);
-  const void* Eu = uniform_ptr(DEL);
-  auto stage = [&](int buf, int r0) {
-    dma_rows<NW>(lds[buf][0], Qu, g.q.sr, r0, g.n, wid, lane);
-    dma_rows<NW>(lds[buf][1], Du, g.dO.sr, r0, g.n, wid, lane);
-    if (wid == 0) dma_stat(lstat[buf][0], Lu, r0, g.n, lane);
-    else if (wid == 1) dma_stat(lstat[buf][1], Eu, r0, g.n, lane);
-  };
-  auto settle = [&](int buf, int r0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (g.n - r0 < 64) {
-      zero_rows<NW>(lds[buf][0], g.n - r0, tid);
-      zero_rows<NW>(lds[buf][1], g.n - r0, tid);
-      __syncthreads();
-    }
-  };
-  stage(0, 0);
-  settle(0, 0);
-  int cur = 0;
-  for (int t = 0; t < nt; ++t) {
-    const bool more = t + 1 < nt;
-    if (more) stage(cur ^ 1, (t + 1) * 64);
-    const char* lq = lds[cur][0];
-    const char* ld = lds[cur][1];
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      // S' = Q~.K^T - LSE and dP' = dO.V^T - delta for both key sub-blocks from one set of row fragments
-      const floatx16 cs = rows16(lstat[cur][0], 32 * qb, h), cd = rows16(lstat[cur][1], 32 * qb, h);
-      bf16x8 qa[4], da[4];
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) { qa[ks] = frag_rows(lq, 32 * qb, ks, lane); da[ks] = frag_rows(ld, 32 * qb, ks, lane); }
-      floatx16 sc[2], dp[2];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) { sc[kb] = cs; dp[kb] = cd; }
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-          sc[kb] = mfma32(qa[ks], kf[kb][ks], sc[kb]);
-          dp[kb] = mfma32(da[ks], vf[kb][ks], dp[kb]);
-        }
-      __builtin_amdgcn_s_setprio(0);
-      bf16x8 pp[2][2], pd[2][2];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        floatx16 P, dS;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = __builtin_amdgcn_exp2f(sc[kb][i]);
-          P[i] = p;
-          dS[i] = p * dp[kb][i];
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) { pp[kb][s2] = pack_acc(P, s2); pd[kb][s2] = pack_acc(dS, s2); }
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        bf16x8 tv[2], tq[2];
-#pragma unroll
-        for (int db = 0; db < 2; ++db) { tv[db] = frag_tr(ld, db, 2 * qb + s2, lane); tq[db] = frag_tr(lq, db, 2 * qb + s2, lane); }
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int db = 0; db < 2; ++db) {
-            dvT[kb][db] = mfma32(tv[db], pp[kb][s2], dvT[kb][db]);
-            dkT[kb][db] = mfma32(tq[db], pd[kb][s2], dkT[kb][db]);
-          }
-        __builtin_amdgcn_s_setprio(0);
-      }
-    }
-    if (more) settle(cur ^ 1, (t + 1) * 64);
-    cur ^= 1;
-  }
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb) {
-    const int key = k0 + 32 * kb + (lane & 31);
-    store_T(g.dv, (long)b * g.dv.sb + hd * g.dv.sh, dvT[kb], 1.f, key, g.nk, lane, kmasked[kb]);
-    store_T(g.dk, (long)b * g.dk.sb + hd * g.dk.sh, dkT[kb], 0.69314718055994531f, key, g.nk, lane, kmasked[kb]);
-  }
-}
-
-template <int NW, int OCC>
-__global__ __launch_bounds__(64 * NW, OCC) void attn_bwd_dq64_kernel(AttnArgs g) {
-  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];  // [buf][K / V]
-  extern __shared__ __attribute__((aligned(16))) float kbl[];   // key bias of keys kb0.. (fill_key_bias)
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
-  const int b = blockIdx.z, hd = blockIdx.y;
-  const int q0 = blockIdx.x * (64 * NW) + wid * 64;
-  const bf16_t* K = g.k.p + b * g.k.sb + hd * g.k.sh;
-  const bf16_t* V = g.v.p + b * g.v.sb + hd * g.v.sh;
-
-  bf16x8 qf[2][4], df[2][4];
-  floatx16 nlse[2], ndel[2];
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int qrow = q0 + 32 * qb + (lane & 31);
-    load_row_frags(qf[qb], g.q.p + b * g.q.sb + hd * g.q.sh, g.q.sr, qrow, g.n, lane);
-    load_row_frags(df[qb], g.dO.p + b * g.dO.sb + hd * g.dO.sh, g.dO.sr, qrow, g.n, lane);
-    const long lo = b * g.l_sb + hd * g.l_sh + qrow;
-    nlse[qb] = splat16(qrow < g.n ? g.lse[lo] : -__builtin_huge_valf());
-    ndel[qb] = splat16(qrow < g.n ? g.delta_in[lo] : 0.f);
-  }
-  floatx16 dqT[2][2];
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) dqT[qb][0] = dqT[qb][1] = splat16(0.f);
-
-  const int nt = (g.nk + 63) / 64;
-  const void* Ku = uniform_ptr(K);
-  const void* Vu = uniform_ptr(V);
-  fill_key_bias<NW>(kbl, g, b, tid);
-  dma_rows<NW>(lds[0][0], Ku, g.k.sr, 0, g.nk, wid, lane);
-  dma_rows<NW>(lds[0][1], Vu, g.v.sr, 0, g.nk, wid, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int cur = 0;
-  for (int t = 0; t < nt; ++t) {
-    const int kv0 = t * 64;
-    const bool more = t + 1 < nt;
-    if (more) {
-      dma_rows<NW>(lds[cur ^ 1][0], Ku, g.k.sr, kv0 + 64, g.nk, wid, lane);
-      dma_rows<NW>(lds[cur ^ 1][1], Vu, g.v.sr, kv0 + 64, g.nk, wid, lane);
-    }
-    const char* lk = lds[cur][0];
-    const char* lv = lds[cur][1];
-    const bool dense = kv0 + 64 <= g.n_dense;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      bf16x8 ka[4], va[4];
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) { ka[ks] = frag_rows(lk, 32 * kb, ks, lane); va[ks] = frag_rows(lv, 32 * kb, ks, lane); }
-      floatx16 sc[2], dp[2];
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb) { sc[qb] = nlse[qb]; dp[qb] = ndel[qb]; }
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb) {
-          sc[qb] = mfma32(ka[ks], qf[qb][ks], sc[qb]);
-          dp[qb] = mfma32(va[ks], df[qb][ks], dp[qb]);
-        }
-      __builtin_amdgcn_s_setprio(0);
-      bf16x8 pd[2][2];
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
-        if (!dense) {  // scalar branch: only the context / padding key tiles carry a bias
-#pragma unroll
-          for (int g4 = 0; g4 < 4; ++g4) {
-            const floatx4 bias = *reinterpret_cast<const floatx4*>(&kbl[kv0 - g.kb0 + 32 * kb + 8 * g4 + 4 * h]);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) sc[qb][4 * g4 + e] += bias[e];
-          }
-        }
-        floatx16 dS;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) dS[i] = __builtin_amdgcn_exp2f(sc[qb][i]) * dp[qb][i];
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) pd[qb][s2] = pack_acc(dS, s2);
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        bf16x8 tk[2];
-#pragma unroll
-        for (int db = 0; db < 2; ++db) tk[db] = frag_tr(lk, db, 2 * kb + s2, lane);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-          for (int db = 0; db < 2; ++db) dqT[qb][db] = mfma32(tk[db], pd[qb][s2], dqT[qb][db]);
-        __builtin_amdgcn_s_setprio(0);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    cur ^= 1;
-  }
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb)
-    store_T(g.dq, (long)b * g.dq.sb + hd * g.dq.sh, dqT[qb], g.scale, q0 + 32 * qb + (lane & 31), g.n, lane, false);
-}
-
-#endif  // VPT_DIAG
-
-#ifdef VPT_DIAG
-// ------------------------------------------------------------------ backward, fused (diagnostic build)
-// Measured slower than the split pair on this shape (see vpt_attn_bwd); kept for A/B (variant 13).
-// One pass over (key block, query tile) pairs computes all three gradients: the 7 products of the
-// split dK/dV + dQ kernels (whose dQ pass recomputes S and dP) become the 5 the math needs
-// (S, dP, dV, dK, dQ), and Q / dO / lse / delta are streamed once per key block instead of K / V
-// being streamed again per query block.
-//   workgroup = NW waves x 32 keys (128 keys for NW = 4); query tiles of 64 rows, double-buffered
-//   by LDS-DMA (as the dK/dV kernel). Per tile each wave:
-//     S = Q~.K^T - LSE, dP = dO.V^T - delta (key on the lane, 16 MFMAs), P = exp2(S), dS = P * dP;
-//     dV^T += dO^T.P, dK^T += Q~^T.dS (16 MFMAs, as the dK/dV kernel);
-//     dS (bf16) -> LDS as [key][query] rows;       --- barrier ---
-//     dQ tile (32 queries x 32 head dims, wave w: query half w>>1, dim half w&1) = dS[32 q x 128 keys] .
-//     K[128 keys x 32 d] from the dS and K images by transposed reads (8 MFMAs), then 16 no-return f32
-//     atomic adds per lane into the dQ accumulator (global, [bh][q][64]); the next tile's DMA wait is
-//     counted (vmcnt(16)) so those atomics stay in flight.
-// Masked keys (bias -inf) get -inf added to their S chain's initial accumulator (lane = key), so P = dS =
-// 0 for them and they add nothing to dQ (their own dK / dV rows are stored as zeros). Query rows past n
-// are zeroed in LDS (no dK / dV contribution); their dQ rows are scratch rows of the padded accumulator.
-// XCD-aware placement: the key blocks of one (b, h) are consecutive in the remapped block order, so
-// they run on one XCD and that head's Q / dO tiles and dQ partials stay in one L2.
-__device__ __forceinline__ void raw_bar() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-// ABL (diagnostic build, timing only): 1 = no dQ atomics (results wrong), 2 = plain stores in place of the
-// atomics (racy, results wrong), 3 = no dQ product and no atomics (results wrong).
-template <int NW, int ABL = 0>
-__global__ __launch_bounds__(64 * NW, 2) void attn_bwd_fused_kernel(AttnArgs g) {
-  static_assert(NW == 4, "dQ tile split assumes 4 waves (2 query halves x 2 head-dim halves)");
-  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];     // [buf][Q / dO], 64 rows each
-  __shared__ __attribute__((aligned(16))) float lstat[2][2][64];     // [buf][-lse / -delta]
-  __shared__ __attribute__((aligned(16))) char lds_k[NW * 32 * 128];  // K rows of the block [key][64 d]
-  __shared__ __attribute__((aligned(16))) char lds_s[NW * 32 * 128];  // dS of the tile [key][64 q] bf16
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
-  const int nkb = gridDim.x;
-  const int nblk = nkb * gridDim.y * gridDim.z;
-  const int lin = blockIdx.x + nkb * (blockIdx.y + gridDim.y * blockIdx.z);
-  const int xcd = lin & 7, q8 = nblk >> 3, r8 = nblk & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (lin >> 3);
-  const int kblk = wg % nkb, bh = wg / nkb, hd = bh % g.H, b = bh / g.H;
-
-  const int kbase = kblk * (32 * NW);
-  const int key = kbase + wid * 32 + (lane & 31);
-  const int keyrow = wid * 32 + (lane & 31);  // row of this lane's key in lds_k / lds_s
-  const bf16_t* Q = g.q.p + b * g.q.sb + hd * g.q.sh;
-  const bf16_t* dO = g.dO.p + b * g.dO.sb + hd * g.dO.sh;
-  const bf16_t* Kp = g.k.p + b * g.k.sb + hd * g.k.sh;
-  const float* LSE = g.lse + b * g.l_sb + hd * g.l_sh;
-  const float* DEL = g.delta_in + b * g.l_sb + hd * g.l_sh;
-
-  bf16x8 kf[4], vf[4];
-  load_row_frags(kf, Kp, g.k.sr, key, g.nk, lane);
-  load_row_frags(vf, g.v.p + b * g.v.sb + hd * g.v.sh, g.v.sr, key, g.nk, lane);
-  const float kbl = key_bias(g, b, key);  // 0 or -inf
-  const bool kmasked = kbl == kNegInf;
-  const bool any_masked = __builtin_amdgcn_ballot_w64(kbl != 0.f) != 0;  // wave-uniform
-
-  floatx16 dvT[2], dkT[2];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) { dvT[0][i] = dvT[1][i] = dkT[0][i] = dkT[1][i] = 0.f; }
-
-  const int nt = (g.n + 63) / 64;
-  const void* Qu = uniform_ptr(Q);
-  const void* Du = uniform_ptr(dO);
-  const void* Lu = uniform_ptr(LSE);
-  const void* Eu = uniform_ptr(DEL);
-  auto stage = [&](int buf, int r0) {
-    dma_rows<NW>(lds[buf][0], Qu, g.q.sr, r0, g.n, wid, lane);
-    dma_rows<NW>(lds[buf][1], Du, g.dO.sr, r0, g.n, wid, lane);
-    if (wid == 0) dma_stat(lstat[buf][0], Lu, r0, g.n, lane);
-    else if (wid == 1) dma_stat(lstat[buf][1], Eu, r0, g.n, lane);
-  };
-  // prologue: the block's K rows (clamped past nk: finite, and their dS is 0) and query tile 0
-  {
-    const void* Ku = uniform_ptr(Kp);
-#pragma unroll
-    for (int t64 = 0; t64 < NW / 2; ++t64) dma_rows<NW>(lds_k + t64 * 8192, Ku, g.k.sr, kbase + 64 * t64, g.nk, wid, lane);
-  }
-  // Staggered query order: key block kblk starts at tile t0 = kblk * nt / nkb and wraps, so the key blocks
-  // of one head (running together on one XCD) add into different dQ rows at any moment instead of all
-  // hammering the same lines.
-  const int t0 = (int)((long)kblk * nt / nkb);
-  stage(0, t0 * 64);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (g.n - t0 * 64 < 64) {
-    zero_rows<NW>(lds[0][0], g.n - t0 * 64, tid);
-    zero_rows<NW>(lds[0][1], g.n - t0 * 64, tid);
-    __syncthreads();
-  }
-  const int qbw = wid >> 1, dbw = wid & 1;  // this wave's dQ tile: query half, head-dim half
-  float* dqrow = g.dqacc + ((long)bh * g.nq_pad + 32 * qbw + 4 * h) * 64 + 32 * dbw + (lane & 31);
-
-  int cur = 0;
-  for (int i = 0; i < nt; ++i) {
-    const int t = t0 + i < nt ? t0 + i : t0 + i - nt;
-    const int tn = t + 1 < nt ? t + 1 : 0;  // next tile in the wrapped order
-    const bool more = i + 1 < nt;
-    if (more) stage(cur ^ 1, tn * 64);
-    const char* lq = lds[cur][0];
-    const char* ld = lds[cur][1];
-    floatx16 cs = rows16(lstat[cur][0], 0, h), cd = rows16(lstat[cur][1], 0, h);
-    bf16x8 qa[4], da[4], pp[2][2], pd[2][2];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) { qa[ks] = frag_rows(lq, 0, ks, lane); da[ks] = frag_rows(ld, 0, ks, lane); }
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      if (any_masked) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) cs[i] += kbl;
-      }
-      floatx16 s = cs, dp = cd;
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        s = mfma32(qa[ks], kf[ks], s);
-        dp = mfma32(da[ks], vf[ks], dp);
-      }
-      __builtin_amdgcn_s_setprio(0);
-      if (qb == 0) {
-        cs = rows16(lstat[cur][0], 32, h);
-        cd = rows16(lstat[cur][1], 32, h);
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) { qa[ks] = frag_rows(lq, 32, ks, lane); da[ks] = frag_rows(ld, 32, ks, lane); }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      floatx16 P, dS;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(s[i]);
-        P[i] = p;
-        dS[i] = p * dp[i];
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        pp[qb][s2] = pack_acc(P, s2);
-        pd[qb][s2] = pack_acc(dS, s2);
-        // dS rows of this key: queries 32qb + 8g4 + 4h + e, g4 = 2s2 (x, y) and 2s2+1 (z, w)
-        const uint4 v = __builtin_bit_cast(uint4, pd[qb][s2]);
-        *reinterpret_cast<uint2*>(lds_s + tile_off(keyrow, 4 * qb + 2 * s2) + 8 * h) = make_uint2(v.x, v.y);
-        *reinterpret_cast<uint2*>(lds_s + tile_off(keyrow, 4 * qb + 2 * s2 + 1) + 8 * h) = make_uint2(v.z, v.w);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        bf16x8 tv[2], tq[2];
-#pragma unroll
-        for (int db = 0; db < 2; ++db) { tv[db] = frag_tr(ld, db, 2 * qb + s2, lane); tq[db] = frag_tr(lq, db, 2 * qb + s2, lane); }
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {
-          dvT[db] = mfma32(tv[db], pp[qb][s2], dvT[db]);
-          dkT[db] = mfma32(tq[db], pd[qb][s2], dkT[db]);
-        }
-        __builtin_amdgcn_s_setprio(0);
-      }
-    raw_bar();  // every wave's dS rows are in lds_s
-    // dQ[32 q x 32 d] = dS[q, 128 keys] . K[128 keys, d]: both operands by transposed reads
-    floatx16 dq = splat16(0.f);
-    if (ABL != 3) {
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2 * NW; ++ks) dq = mfma32(frag_tr(lds_s, qbw, ks, lane), frag_tr(lds_k, dbw, ks, lane), dq);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    float* dst = dqrow + (long)t * 64 * 64;
-    if (ABL == 0) {
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) unsafeAtomicAdd(dst + (8 * g4 + e) * 64, dq[4 * g4 + e]);
-    } else if (ABL == 2) {
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dst[(8 * g4 + e) * 64] = dq[4 * g4 + e];
-    } else if (ABL == 1) {
-      if (dq[0] == 1234.5f) dst[0] = dq[1];  // keeps the dQ product alive
-    }
-    if (more) {
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // next tile landed; this tile's 16 atomics may fly
-      raw_bar();  // ... for every wave; this tile's Q / dO / dS images are no longer read
-      const int nv = g.n - tn * 64;
-      if (nv < 64) {
-        zero_rows<NW>(lds[cur ^ 1][0], nv, tid);
-        zero_rows<NW>(lds[cur ^ 1][1], nv, tid);
-        __syncthreads();
-      }
-    }
-    cur ^= 1;
-  }
-  store_T(g.dv, (long)b * g.dv.sb + hd * g.dv.sh, dvT, 1.f, key, g.nk, lane, kmasked);
-  store_T(g.dk, (long)b * g.dk.sb + hd * g.dk.sh, dkT, 0.69314718055994531f, key, g.nk, lane, kmasked);
-}
-
-// delta = -rowsum(dO * O) (negated: the dP chains' initial accumulator) and the dQ accumulator rows of the
-// fused backward zeroed; 8 lanes per (b, h, q) row.
-__global__ void attn_bwd_pre_fused_kernel(AttnArgs g, long rows_total) {
-  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long row = gid >> 3;
-  const int part = gid & 7;
-  float s = 0.f;
-  long b = 0, hd = 0, q = 0, bh = 0;
-  if (row < rows_total) {
-    q = row % g.n; bh = row / g.n; hd = bh % g.H; b = bh / g.H;
-    const uint4 a = *reinterpret_cast<const uint4*>(g.dO.p + b * g.dO.sb + hd * g.dO.sh + q * g.dO.sr + part * 8);
-    const uint4 o = *reinterpret_cast<const uint4*>(g.o.p + b * g.o.sb + hd * g.o.sh + q * g.o.sr + part * 8);
-    float fa[8], fo[8];
-    unpack8(a, fa); unpack8(o, fo);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s += fa[e] * fo[e];
-    floatx4* z = reinterpret_cast<floatx4*>(g.dqacc + ((long)bh * g.nq_pad + q) * 64 + part * 8);
-    z[0] = floatx4{0.f, 0.f, 0.f, 0.f};
-    z[1] = floatx4{0.f, 0.f, 0.f, 0.f};
-  }
-  s += __shfl_xor(s, 1, 64);
-  s += __shfl_xor(s, 2, 64);
-  s += __shfl_xor(s, 4, 64);
-  if (row < rows_total && part == 0) g.delta_out[b * g.l_sb + hd * g.l_sh + q] = -s;
-}
-
-// dq = bf16(scale * dQ accumulator) for the n real query rows; 8 lanes per row.
-__global__ void attn_bwd_dq_store_kernel(AttnArgs g, long rows_total) {
-  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long row = gid >> 3;
-  const int part = gid & 7;
-  if (row >= rows_total) return;
-  const long q = row % g.n, bh = row / g.n, hd = bh % g.H, b = bh / g.H;
-  const floatx4* src = reinterpret_cast<const floatx4*>(g.dqacc + ((long)bh * g.nq_pad + q) * 64 + part * 8);
-  const floatx4 a = src[0], c = src[1];
-  uint4 w;
-  w.x = pack_bf16x2(a[0] * g.scale, a[1] * g.scale);
-  w.y = pack_bf16x2(a[2] * g.scale, a[3] * g.scale);
-  w.z = pack_bf16x2(c[0] * g.scale, c[1] * g.scale);
-  w.w = pack_bf16x2(c[2] * g.scale, c[3] * g.scale);
-  *reinterpret_cast<uint4*>(g.dq.p + b * g.dq.sb + hd * g.dq.sh + q * g.dq.sr + part * 8) = w;
-}
-
-#endif  // VPT_DIAG
-
 // Dynamic LDS of the key-bias array (fill_key_bias); n <= 32768 keeps it within 128 KB.
 size_t key_bias_lds_bytes(const AttnArgs& g) { return (size_t)((g.nk + 63) / 64 * 64 - g.kb0) * sizeof(float); }
 
@@ -1157,6 +671,10 @@ int check_common(int B, int H, int n, int nk) {
   VPT_CHECK_ARG(nk <= 32768, "attention: nk <= 32768 (key-bias LDS array)");
   return VPT_OK;
 }
+
+#ifdef VPT_DIAG
+#include "diag/attention_diag_kernels.inc"
+#endif
 
 }  // namespace
 
@@ -1195,19 +713,6 @@ extern "C" int vpt_attn_fwd(const void* q, long q_sb, long q_sh, long q_sr,
   return VPT_OK;
 }
 
-#ifdef VPT_DIAG
-// Diagnostic build: the fused backward (variants 0 / 10-12 there) needs an f32 dQ accumulator,
-// [B*H][round_up(n, 64)][64]; vpt_attn_set_fused_workspace hands it over (process-wide).
-float* g_fused_ws = nullptr;
-extern "C" long vpt_attn_fused_workspace_bytes(int B, int H, int n) {
-  if (B <= 0 || H <= 0 || n <= 0) return 0;
-  return (long)B * H * ((n + 63) / 64 * 64) * 64 * 4;
-}
-extern "C" int vpt_attn_set_fused_workspace(void* ws) {
-  g_fused_ws = (float*)ws;
-  return VPT_OK;
-}
-#endif
 
 extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
                             const void* k, long k_sb, long k_sh, long k_sr,
@@ -1241,45 +746,9 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
   g.H = H;
   hipStream_t s = (hipStream_t)stream;
   const long rows = (long)B * H * n;
+  g.dqacc = nullptr;
 #ifdef VPT_DIAG
-  g.dqacc = g_fused_ws;
-  if (g_variant >= 10 && !g_fused_ws) { vpt_set_error("vpt_attn_bwd: fused variants need vpt_attn_set_fused_workspace"); return VPT_EINVAL; }
-  if (g_variant != 0 || g_waves == 8) {  // the split dK/dV + dQ kernels (A/B and their ablations)
-    hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, s, g, H, rows);
-    VPT_LAUNCH_CHECK();
-    const size_t kbl = key_bias_lds_bytes(g);
-    const dim3 g4((n + 127) / 128, H, B), g8((n + 255) / 256, H, B);  // dQ: over queries
-    const dim3 k4((nk + 127) / 128, H, B), k8((nk + 255) / 256, H, B);  // dK/dV: over keys
-    if (g_variant >= 10 && g_variant <= 13) {
-      hipLaunchKernelGGL(attn_bwd_pre_fused_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, s, g, rows);
-      const dim3 gf((nk + 127) / 128, H, B);
-      if (g_variant == 13) hipLaunchKernelGGL((attn_bwd_fused_kernel<4, 0>), gf, dim3(256), 0, s, g);
-      if (g_variant == 10) hipLaunchKernelGGL((attn_bwd_fused_kernel<4, 1>), gf, dim3(256), 0, s, g);
-      if (g_variant == 11) hipLaunchKernelGGL((attn_bwd_fused_kernel<4, 2>), gf, dim3(256), 0, s, g);
-      if (g_variant == 12) hipLaunchKernelGGL((attn_bwd_fused_kernel<4, 3>), gf, dim3(256), 0, s, g);
-      hipLaunchKernelGGL(attn_bwd_dq_store_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, s, g, rows);
-    } else if (g_variant == 1) {
-      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<1, 4>), k4, dim3(256), 0, s, g);
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<1, 4>), g4, dim3(256), kbl, s, g);
-    } else if (g_variant == 2) {
-      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, 4>), k4, dim3(256), 0, s, g);
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<2, 4>), g4, dim3(256), kbl, s, g);
-    } else if (g_variant == 7) {  // compiler-scheduled dK/dV body (correct results, A/B)
-      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 4>), k4, dim3(256), 0, s, g);
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 4>), g4, dim3(256), kbl, s, g);
-    } else if (g_variant >= 3 && g_variant <= 6) {  // dK/dV-only timing ablations (dQ kernel unchanged)
-      if (g_variant == 3) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<3, 4>), k4, dim3(256), 0, s, g);
-      if (g_variant == 4) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<4, 4>), k4, dim3(256), 0, s, g);
-      if (g_variant == 5) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<5, 4>), k4, dim3(256), 0, s, g);
-      if (g_variant == 6) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<6, 4>), k4, dim3(256), 0, s, g);
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 4>), g4, dim3(256), kbl, s, g);
-    } else {
-      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<0, 8>), k8, dim3(512), 0, s, g);
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 8>), g8, dim3(512), kbl, s, g);
-    }
-    VPT_LAUNCH_CHECK();
-    return VPT_OK;
-  }
+  if (const int rc = diag_attn_bwd_variants(g, B, H, n, nk, s, rows); rc >= 0) return rc;
 #endif
   // production: the split dK/dV pass (explicitly ordered body) + the dQ pass, launched as one grid
   // (attn_bwd_kernel: dK/dV blocks, then dQ blocks). The fused single pass
@@ -1289,21 +758,7 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, s, g, H, rows);
   VPT_LAUNCH_CHECK();
 #ifdef VPT_DIAG
-  if (g_rows64) {  // 64 rows per wave (attn_bwd_dkdv64_kernel / attn_bwd_dq64_kernel)
-    if (g_rows64 & 1)
-      hipLaunchKernelGGL((attn_bwd_dkdv64_kernel<4>), dim3((nk + 255) / 256, H, B), dim3(256), 0, s, g);
-    else
-      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<8, 4>), dim3((nk + 127) / 128, H, B), dim3(256), 0, s, g);
-    VPT_LAUNCH_CHECK();
-    if (g_rows64 & 2)
-      hipLaunchKernelGGL((attn_bwd_dq64_kernel<4, 2>), dim3((n + 255) / 256, H, B), dim3(256), key_bias_lds_bytes(g), s, g);
-    else if (g_rows64 & 4)
-      hipLaunchKernelGGL((attn_bwd_dq64_kernel<4, 1>), dim3((n + 255) / 256, H, B), dim3(256), key_bias_lds_bytes(g), s, g);
-    else
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<0, 4>), dim3((n + 127) / 128, H, B), dim3(256), key_bias_lds_bytes(g), s, g);
-    VPT_LAUNCH_CHECK();
-    return VPT_OK;
-  }
+  if (const int rc = diag_attn_bwd_rows64(g, B, H, n, nk, s); rc >= 0) return rc;
 #endif
   const int nkb = (nk + 127) / 128, nqb = (n + 127) / 128;
   hipLaunchKernelGGL(attn_bwd_kernel, dim3((nkb + nqb) * H * B), dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
@@ -1312,31 +767,5 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
 }
 
 #ifdef VPT_DIAG
-// Test hook: the forward lazy-rescale threshold (log2 units; 0 = rescale whenever the max grows).
-extern "C" int vpt_attn_set_rescale_threshold(float tau) {
-  VPT_CHECK_ARG(tau >= 0.f && tau <= 64.f, "vpt_attn_set_rescale_threshold: tau in [0, 64]");
-  g_tau = tau;
-  return VPT_OK;
-}
-
-// A/B hook: 1 = the 64-rows-per-wave backward pair (production), 0 = the 32-row pair.
-extern "C" int vpt_attn_set_rows64(int on) {
-  g_rows64 = on;
-  return VPT_OK;
-}
-
-// Benchmark hook: kernel variant (0 = production: split dK/dV + dQ kernels; 13 = the fused single pass
-// with dQ atomics (correct; needs vpt_attn_set_fused_workspace), 10-12 = its timing ablations (wrong
-// results: no atomics / plain stores / no dQ product); 1, 2 = timing-only backward ablations
-// whose results are wrong: 1 = no in-loop tile staging, 2 = row reads in place of transposed reads;
-// 3 = 8-wave blocks, correct, A/B only; dK/dV-kernel-only ablations (wrong results): 4 = no exp2,
-// 5 = 4 of the 16 dV/dK MFMAs, 6 = no transposed LDS reads, 7 = no S/dP LDS reads; 8 = the
-// compiler-scheduled dK/dV body the production ordered body replaced, correct, A/B).
-extern "C" int vpt_attn_set_variant(int v) {
-  VPT_CHECK_ARG(v >= 0 && v <= 13 && v != 9, "vpt_attn_set_variant: 0..8, 10..13");
-  if (v >= 10) { g_variant = v; g_waves = 4; return VPT_OK; }
-  g_variant = v == 3 ? 0 : (v >= 4 ? v - 1 : v);
-  g_waves = v == 3 ? 8 : 4;
-  return VPT_OK;
-}
+#include "diag/attention_diag_api.inc"
 #endif  // VPT_DIAG

@@ -34,6 +34,7 @@ __device__ __forceinline__ float gauss(uint64_t seed, uint64_t idx) {
 __global__ void flow_noise_kernel(const bf16_t* __restrict__ x, const float* __restrict__ t, long n_per, long total,
                                   float noise_scale, int clean_at_zero, uint64_t seed, const bf16_t* __restrict__ eps_in,
                                   bf16_t* __restrict__ z, bf16_t* __restrict__ eps_out) {
+#pragma clang fp contract(off)  // torch: two f32 products and one add, each rounded (no FMA)
   const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
   if (i >= total) return;
   const float tb = t[i / n_per];

@@ -35,7 +35,7 @@ def _needs(obj: Path, deps: list[Path]) -> bool:
 
 def _compile(src: Path, diag: bool = False) -> Path:
     obj = (BUILD_DIAG if diag else BUILD) / (src.stem + ".o")
-    deps = [src] + sorted(CSRC.glob("*.h"))
+    deps = [src] + sorted(CSRC.glob("*.h")) + (sorted((CSRC / "diag").glob("*.inc")) if diag else [])
     if _needs(obj, deps):
         cmd = [HIPCC, *CFLAGS, *UNIT_FLAGS.get(src.name, []), *(["-DVPT_DIAG"] if diag else []), "-c", str(src), "-o",
                str(obj)]
