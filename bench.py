@@ -311,8 +311,8 @@ def main():
 def bench_c5(args):
     """BASELINE config 5 on one GPU: the SDXL flow-matching QLoRA step (train/sdxl/flow_match.py:109-174) at
     1024^2 (latents 4 x 128 x 128), batch 4 (configs/sdxl/flow_match/config.yml): t ~ scale_shift_sigmoid,
-    noising, the UNet's 11 SpatialTransformers (70 blocks, 700 LoRA r=16 targets, NF4 bases dequantised inside
-    the GEMMs) inside a frozen skeleton of the UNet's topology (its ResNet / conv path is outside SURVEY §8),
+    noising, the UNet's 11 SpatialTransformers (70 blocks, 700 LoRA r=16 targets over NF4 bases, dequantised per
+    call as bitsandbytes' MatMul4Bit does -- vpt.sdxl.BASE_MODES, VPT_NF4_BASE) inside a frozen skeleton of the UNet's topology (its ResNet / conv path is outside SURVEY §8),
     velocity MSE, backward, RAdamScheduleFree on the adapters (vpt/sdxl_flow.py)."""
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         raise SystemExit("--workload c5 is a 1-GPU configuration")
@@ -332,7 +332,7 @@ def bench_c5(args):
     dt = time.perf_counter() - t0
     loss = m.loss.item()
     # probe pass after the timed region: NF4 GEMM and attention launches timed with HIP events
-    probes = {k: ops.KernelProbe(k) for k in ("gemm_nf4", "attn_fwd", "attn_bwd", "gemm")}
+    probes = {k: ops.KernelProbe(k) for k in ("gemm_lora", "gemm_nf4", "attn_fwd", "attn_bwd", "gemm", "nf4_dequant")}
     ops.PROBES.update(probes)
     for p in probes.values():
         p.active = True
@@ -344,9 +344,20 @@ def bench_c5(args):
     kern = {}
     for k, pr in probes.items():
         n, ms, fl = pr.summary()
-        kern[k] = dict(launches=n, mean_ms=round(ms, 4), total_ms=round(n * ms, 3),
-                       tflops=round(fl / (ms * 1e-3) / 1e12, 2) if ms else 0.0)
-    n, ms, fl = probes["gemm_nf4"].summary()
+        if k == "nf4_dequant":  # HBM-bound: algorithmic bytes / time
+            kern[k] = dict(launches=n, mean_ms=round(ms, 4), total_ms=round(n * ms, 3),
+                           gb_s=round(fl / (ms * 1e-3) / 1e9, 1) if ms else 0.0,
+                           frac=round(fl / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 3) if ms else 0.0)
+        else:
+            kern[k] = dict(launches=n, mean_ms=round(ms, 4), total_ms=round(n * ms, 3),
+                           tflops=round(fl / (ms * 1e-3) / 1e12, 2) if ms else 0.0)
+    if args.breakdown:  # per-shape totals of the base+LoRA GEMMs over the probed step
+        rows = {k: dict(launches=n, total_ms=round(t, 3), tflops=round(w / (t * 1e-3) / 1e12, 1))
+                for k, (n, t, w) in sorted(probes["gemm_lora"].by_key().items(), key=lambda kv: -kv[1][1])}
+        json.dump(rows, open(args.breakdown, "w"), indent=1)
+    # headline roofline: the MFMA op with the largest total time in the step
+    dom = max((k for k in kern if k != "nf4_dequant"), key=lambda k: kern[k]["total_ms"])
+    n, ms, fl = probes[dom].summary()
     tf = fl / (ms * 1e-3) / 1e12 if ms else 0.0
     step_tf = m.flops_per_step() / 1e12
     res = {
@@ -361,8 +372,9 @@ def bench_c5(args):
                                "pixel-(un)shuffle + Linear maps (outside SURVEY §8); VAE and text encoders not run",
                    "global_batch": B, "lora_rank": 16, "lora_alpha": 1.0, "adapter_params": m.n_adapter_params(),
                    "loss": "flow-matching velocity MSE (loss_with_predicted_velocity)",
+                   "nf4_base": __import__("vpt.sdxl", fromlist=["x"]).DEFAULT_BASE_MODE,
                    "optimizer": "RAdamScheduleFree (fused HIP)"},
-        "roofline": {"bound": "mfma", "kernel": "gemm_nf4", "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS,
+        "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(tf / PEAK_BF16_TFLOPS, 4), "traffic": None,
                      "mean_launch_ms": round(ms, 4), "launches_per_step": n},
         "kernels": kern,

@@ -32,7 +32,8 @@ const char* vpt_build_info(void);
  * C[M,N] (=|+=) sum_k A(m,k) B(n,k) (+bias[n]) (+resid[m,n]) (SiLU).
  * A(m,k) = A[m*lda + k] if a_kmajor else A[k*lda + m]; same for B with n.
  * out_mode 0 = bf16 store, 1 = f32 store, 2 = f32 accumulate; act 0 = none, 1 = SiLU.
- * splits > 1: split-K into f32 slabs in `workspace` (vpt_gemm_workspace_bytes), deterministic sum.
+ * splits > 1: split-K into f32 slabs in `workspace` (vpt_gemm_workspace_bytes), deterministic sum; the
+ * slab reduce applies bias / residual (bf16 output; no SiLU, alpha 1).
  * Replaces nn.Linear / 1x1 & patch Conv2d forward and their autograd backward:
  *   src/models/jit/denoiser.py:36-49,59-65 (BottleneckPatchEmbed), :80-84 (TimestepEmbedder MLP),
  *   :318-323,360-366,391-395 (Attention to_q/k/v/o), :492-504 (SwiGLU), :535-543 (FinalLayer),
@@ -49,6 +50,29 @@ int vpt_gemm_bf16_tiled(const void* A, long lda, int a_kmajor, const void* B, lo
                         long ldc, int M, int N, int K, const void* bias, const void* resid, long ldr, int out_mode,
                         int act, int splits, void* workspace, float alpha, int geometry, int ring_grid,
                         void* stream);
+/* LoRALinear over a frozen base (src/modules/peft/lora.py:92-104; the QLoRA targets of
+ * configs/sdxl/flow_match/config.yml), the base GEMM and the LoRA term in one f32 accumulator:
+ * C[M,N] = A.B (+bias) (+resid, as vpt_gemm_bf16) + A2.B2 over K2 extra reduction elements.
+ *   forward:        A = x [M][K], B = W [N][K] (b_kmajor 1), A2 = s*x.down^T [M][r], B2 = up [N][r]
+ *   input gradient: A = dy [M][N_out], B = W [N_out][K_in] (b_kmajor 0), A2 = s*dy.up [M][r], B2 = down [r][K_in]
+ * W is the bf16 base weight (for an NF4 base: vpt_nf4_dequant's output, exactly what bitsandbytes'
+ * MatMul4Bit dequantises before its torch.nn.functional.linear). A, A2 k-major; K % 64 == 0; K2 % 8 == 0,
+ * 0 < K2 <= 256 (several adapters side by side: K2 = their ranks summed, B2 block-diagonal); splits > 1:
+ * split-K over `workspace` (vpt_gemm_workspace_bytes; the extension rides the last slice, bias / residual are
+ * applied by the slab reduce); geometry as vpt_gemm_bf16_tiled (0 = automatic). Deterministic. */
+int vpt_gemm_bf16_lora(const void* A, long lda, const void* B, long ldb, int b_kmajor, const void* A2, long lda2,
+                       const void* B2, long ldb2, int K2, void* C, long ldc, int M, int N, int K, const void* bias,
+                       const void* resid, long ldr, int out_mode, int splits, void* workspace, int geometry,
+                       void* stream);
+/* Several LoRA targets reading one input (the attention q / k / v projections of a TransformerBlock,
+ * src/models/sdxl/denoiser.py:101-171 over lora.py:92-104) as ONE GEMM: B = the G base weights stacked
+ * [G*g_n][K] (k-major), C[:, g*g_n:(g+1)*g_n] = A.W_g^T (+bias, +resid) + A2[:, g*r:(g+1)*r].up_g^T with
+ * up_g = B2s[g] ([g_n][r], k-major). 1 <= G <= 4, r % 8 == 0, r <= 64, g_n % 128 == 0 (a 256-wide ring tile is
+ * used only when g_n % 256 == 0), K % 64 == 0; splits / workspace / geometry as vpt_gemm_bf16_lora. */
+int vpt_gemm_bf16_lora_grouped(const void* A, long lda, const void* B, long ldb, const void* A2, long lda2,
+                               const void* const* B2s, int G, int r, void* C, long ldc, int M, int g_n, int K,
+                               const void* bias, const void* resid, long ldr, int splits, void* workspace,
+                               int geometry, void* stream);
 /* nn.Linear weight and bias gradient in one call (torch autograd of F.linear for every Linear of
  * src/models/jit/denoiser.py, e.g. :318-323 attention projections, :492-504 SwiGLU, :535-543 FinalLayer):
  * dw[N][K] (=|+=) dy[M][N]^T . x[M][K] and, if db != NULL, db[N] (=|+=) sum_m dy[m][N], both f32
@@ -221,6 +245,19 @@ int vpt_geglu_bwd(const void* dy, const void* x12, long ldx, int F, long M, void
  * quantize (quantize_4bit, load time) uses absmax_scratch f32 [n/64]. */
 int vpt_nf4_dequant(const void* packed, const void* qabsmax, const float* absmax2, const float* code2,
                     const float* offset, long n, void* out, void* stream);
+/* Up to 16 NF4 tensors dequantised in one launch (a transformer block's LoRA bases before its forward or its
+ * input-gradient GEMMs: bnb's per-call dequantize_4bit of each Linear4bit, batched); same values as
+ * vpt_nf4_dequant. Each job: n % 64 == 0. */
+typedef struct {
+  const void* packed;
+  const void* qabsmax;
+  const float* absmax2;
+  const float* code2;
+  const float* offset;
+  void* out;
+  long n;
+} VptNf4Job;
+int vpt_nf4_dequant_batch(const VptNf4Job* jobs, int njobs, void* stream);
 /* NF4 dequant-in-GEMM with the LoRA up-projection fused as one extra K tile (replaces, per QLoRA target,
  * LoRALinear.forward src/modules/peft/lora.py:92-104 = Linear4bit's dequantize_4bit + matmul
  * (src/modules/quant/bnb.py:37-129) + lora_up(lora_down(x)) * scale + add, and their input gradient).
@@ -290,6 +327,9 @@ int vpt_space_to_depth(const void* src, void* dst, int B, int C, int H, int W, i
 /* Elementwise bf16: out = a + b (residual sums), out = s * a (LoRA scale gradient); n % 8 == 0. */
 int vpt_add_bf16(const void* a, const void* b, long n, void* out, void* stream);
 int vpt_scale_bf16(const void* a, long n, float s, void* out, void* stream);
+/* out[r][c] = s * a[r][c] on a row-strided [rows][cols] block (in place allowed; cols, lda, ldo % 8 == 0): the
+ * attention q pre-scale (vpt_attn_q_scale) of a q that is a column block of a fused q | k | v output. */
+int vpt_scale_bf16_2d(const void* a, long lda, long rows, int cols, float s, void* out, long ldo, void* stream);
 int vpt_nf4_quantize(const void* w, long n, const float* code2, void* packed, void* qabsmax, float* absmax2,
                      float* offset, float* absmax_scratch, void* stream);
 

@@ -154,6 +154,139 @@ def test_gemm_nf4_bit_exact_vs_dequant_gemm(ops, forward, lora):
     assert torch.equal(out, ref), (out.float() - ref.float()).abs().max().item()
 
 
+@pytest.mark.parametrize("geometry,splits", [(128, 1), (256, 1), (256, 3), (128, 2)])
+@pytest.mark.parametrize("forward", [True, False])
+@pytest.mark.parametrize("r", [16, 48])
+def test_gemm_lora_bit_exact_vs_concatenated_gemm(ops, geometry, splits, forward, r):
+    """vpt_gemm_bf16_lora (the LoRA term as a K-extension of the base GEMM) == one bf16 GEMM of the same
+    geometry over the concatenated operands [A | A2 | 0] . [B | B2 | 0] (the extension tile zero-padded to the
+    geometry's K step: 64 for T128, 32 for the ring): the same MFMA sequence, so bit-exact. Partial M and N
+    tiles, bias and residual epilogues; r = 48 is three adapters side by side (a block-diagonal B2). Split-K (the
+    extension in the last slice, bias / residual in the slab reduce) equals the same split of the concatenated GEMM."""
+    M, Nw, Kw = 600, 1280, 640
+    N, K = (Nw, Kw) if forward else (Kw, Nw)
+    W = rnd(Nw, Kw, scale=0.05, seed=30)
+    a = rnd(M, K, seed=31)
+    a2 = rnd(M, r, scale=0.5, seed=32)
+    b2 = rnd(N, r, scale=0.1, seed=33) if forward else rnd(r, N, scale=0.1, seed=33)
+    bias = rnd(N, scale=0.1, seed=34) if forward else None
+    resid = rnd(M, N, seed=35)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops.gemm_lora(a, W, forward, a2, b2, M, N, K, out, bias=bias, resid=resid, geometry=geometry, splits=splits)
+    step = 64 if geometry == 128 else 32
+    pad = (r + step - 1) // step * step
+    ac = torch.zeros(M, K + pad, dtype=torch.bfloat16, device=DEV)
+    ac[:, :K], ac[:, K:K + r] = a, a2
+    if forward:
+        bc = torch.zeros(N, K + pad, dtype=torch.bfloat16, device=DEV)
+        bc[:, :K], bc[:, K:K + r] = W, b2
+    else:
+        bc = torch.zeros(K + pad, N, dtype=torch.bfloat16, device=DEV)
+        bc[:K], bc[K:K + r] = W, b2
+    ref = torch.empty_like(out)
+    if splits == 1:
+        ops.gemm(ac, True, bc, forward, M, N, K + pad, ref, bias=bias, resid=resid, geometry=geometry)
+    else:  # the same K slices: the concatenated K split at the base GEMM's slice length
+        sl = ((K + splits - 1) // splits + 63) // 64 * 64
+        parts = [(k0, min(K, k0 + sl)) for k0 in range(0, K, sl)]
+        acc = torch.zeros(M, N, dtype=torch.float32, device=DEV)
+        for i, (k0, k1) in enumerate(parts):
+            last = i == len(parts) - 1
+            kk = slice(k0, (K + pad) if last else k1)
+            sl_out = torch.empty(M, N, dtype=torch.float32, device=DEV)
+            ops.gemm(ac[:, kk].contiguous(), True, (bc[:, kk] if forward else bc[kk]).contiguous(), forward, M, N,
+                     (K + pad if last else k1) - k0, sl_out, out_mode=ops.OUT_F32, geometry=geometry)
+            acc += sl_out
+        y = acc + (bias.float() if bias is not None else 0.0)
+        ref = (y.bfloat16().float() + resid.float()).bfloat16()
+    torch.cuda.synchronize()
+    if splits == 1:
+        assert torch.equal(out, ref), (out.float() - ref.float()).abs().max().item()
+    else:  # slab sum order (z = 0, 1, ...) equals the += order above; per-slice MFMA order as the slice GEMM
+        assert rel(out, ref) < 1e-3
+    # and against fp32 math: bf16(bf16(A.B + bias + A2.B2) + resid)
+    Bf = W.float() if forward else W.float().t()
+    B2f = b2.float() if forward else b2.float().t()
+    y = a.float() @ Bf.t() + a2.float() @ B2f.t() + (bias.float() if bias is not None else 0.0)
+    assert rel(out.float() - resid.float(), y) < 1e-2
+
+
+@pytest.mark.parametrize("gn,geometry", [(1280, 128), (1280, 256), (640, 128)])
+def test_gemm_lora_grouped_bit_exact_vs_per_target(ops, gn, geometry):
+    """vpt_gemm_bf16_lora_grouped (q | k | v of one input as one GEMM, each column block with its own LoRA term)
+    == three vpt_gemm_bf16_lora calls of the same geometry, column block by column block (bit-exact)."""
+    M, K, r = 700, 1280, 16
+    x = rnd(M, K, seed=50)
+    Ws = [rnd(gn, K, scale=0.03, seed=51 + g) for g in range(3)]
+    ups = [rnd(gn, r, scale=0.1, seed=55 + g) for g in range(3)]
+    ds = rnd(M, 3 * r, scale=0.5, seed=59)
+    out = torch.empty(M, 3 * gn, dtype=torch.bfloat16, device=DEV)
+    ops.gemm_lora_grouped(x, torch.cat(Ws, 0), ds, ups, out, geometry=geometry)
+    for g in range(3):
+        ref = torch.empty(M, gn, dtype=torch.bfloat16, device=DEV)
+        ops.gemm_lora(x, Ws[g], True, ds[:, g * r:(g + 1) * r].contiguous(), ups[g], M, gn, K, ref, geometry=geometry,
+                      splits=1)
+        torch.cuda.synchronize()
+        assert torch.equal(out[:, g * gn:(g + 1) * gn], ref), g
+
+
+def test_sdxl_block_fused_qkv_matches_per_target(ops, monkeypatch):
+    """The block's fused q|k|v GEMMs (forward and input gradient) against the per-target LoRALinear path on the same
+    weights and inputs: output, input / context gradients and every adapter gradient within bf16 rounding (the
+    fused input gradient sums the three projections' contributions in f32 before one rounding)."""
+    from vpt import sdxl
+    fx, d, sd = _block_inputs()
+    res = []
+    for fuse in (True, False):
+        blk = sdxl.SDXLTransformerBlock(d["dim"], d["heads"], d["context_dim"], d["rank"], d["alpha"], sd)
+        for t in sdxl.TARGETS:  # non-zero ups so every adapter term is live
+            blk.lin[t].up = rnd(*blk.lin[t].up.shape, scale=0.05, seed=70 + sdxl.TARGETS.index(t))
+        if not fuse:
+            monkeypatch.setattr(blk, "_fuse_qkv", lambda Wb: False)
+        B, n, nc = 2, 80, 20
+        x = rnd(B * n, d["dim"], seed=60)
+        ctx = rnd(B * nc, d["context_dim"], seed=61)
+        y = blk.forward(x, ctx, B, n, nc)
+        dx, dctx = blk.backward(rnd(B * n, d["dim"], scale=0.1, seed=62))
+        torch.cuda.synchronize()
+        res.append((y, dx, dctx, {t: (blk.lin[t].g_up.clone(), blk.lin[t].g_down.clone()) for t in sdxl.TARGETS}))
+    (y0, dx0, c0, g0), (y1, dx1, c1, g1) = res
+    assert torch.equal(y0, y1)  # the grouped forward is per-column-block identical
+    assert rel(dx0, dx1) < 5e-3 and rel(c0, c1) < 5e-3
+    for t in sdxl.TARGETS:
+        assert rel(g0[t][0], g1[t][0]) < 5e-3 and rel(g0[t][1], g1[t][1]) < 5e-3, t
+
+
+@pytest.mark.parametrize("mode", ["dequant", "resident", "inline"])
+def test_lora_linear_nf4_base_modes_agree(ops, mode):
+    """The three ways the NF4 base enters the GEMM (vpt.sdxl.BASE_MODES) on one LoRA target at the config-5
+    1280-channel shape: "dequant" (bitsandbytes MatMul4Bit: dequantise per call, bf16 GEMM) and "resident" are
+    bitwise identical; "inline" (dequant inside the GEMM) agrees to bf16 rounding of differently ordered sums."""
+    from vpt.sdxl import LoRALinearNF4, NF4Weight
+    g = torch.Generator().manual_seed(40)
+    st = SO.nf4_quantize(torch.randn(1280, 1280, generator=g) * 0.03)
+    base = NF4Weight.from_state(dict(st, shape=torch.tensor([1280, 1280])))
+    down, up = rnd(16, 1280, scale=0.05, seed=41), rnd(1280, 16, scale=0.05, seed=42)
+    bias = rnd(1280, scale=0.1, seed=43)
+    x, dy, res = rnd(4096, 1280, seed=44), rnd(4096, 1280, seed=45), rnd(4096, 1280, seed=46)
+    out = []
+    for md in ("dequant", mode):
+        lin = LoRALinearNF4(base, bias, down, up, alpha=1.0, rank=16, base_mode=md)
+        y = lin.forward(x, resid=res)
+        dx = lin.backward(dy)
+        out.append((y, dx, lin.g_up.clone(), lin.g_down.clone()))
+    for u, v in zip(*out):
+        if mode == "inline":
+            assert rel(u, v) < 5e-3
+        else:
+            assert torch.equal(u, v)
+    # the dequant path against fp32 math on the oracle's dequantised base
+    W = SO.nf4_dequantize(st).bfloat16().float().to(DEV)
+    ds = (x.float() @ down.float().t() * (1.0 / 16)).bfloat16().float()
+    yr = x.float() @ W.t() + bias.float() + ds @ up.float().t()
+    assert rel(out[0][0].float() - res.float(), yr) < 1e-2
+
+
 def test_lora_linear_nf4_fused_vs_dequant_path(ops):
     """The fused LoRALinearNF4 path and the dequant-to-scratch path agree (same math, one vs three bf16
     roundings of the LoRA sum): rel <= 1e-2 on y, dx and both adapter grads, at SDXL's 640 / 2048 widths."""

@@ -57,6 +57,17 @@ struct GemmArgs {
   // ring kernel: start delay (s_memrealtime ticks, 10 ns) of the blocks with bit 3 of blockIdx set, so
   // that half the CUs reach their (HBM-bound) epilogues while the other half run K loops (0 = off)
   int stagger;
+  // K-extension (LoRA, vpt_gemm_bf16_lora): K2 more reduction elements from A2 (k-major [M][K2]) and B2 (the
+  // layout of B: k-major [N][K2] or mn-major [K2][N]) after the K of A / B, in the same f32 accumulator.
+  // K2 = 0: none. With K2 > 0: one split, K % 64 == 0.
+  const bf16_t* A2; long lda2;
+  const bf16_t* B2; long ldb2;
+  int K2;
+  // grouped K-extension (forward of several LoRA targets sharing one input, outputs side by side): output
+  // columns [g * g_n, (g + 1) * g_n) take their extension from A2 columns [g * K2, (g + 1) * K2) and B2g[g]
+  // ([g_n][K2], k-major); g_n = 0: ungrouped (B2). Tiles never straddle groups (g_n % tile width == 0).
+  const bf16_t* B2g[4];
+  int g_n;
 };
 
 // ---- LDS images -----------------------------------------------------------------------------
@@ -277,6 +288,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_bf16_kernel(GemmArgs g
   const int kend = min(g.K, kbeg + g.k_split);
   const int nfull = (kend - kbeg) / BK;
   const bool ktail = (kend - kbeg) % BK != 0;
+  // K-extension tiles (K % BK == 0): in the last split's K loop only
+  const int next = g.K2 > 0 && (int)blockIdx.y == g.splits - 1 ? (g.K2 + BK - 1) / BK : 0;
 
   floatx4 acc[G::MI][G::NI];
 #pragma unroll
@@ -287,12 +300,27 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_bf16_kernel(GemmArgs g
   // Main loop: LDS-DMA only (no ordinary VGPR loads in the loop), next tile in flight while this one
   // computes. A partial last K tile (wgrad over a token count) is DMA'd with clamped addresses and
   // its out-of-range k rows / chunks are zeroed in LDS before it is consumed.
-  const int nk = nfull + (ktail ? 1 : 0);
+  const int nkm = nfull + (ktail ? 1 : 0);  // main K tiles
+  const int nk = nkm + next;
+  // tile t -> its valid k and the DMA of both operands into `buf` (main K, then the K-extension)
+  auto issue = [&](char* buf, int t) -> int {
+    if (t < nkm) {
+      const int k0 = kbeg + t * BK, kv = min(BK, kend - k0);
+      glds_tile<AK, TM, G::NW>(buf, tile_ptr<AK>(g.A, g.lda, m0, k0), g.lda, m0, g.M, kv, wid, lane);
+      glds_tile<BK_, TN, G::NW>(buf + G::A_BYTES, tile_ptr<BK_>(g.B, g.ldb, n0, k0), g.ldb, n0, g.N, kv, wid, lane);
+      return kv;
+    }
+    const int e0 = (t - nkm) * BK, kv = min(BK, g.K2 - e0);
+    const int grp = g.g_n > 0 ? n0 / g.g_n : 0;  // grouped extension: this tile's target
+    const bf16_t* b2 = g.g_n > 0 ? g.B2g[grp] : g.B2;
+    const int nb0 = n0 - grp * g.g_n, nrows = g.g_n > 0 ? g.g_n : g.N;
+    glds_tile<AK, TM, G::NW>(buf, tile_ptr<AK>(g.A2 + grp * g.K2, g.lda2, m0, e0), g.lda2, m0, g.M, kv, wid, lane);
+    glds_tile<BK_, TN, G::NW>(buf + G::A_BYTES, tile_ptr<BK_>(b2, g.ldb2, nb0, e0), g.ldb2, nb0, nrows, kv, wid, lane);
+    return kv;
+  };
   int cur = 0;
   {
-    const int kv = min(BK, kend - kbeg);
-    glds_tile<AK, TM, G::NW>(smem, tile_ptr<AK>(g.A, g.lda, m0, kbeg), g.lda, m0, g.M, kv, wid, lane);
-    glds_tile<BK_, TN, G::NW>(smem + G::A_BYTES, tile_ptr<BK_>(g.B, g.ldb, n0, kbeg), g.ldb, n0, g.N, kv, wid, lane);
+    const int kv = issue(smem, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (kv < BK) {
@@ -302,13 +330,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_bf16_kernel(GemmArgs g
     }
   }
   for (int kt = 0; kt < nk; ++kt) {
-    const int kn = kbeg + (kt + 1) * BK;
-    const int kv = min(BK, kend - kn);  // valid k rows of the next tile (<= 0: no next tile)
     char* nb = smem + (cur ^ 1) * G::STAGE;
-    if (kv > 0) {
-      glds_tile<AK, TM, G::NW>(nb, tile_ptr<AK>(g.A, g.lda, m0, kn), g.lda, m0, g.M, kv, wid, lane);
-      glds_tile<BK_, TN, G::NW>(nb + G::A_BYTES, tile_ptr<BK_>(g.B, g.ldb, n0, kn), g.ldb, n0, g.N, kv, wid, lane);
-    }
+    const int kv = kt + 1 < nk ? issue(nb, kt + 1) : 0;  // valid k rows of the next tile (0: no next tile)
     mma_tile<AK, BK_, G>(smem + cur * G::STAGE, acc, wm, wn, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA for tile kt+1 has landed
     __syncthreads();                                   // ... and every other wave's too
@@ -496,6 +519,11 @@ __device__ __forceinline__ RingItem ring_item(const GemmArgs& g, int item, int i
   it.kend = min(g.K, it.kbeg + g.k_split);
   it.nk = (it.kend - it.kbeg + RBK - 1) / RBK;
   it.klast = it.kend - it.kbeg - (it.nk - 1) * RBK;  // valid k of the last tile (1..32)
+  if (g.K2 > 0 && it.split == g.splits - 1) {  // K-extension tiles after the main K (K % 64 == 0), last split
+    const int ne = (g.K2 + RBK - 1) / RBK;
+    it.nk += ne;
+    it.klast = g.K2 - (ne - 1) * RBK;
+  }
   it.va0 = tile_voff<AK, 256>(g.lda, it.m0, g.M, RBK, wid, lane, 0);
   it.va1 = tile_voff<AK, 256>(g.lda, it.m0, g.M, RBK, wid, lane, 1);
   if (SW) {
@@ -515,6 +543,19 @@ __device__ __forceinline__ void ring_issue(const GemmArgs& g, const RingItem& it
   constexpr int A32 = 256 * RBK * 2, STAGE32 = 2 * A32;
   const uint32_t la = __builtin_amdgcn_readfirstlane(lds0 + (t & (RSTAGES - 1)) * STAGE32);
   const int k0 = it.kbeg + t * RBK;
+  if (k0 >= it.kend) {  // K-extension tile (A2 / B2); its k >= K2 lanes are masked like a partial last tile
+    const int e0 = k0 - it.kend, kv = min(RBK, g.K2 - e0);
+    const int grp = g.g_n > 0 ? it.n0 / g.g_n : 0;  // grouped extension: this tile's target
+    const bf16_t* b2 = g.g_n > 0 ? g.B2g[grp] : g.B2;
+    const int nb0 = it.n0 - grp * g.g_n, nrows = g.g_n > 0 ? g.g_n : g.N;
+    const void* ab = uniform_ptr(tile_ptr<AK>(g.A2 + grp * g.K2, g.lda2, it.m0, e0));
+    const void* bb = uniform_ptr(tile_ptr<BK_>(b2, g.ldb2, nb0, e0));
+    glds_step(ab, bb, tile_voff<AK, 256>(g.lda2, it.m0, g.M, kv, wid, lane, 0),
+              tile_voff<AK, 256>(g.lda2, it.m0, g.M, kv, wid, lane, 1),
+              tile_voff<BK_, 256>(g.ldb2, nb0, nrows, kv, wid, lane, 0),
+              tile_voff<BK_, 256>(g.ldb2, nb0, nrows, kv, wid, lane, 1), la, la + 1024, la + A32, la + A32 + 1024);
+    return;
+  }
   const int kv = min(RBK, it.kend - k0);
   const void* ab = uniform_ptr(tile_ptr<AK>(g.A, g.lda, it.m0, k0));
   const void* bb = uniform_ptr(tile_ptr<BK_>(g.B, g.ldb, SW ? 0 : it.n0, k0));
@@ -1074,7 +1115,8 @@ int launch_geo(const GemmArgs& g, int splits, int geo, hipStream_t s) {
 // per-split row sums of a fused bias gradient (blocks from cblocks: rout[m] (+)= sum_z rpart[z][m]).
 __global__ void splitk_reduce_kernel(const float* __restrict__ part, long n, int splits, long stride,
                                      void* out, int out_mode, long cblocks, const float* __restrict__ rpart,
-                                     int rsplits, int rn, float* rout, int racc) {
+                                     int rsplits, int rn, float* rout, int racc, const bf16_t* __restrict__ bias,
+                                     const bf16_t* __restrict__ resid, long ldr, int ncols) {
   if ((long)blockIdx.x >= cblocks) {
     const long m = ((long)blockIdx.x - cblocks) * blockDim.x + threadIdx.x;
     if (m >= rn) return;
@@ -1087,6 +1129,21 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ part, long n, int
   if (i4 >= n) return;
   floatx4 s = *reinterpret_cast<const floatx4*>(part + i4);
   for (int z = 1; z < splits; ++z) s += *reinterpret_cast<const floatx4*>(part + z * stride + i4);
+  if (bias || resid) {  // the GEMM epilogue's bias / residual, applied to the summed slabs (bf16 output)
+    const long row = i4 / ncols, col = i4 - row * ncols;
+    if (bias) {
+      const uint2 bv = *reinterpret_cast<const uint2*>(bias + col);
+      s[0] += __uint_as_float(bv.x << 16); s[1] += __uint_as_float(bv.x & 0xffff0000u);
+      s[2] += __uint_as_float(bv.y << 16); s[3] += __uint_as_float(bv.y & 0xffff0000u);
+    }
+    if (resid) {  // reference semantics: residual + bf16(linear output), rounded again to bf16
+      const uint2 rv = *reinterpret_cast<const uint2*>(resid + row * ldr + col);
+      s[0] = bf2f(f2bf(s[0])) + __uint_as_float(rv.x << 16);
+      s[1] = bf2f(f2bf(s[1])) + __uint_as_float(rv.x & 0xffff0000u);
+      s[2] = bf2f(f2bf(s[2])) + __uint_as_float(rv.y << 16);
+      s[3] = bf2f(f2bf(s[3])) + __uint_as_float(rv.y & 0xffff0000u);
+    }
+  }
   if (out_mode == OUT_BF16) {
     uint2 w;
     w.x = pack_bf16x2(s[0], s[1]);
@@ -1119,7 +1176,9 @@ int pick_geo(int M, int N, int splits, int req) {
 int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, int b_kmajor, void* C, long ldc, int M,
               int N, int K, const void* bias, const void* resid, long ldr, int out_mode, int act, int splits,
               void* workspace, float alpha, int geo_req, int ring_grid, void* stream, float* rsum_out = nullptr,
-              int rsum_acc = 0, bool* rsum_done = nullptr);
+              int rsum_acc = 0, bool* rsum_done = nullptr, const void* A2 = nullptr, long lda2 = 0,
+              const void* B2 = nullptr, long ldb2 = 0, int K2 = 0, const void* const* B2g = nullptr, int G = 0,
+              int g_n = 0);
 
 }  // namespace
 
@@ -1129,6 +1188,40 @@ extern "C" int vpt_gemm_bf16(const void* A, long lda, int a_kmajor, const void* 
                              int splits, void* workspace, float alpha, void* stream) {
   return gemm_impl(A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, M, N, K, bias, resid, ldr, out_mode, act, splits,
                    workspace, alpha, 0, 0, stream);
+}
+
+// C[M,N] = A . B (as vpt_gemm_bf16, one split) + A2 . B2 over K2 more reduction elements in the same f32
+// accumulator: the LoRA term of LoRALinear (src/modules/peft/lora.py:92-104) as a K-extension of the base
+// GEMM (forward: A2 = s * x . down^T [M][r], B2 = up [N][r]; input gradient: A2 = s * dy . up [M][r], B2 = down
+// [r][K_in], the layout of B). A and A2 k-major; K % 64 == 0; K2 % 8 == 0, 0 < K2 <= 256. splits > 1: split-K
+// (the extension rides the last slice; bias / residual applied by the slab reduce; vpt_gemm_workspace_bytes).
+extern "C" int vpt_gemm_bf16_lora(const void* A, long lda, const void* B, long ldb, int b_kmajor, const void* A2,
+                                  long lda2, const void* B2, long ldb2, int K2, void* C, long ldc, int M, int N, int K,
+                                  const void* bias, const void* resid, long ldr, int out_mode, int splits,
+                                  void* workspace, int geometry, void* stream) {
+  VPT_CHECK_ARG(A2 && B2, "vpt_gemm_bf16_lora: null LoRA operand");
+  VPT_CHECK_ARG(K % 64 == 0 && K2 > 0 && K2 <= 256 && K2 % 8 == 0, "vpt_gemm_bf16_lora: K % 64 == 0, K2 in 8..256, K2 % 8 == 0");
+  VPT_CHECK_ARG(lda2 % 8 == 0 && ldb2 % 8 == 0 && lda2 >= K2 && (b_kmajor ? ldb2 >= K2 : ldb2 >= N),
+                "vpt_gemm_bf16_lora: LoRA leading dims (16-B multiples, >= K2 / N)");
+  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256, "vpt_gemm_bf16_lora: geometry 0, 128 or 256");
+  return gemm_impl(A, lda, 1, B, ldb, b_kmajor, C, ldc, M, N, K, bias, resid, ldr, out_mode, ACT_NONE, splits, workspace,
+                   1.f, geometry, 0, stream, nullptr, 0, nullptr, A2, lda2, B2, ldb2, K2);
+}
+
+// G LoRA targets that read the same input, computed as ONE GEMM (the base weights stacked [G * g_n][K]): outputs
+// C[:, g * g_n : (g + 1) * g_n] = A . W_g^T + A2[:, g * r : (g + 1) * r] . up_g^T (up_g = B2s[g], [g_n][r]).
+extern "C" int vpt_gemm_bf16_lora_grouped(const void* A, long lda, const void* B, long ldb, const void* A2, long lda2,
+                                          const void* const* B2s, int G, int r, void* C, long ldc, int M, int g_n,
+                                          int K, const void* bias, const void* resid, long ldr, int splits,
+                                          void* workspace, int geometry, void* stream) {
+  VPT_CHECK_ARG(A2 && B2s && G > 0 && G <= 4, "vpt_gemm_bf16_lora_grouped: 1..4 groups");
+  for (int i = 0; i < G; ++i) VPT_CHECK_ARG(B2s[i], "vpt_gemm_bf16_lora_grouped: null up");
+  VPT_CHECK_ARG(K % 64 == 0 && r > 0 && r <= 64 && r % 8 == 0 && g_n % 128 == 0,
+                "vpt_gemm_bf16_lora_grouped: K % 64 == 0, r in 8..64 (r % 8 == 0), g_n % 128 == 0");
+  VPT_CHECK_ARG(lda2 % 8 == 0 && lda2 >= G * r, "vpt_gemm_bf16_lora_grouped: lda2 >= G * r (16-B multiple)");
+  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256, "vpt_gemm_bf16_lora_grouped: geometry 0, 128, 256");
+  return gemm_impl(A, lda, 1, B, ldb, 1, C, ldc, M, G * g_n, K, bias, resid, ldr, OUT_BF16, ACT_NONE, splits, workspace,
+                   1.f, geometry, 0, stream, nullptr, 0, nullptr, A2, lda2, B2s[0], r, r, B2s, G, g_n);
 }
 
 extern "C" int vpt_gemm_bf16_tiled(const void* A, long lda, int a_kmajor, const void* B, long ldb, int b_kmajor,
@@ -1147,7 +1240,8 @@ namespace {
 int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, int b_kmajor, void* C, long ldc, int M,
               int N, int K, const void* bias, const void* resid, long ldr, int out_mode, int act, int splits,
               void* workspace, float alpha, int geo_req, int ring_grid, void* stream, float* rsum_out, int rsum_acc,
-              bool* rsum_done) {
+              bool* rsum_done, const void* A2, long lda2, const void* B2, long ldb2, int K2,
+              const void* const* B2g, int G, int g_n) {
   VPT_CHECK_ARG(A && B && C, "vpt_gemm_bf16: null operand");
   VPT_CHECK_ARG(M > 0 && N > 0 && K > 0, "vpt_gemm_bf16: empty shape");
   VPT_CHECK_ARG(N % 4 == 0, "vpt_gemm_bf16: N%4 required");
@@ -1167,6 +1261,13 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
   g.act = act;
   g.alpha = alpha;
   g.ring_grid = ring_grid;
+  g.A2 = (const bf16_t*)A2; g.lda2 = lda2;
+  g.B2 = (const bf16_t*)B2; g.ldb2 = ldb2;
+  g.K2 = A2 ? K2 : 0;
+  if (B2g && G > 0) {
+    for (int i = 0; i < G; ++i) g.B2g[i] = (const bf16_t*)B2g[i];
+    g.g_n = g_n;
+  }
 #ifdef VPT_DIAG
   g.dbg = g_dbg;
   if (g_ring_grid_override) g.ring_grid = g_ring_grid_override;
@@ -1175,8 +1276,12 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
   int final_mode = out_mode;
   if (splits > 1) {
     VPT_CHECK_ARG(workspace != nullptr, "vpt_gemm_bf16: split-K needs a workspace");
-    VPT_CHECK_ARG(!bias && !resid && act == ACT_NONE && alpha == 1.f, "vpt_gemm_bf16: split-K has no fused epilogue");
+    VPT_CHECK_ARG(act == ACT_NONE && alpha == 1.f && (out_mode == OUT_BF16 || (!bias && !resid)),
+                  "vpt_gemm_bf16: split-K epilogue: bias / residual with bf16 output only, no SiLU / alpha");
     VPT_CHECK_ARG(ldc == N, "vpt_gemm_bf16: split-K needs dense C");
+    VPT_CHECK_ARG(N % 4 == 0 && (!resid || ldr % 4 == 0), "vpt_gemm_bf16: split-K epilogue needs N % 4 == 0");
+    g.bias = nullptr;  // applied by the slab reduce
+    g.resid = nullptr;
     int per = (K + splits - 1) / splits;
     per = (per + BK - 1) / BK * BK;
     splits = (K + per - 1) / per;
@@ -1192,7 +1297,8 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
     g.split_stride = 0;
     g.out_mode = out_mode;
   }
-  const int geo = pick_geo(M, N, splits, geo_req);
+  int geo = pick_geo(M, N, splits, geo_req);
+  if (g.g_n > 0 && g.g_n % 256 != 0) geo = 128;  // grouped extension: a 256-wide tile would straddle two groups
   const bool rs = rsum_out && !a_kmajor && geo == 256 && N % 8 == 0 && workspace != nullptr;
   if (rsum_done) *rsum_done = rs;
   float* rpart = nullptr;
@@ -1211,7 +1317,8 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
   const long cblocks = (n / 4 + threads - 1) / threads;
   const long rblocks = rs ? (M + threads - 1) / threads : 0;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(cblocks + rblocks), dim3(threads), 0, s, (const float*)workspace, n,
-                     splits, (long)M * N, C, final_mode, cblocks, rpart, splits, M, rsum_out, rsum_acc);
+                     splits, (long)M * N, C, final_mode, cblocks, rpart, splits, M, rsum_out, rsum_acc,
+                     splits > 1 ? (const bf16_t*)bias : nullptr, splits > 1 ? (const bf16_t*)resid : nullptr, ldr, N);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
@@ -1427,7 +1534,11 @@ __device__ __forceinline__ Nf4Regs nf4_load(const GemmArgs& g, const Nf4Args& f,
 template <bool BKMAJ>
 __device__ __forceinline__ void nf4_store(char* lb, const Nf4Regs& r, const float* lut, const float* code2, float off,
                                           int tid) {
-  const float am = code2[r.q] * r.a2 + off;
+  float am;
+  {
+#pragma clang fp contract(off)  // bnb: dequantize_blockwise (a product), then absmax += offset (a sum)
+    am = code2[r.q] * r.a2 + off;
+  }
   const uint32_t w[4] = {r.codes.x, r.codes.y, r.codes.z, r.codes.w};
   const float2_t* lut2 = reinterpret_cast<const float2_t*>(lut);  // [256] (NF4[b >> 4], NF4[b & 15])
 #pragma unroll

@@ -143,6 +143,20 @@ __global__ void scale_bf16_kernel(const bf16_t* __restrict__ a, long n8, float s
   reinterpret_cast<uint4*>(out)[i] = pack8(fa);
 }
 
+// The same on a [rows][cols] block of a row-strided matrix (in place allowed): the attention query pre-scale of
+// a q that is one column block of a fused q | k | v projection.
+__global__ void scale_bf16_2d_kernel(const bf16_t* __restrict__ a, long lda, long rows, int cols8, float s,
+                                     bf16_t* __restrict__ out, long ldo) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * cols8) return;
+  const long r = i / cols8, c = (i - r * cols8) * 8;
+  float fa[8];
+  unpack8(*reinterpret_cast<const uint4*>(a + r * lda + c), fa);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) fa[e] *= s;
+  *reinterpret_cast<uint4*>(out + r * ldo + c) = pack8(fa);
+}
+
 // Flow-matching MSE over patch-layout predictions; also writes d(loss)/d(pred) (bf16, patch layout).
 // target 0 ("image"): mse(pred, x); target 1 ("velocity"): mse((pred-z)/c, (x-z)/c), c = clamp(1-t, eps).
 __global__ __launch_bounds__(256) void loss_kernel(const bf16_t* __restrict__ pred, const unsigned short* __restrict__ img,
@@ -585,6 +599,17 @@ extern "C" int vpt_scale_bf16(const void* a, long n, float s, void* out, void* s
   VPT_CHECK_ARG(a && out && n % 8 == 0, "vpt_scale_bf16: n must be a multiple of 8");
   hipLaunchKernelGGL(scale_bf16_kernel, grid1(n / 8), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)a, n / 8, s,
                      (bf16_t*)out);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_scale_bf16_2d(const void* a, long lda, long rows, int cols, float s, void* out, long ldo,
+                                 void* stream) {
+  VPT_CHECK_ARG(a && out && rows > 0 && cols > 0 && cols % 8 == 0 && lda % 8 == 0 && ldo % 8 == 0,
+                "vpt_scale_bf16_2d: cols and leading dims must be multiples of 8");
+  const long n8 = rows * (cols / 8);
+  hipLaunchKernelGGL(scale_bf16_2d_kernel, grid1(n8), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)a, lda, rows,
+                     cols / 8, s, (bf16_t*)out, ldo);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

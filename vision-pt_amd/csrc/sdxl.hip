@@ -5,6 +5,7 @@
 //                            nested absmax (8-bit blockwise over the signed dynamic map, blocksize 256, + offset)
 // Row kernels: one wave per row, 16-B (8 x bf16) vector accesses, up to 4 chunks per lane (D <= 2048).
 #include "common.h"
+#include "../../include/vpt_hip.h"  // C-ABI types (VptNf4Job)
 
 namespace {
 
@@ -193,18 +194,69 @@ __constant__ float kNF4[16] = {-1.0f, -0.6961928009986877f, -0.5250730514526367f
                                0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
                                0.7229568362236023f, 1.0f};
 
-// W[i] = NF4[code_i] * absmax[i / 64], absmax[j] = code2[qabsmax[j]] * absmax2[j / 256] + offset; one
-// thread per packed byte (two weights, the first in the high nibble); bf16 output in the original
-// [out][in] layout, ready as the k-major B operand of the GEMM.
-__global__ void nf4_dequant_kernel(const uint8_t* __restrict__ packed, const uint8_t* __restrict__ qabsmax,
-                                   const float* __restrict__ absmax2, const float* __restrict__ code2,
-                                   const float* __restrict__ offset, long nbytes, bf16_t* __restrict__ out) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nbytes) return;
-  const long blk = (2 * i) / 64;
-  const float am = code2[qabsmax[blk]] * absmax2[blk / 256] + offset[0];
-  const uint8_t p = packed[i];
-  reinterpret_cast<uint32_t*>(out)[i] = pack_bf16x2(kNF4[p >> 4] * am, kNF4[p & 15] * am);
+// W[i] = NF4[code_i] * absmax[i / 64], absmax[j] = code2[qabsmax[j]] * absmax2[j / 256] + offset (bnb's
+// dequantize_blockwise of the nested absmax, then `absmax += offset`: a product and a sum, each rounded -- no
+// FMA); bf16 output in the original [out][in] layout, ready as the B operand of the GEMM. One thread per 16
+// packed bytes (32 weights, half a block: one absmax), byte -> (NF4[hi], NF4[lo]) from a 256-entry LDS table,
+// 16-B loads and stores. HBM-bound: 0.5 B in + 2 B out per weight.
+__device__ __forceinline__ float nf4_absmax(float c2, float a2, float off) {
+#pragma clang fp contract(off)
+  return c2 * a2 + off;
+}
+
+// 16 packed bytes (32 weights, one absmax) -> 4 x 16-B bf16 stores
+__device__ __forceinline__ void nf4_dequant_chunk(const uint8_t* __restrict__ packed, const uint8_t* __restrict__ qabsmax,
+                                                  const float* __restrict__ absmax2, const float* __restrict__ code2,
+                                                  float off, long i, const float2_t* lut, bf16_t* __restrict__ out) {
+  const long blk = i >> 1;
+  const float am = nf4_absmax(code2[qabsmax[blk]], absmax2[blk >> 8], off);
+  const uint4 c = *reinterpret_cast<const uint4*>(packed + i * 16);
+  const uint32_t w[4] = {c.x, c.y, c.z, c.w};
+  uint4* dst = reinterpret_cast<uint4*>(out + i * 32);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float2_t pr = lut[(w[q] >> (8 * j)) & 0xffu];  // first weight in the high nibble
+      v[2 * j] = pr[0] * am;
+      v[2 * j + 1] = pr[1] * am;
+    }
+    dst[q] = pack8(v);
+  }
+}
+
+struct Nf4Batch {
+  VptNf4Job job[16];
+  long block0[17];  // first block of each job (prefix over ceil(chunks / 256))
+  int njobs;
+};
+
+__global__ __launch_bounds__(256) void nf4_dequant_batch_kernel(Nf4Batch b) {
+  __shared__ float2_t lut[256];
+  lut[threadIdx.x] = float2_t{kNF4[threadIdx.x >> 4], kNF4[threadIdx.x & 15]};
+  __syncthreads();
+  int j = 0;
+  while (j + 1 < b.njobs && (long)blockIdx.x >= b.block0[j + 1]) ++j;  // wave-uniform
+  const VptNf4Job& jb = b.job[j];
+  const long i = ((long)blockIdx.x - b.block0[j]) * blockDim.x + threadIdx.x;
+  if (i >= jb.n / 32) return;
+  nf4_dequant_chunk((const uint8_t*)jb.packed, (const uint8_t*)jb.qabsmax, jb.absmax2, jb.code2, jb.offset[0], i, lut,
+                    (bf16_t*)jb.out);
+}
+
+__global__ __launch_bounds__(256) void nf4_dequant_kernel(const uint8_t* __restrict__ packed,
+                                                          const uint8_t* __restrict__ qabsmax,
+                                                          const float* __restrict__ absmax2,
+                                                          const float* __restrict__ code2,
+                                                          const float* __restrict__ offset, long nchunks,
+                                                          bf16_t* __restrict__ out) {
+  __shared__ float2_t lut[256];
+  lut[threadIdx.x] = float2_t{kNF4[threadIdx.x >> 4], kNF4[threadIdx.x & 15]};
+  __syncthreads();
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // chunk of 16 packed bytes
+  if (i >= nchunks) return;
+  nf4_dequant_chunk(packed, qabsmax, absmax2, code2, offset[0], i, lut, out);
 }
 
 // Pass 1 of quantize_4bit: per 64-block absmax (one wave per block), nearest NF4 code of w / absmax
@@ -461,8 +513,28 @@ extern "C" int vpt_nf4_dequant(const void* packed, const void* qabsmax, const fl
                                const float* offset, long n, void* out, void* stream) {
   VPT_CHECK_ARG(packed && qabsmax && absmax2 && code2 && offset && out && n % 64 == 0 && n > 0,
                 "vpt_nf4_dequant: n must be a positive multiple of 64");
-  hipLaunchKernelGGL(nf4_dequant_kernel, grid1(n / 2), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)packed,
-                     (const uint8_t*)qabsmax, absmax2, code2, offset, n / 2, (bf16_t*)out);
+  const long chunks = n / 32;
+  hipLaunchKernelGGL(nf4_dequant_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const uint8_t*)packed, (const uint8_t*)qabsmax, absmax2, code2, offset, chunks, (bf16_t*)out);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_nf4_dequant_batch(const VptNf4Job* jobs, int njobs, void* stream) {
+  VPT_CHECK_ARG(jobs && njobs > 0 && njobs <= 16, "vpt_nf4_dequant_batch: 1..16 jobs");
+  Nf4Batch b = {};
+  b.njobs = njobs;
+  long blocks = 0;
+  for (int j = 0; j < njobs; ++j) {
+    const VptNf4Job& jb = jobs[j];
+    VPT_CHECK_ARG(jb.packed && jb.qabsmax && jb.absmax2 && jb.code2 && jb.offset && jb.out && jb.n > 0 && jb.n % 64 == 0,
+                  "vpt_nf4_dequant_batch: job n must be a positive multiple of 64");
+    b.job[j] = jb;
+    b.block0[j] = blocks;
+    blocks += (jb.n / 32 + 255) / 256;
+  }
+  b.block0[njobs] = blocks;
+  hipLaunchKernelGGL(nf4_dequant_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, b);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

@@ -25,6 +25,7 @@ SIGNATURES: dict[str, list] = {
     "vpt_gemm_bf16": [P, L, I, P, L, I, P, L, I, I, I, P, P, L, I, I, I, P, F, P],
     "vpt_gemm_workspace_bytes": [I, I, I, I],
     "vpt_gemm_bf16_tiled": [P, L, I, P, L, I, P, L, I, I, I, P, P, L, I, I, I, P, F, I, I, P],
+    "vpt_gemm_bf16_lora": [P, L, P, L, I, P, L, P, L, I, P, L, I, I, I, P, P, L, I, I, P, I, P],
     "vpt_linear_wgrad": [P, L, P, L, P, L, P, L, I, I, I, I, P, I, I, P],
     "vpt_linear_wgrad_workspace_bytes": [L, I, I, I],
     "vpt_gemm_swiglu_fwd": [P, L, P, L, P, P, L, P, L, I, I, I, P],
@@ -71,6 +72,9 @@ SIGNATURES: dict[str, list] = {
     "vpt_geglu_fwd": [P, L, I, L, P, P],
     "vpt_geglu_bwd": [P, P, L, I, L, P, L, P],
     "vpt_nf4_dequant": [P, P, P, P, P, L, P, P],
+    "vpt_nf4_dequant_batch": [P, I, P],
+    "vpt_scale_bf16_2d": [P, L, L, I, F, P, L, P],
+    "vpt_gemm_bf16_lora_grouped": [P, L, P, L, P, L, P, I, I, P, L, I, I, I, P, P, L, I, P, I, P],
     "vpt_groupnorm_fwd": [P, P, P, P, P, P, I, I, I, L, F, P],
     "vpt_groupnorm_bwd": [P, P, P, P, P, P, P, I, I, I, L, P],
     "vpt_transpose_add": [P, P, P, I, I, I, P],

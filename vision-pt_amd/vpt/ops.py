@@ -130,6 +130,91 @@ def gemm(a, a_kmajor: bool, b, b_kmajor: bool, M: int, N: int, K: int, out, *, b
     return out
 
 
+_WS: dict = {}  # (device, tag) -> f32 workspace grown on demand (stream-ordered reuse on one stream)
+
+
+def workspace(dev, tag: str, nfloats: int) -> torch.Tensor:
+    buf = _WS.get((str(dev), tag))
+    if buf is None or buf.numel() < nfloats:
+        buf = _WS[(str(dev), tag)] = torch.empty(nfloats, dtype=F32, device=dev)
+    return buf
+
+
+def lora_gemm_plan(M: int, N: int, K: int) -> tuple[int, int]:
+    """(geometry, splits) for a base+LoRA GEMM: the 256 x 256 ring when its tiles fill the chip (>= 160), a
+    K-split ring for small grids over a long reduction (K >= 4096: ~240 work items), otherwise 128 x 128 tiles
+    (2 blocks per CU). Measured at the config-5 shapes (tools/c5_gemm_shapes.py, profiles/r03/)."""
+    t256 = ((M + 255) // 256) * ((N + 255) // 256)
+    if t256 >= 160:
+        return 256, 1
+    if K >= 4096:
+        sp = max(2, min(4, round(240 / t256), K // 1024))
+        return 256, sp
+    return 128, 1
+
+
+def gemm_lora(a, b, b_kmajor: bool, a2, b2, M: int, N: int, K: int, out, *, bias=None, resid=None, geometry=None,
+              splits=None):
+    """out[M,N] = A . B (+bias) (+resid) + a2 . B2 with one rounding (vpt_gemm_bf16_lora): the base GEMM of a
+    LoRALinear with its adapter term as a K-extension. Forward: a = x [M,K], b = W [N,K] (b_kmajor), a2 = ds [M,r],
+    b2 = up [N,r]; input gradient: a = dy [M,N_out] (K = N_out), b = W [N_out, K_in] (not b_kmajor, N = K_in),
+    a2 = vs [M,r], b2 = down [r, K_in]."""
+    for t, n in ((a, "a"), (b, "b"), (a2, "a2"), (b2, "b2")):
+        _chk(t, BF16, n)
+    _chk(out, BF16, "out")
+    if bias is not None:
+        _chk(bias, BF16, "bias")
+    if resid is not None:
+        _chk(resid, BF16, "resid")
+    K2 = a2.shape[1]
+    geo, sp = lora_gemm_plan(M, N, K)
+    geometry = geo if geometry is None else geometry
+    splits = sp if splits is None else splits
+    ws = workspace(out.device, "gemm_lora", splits * M * N) if splits > 1 else None
+
+    def run():
+        call("vpt_gemm_bf16_lora", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), int(b_kmajor), a2.data_ptr(),
+             a2.stride(0), b2.data_ptr(), b2.stride(0), K2, out.data_ptr(), out.stride(0), M, N, K, _p(bias), _p(resid),
+             0 if resid is None else resid.stride(0), OUT_BF16, int(splits), _p(ws), int(geometry), stream())
+    pr = PROBES.get("gemm_lora")
+    if pr is None:
+        run()
+    else:
+        pr.record(2.0 * M * N * (K + K2), run, key=f"{'fwd' if b_kmajor else 'dgrad'} M{M} N{N} K{K}")
+    return out
+
+
+def gemm_lora_grouped(x, w_stacked, a2, ups, out, *, bias=None, resid=None, geometry=None, splits=None):
+    """G LoRA targets reading x as one GEMM (vpt_gemm_bf16_lora_grouped): out[:, g*n:(g+1)*n] = x . W_g^T +
+    a2[:, g*r:(g+1)*r] . ups[g]^T, W_g = w_stacked[g*n:(g+1)*n] (the dequantised bases side by side)."""
+    for t, n in ((x, "x"), (w_stacked, "w_stacked"), (a2, "a2"), (out, "out")):
+        _chk(t, BF16, n)
+    G = len(ups)
+    for u in ups:
+        _chk(u, BF16, "up")
+        if not u.is_contiguous():
+            raise ValueError("ups must be contiguous [n, r]")
+    M, K = x.shape
+    gn, r = ups[0].shape
+    geo, sp = lora_gemm_plan(M, G * gn, K)
+    geometry = geo if geometry is None else geometry
+    splits = sp if splits is None else splits
+    ws = workspace(out.device, "gemm_lora", splits * M * G * gn) if splits > 1 else None
+    ptrs = (ctypes.c_void_p * G)(*[u.data_ptr() for u in ups])
+
+    def run():
+        call("vpt_gemm_bf16_lora_grouped", x.data_ptr(), x.stride(0), w_stacked.data_ptr(), w_stacked.stride(0),
+             a2.data_ptr(), a2.stride(0), ctypes.cast(ptrs, ctypes.c_void_p), G, r, out.data_ptr(), out.stride(0), M, gn,
+             K, _p(bias), _p(resid), 0 if resid is None else resid.stride(0), int(splits), _p(ws), int(geometry),
+             stream())
+    pr = PROBES.get("gemm_lora")
+    if pr is None:
+        run()
+    else:
+        pr.record(2.0 * M * G * gn * (K + r), run, key=f"fwd{G} M{M} N{G * gn} K{K}")
+    return out
+
+
 def linear(x, w, bias=None, resid=None, out=None, act=ACT_NONE, **tile):
     """y = x @ w.T (+bias) (+resid) in bf16 — nn.Linear forward."""
     M, K = x.shape
@@ -641,6 +726,14 @@ def add_bf16(a, b, out=None):
     return out
 
 
+def scale_bf16_2d(a, s, out=None):
+    """s * a on a row-strided 2-D view (in place when out is a)."""
+    out = torch.empty_like(a) if out is None else out
+    call("vpt_scale_bf16_2d", a.data_ptr(), a.stride(0), a.shape[0], a.shape[1], float(s), out.data_ptr(), out.stride(0),
+         stream())
+    return out
+
+
 def scale_bf16(a, s, out=None):
     out = torch.empty_like(a) if out is None else out
     call("vpt_scale_bf16", a.data_ptr(), a.numel(), float(s), out.data_ptr(), stream())
@@ -648,9 +741,29 @@ def scale_bf16(a, s, out=None):
 
 
 def nf4_dequant(packed, qabsmax, absmax2, code2, offset, n, out):
-    call("vpt_nf4_dequant", packed.data_ptr(), qabsmax.data_ptr(), absmax2.data_ptr(), code2.data_ptr(),
-         offset.data_ptr(), n, out.data_ptr(), stream())
+    def run():
+        call("vpt_nf4_dequant", packed.data_ptr(), qabsmax.data_ptr(), absmax2.data_ptr(), code2.data_ptr(),
+             offset.data_ptr(), n, out.data_ptr(), stream())
+    _launch("nf4_dequant", 2.5 * n, run)  # algorithmic HBM bytes: 0.5 B of codes in, 2 B of bf16 out per weight
     return out
+
+
+class _Nf4Job(ctypes.Structure):
+    """VptNf4Job (include/vpt_hip.h)."""
+    _fields_ = [("packed", ctypes.c_void_p), ("qabsmax", ctypes.c_void_p), ("absmax2", ctypes.c_void_p),
+                ("code2", ctypes.c_void_p), ("offset", ctypes.c_void_p), ("out", ctypes.c_void_p), ("n", ctypes.c_long)]
+
+
+def nf4_dequant_batch(pairs):
+    """[(NF4Weight, bf16 out)] -> one vpt_nf4_dequant_batch launch per 16 tensors."""
+    for i in range(0, len(pairs), 16):
+        chunk = pairs[i:i + 16]
+        jobs = (_Nf4Job * len(chunk))(*[_Nf4Job(w.packed.data_ptr(), w.qabsmax.data_ptr(), w.absmax2.data_ptr(),
+                                                 w.code2.data_ptr(), w.offset.data_ptr(), out.data_ptr(), w.numel)
+                                         for w, out in chunk])
+        _launch("nf4_dequant", 2.5 * sum(w.numel for w, _ in chunk),
+                lambda: call("vpt_nf4_dequant_batch", ctypes.cast(jobs, ctypes.c_void_p), len(chunk), stream()))
+    return [out for _, out in pairs]
 
 
 def gemm_nf4(a, w, forward: bool, out, *, lora_a=None, lora_b=None, bias=None, resid=None, out_mode=OUT_BF16,

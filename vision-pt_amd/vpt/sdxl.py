@@ -2,8 +2,9 @@
 
 a29  LoRALinearNF4: LoRALinear (src/modules/peft/lora.py:92-104) over a bitsandbytes NF4 Linear4bit
      (src/modules/quant/bnb.py:37-129): y = bf16(bf16(x W^T + b) + bf16(s * up(down(x)))), s = alpha/rank,
-     with W dequantised tile by tile inside the GEMM (`vpt_gemm_nf4`, no bf16 weight in HBM) and the LoRA
-     term fused into the same GEMM as an extra K tile. Base weight frozen; the adapters train (f32 grads).
+     the LoRA term fused into the base GEMM as a K-extension (one f32 accumulator), the NF4 base entering it
+     as BASE_MODES below says (default: dequantised per call as bitsandbytes' MatMul4Bit does). Base weight
+     frozen; the adapters train (f32 grads).
 a30  SDXLTransformerBlock: TransformerBlock.forward (src/models/sdxl/denoiser.py:258-280) --
      LayerNorm -> self-attention -> LayerNorm -> cross-attention to the text context -> LayerNorm ->
      GeGLU feed-forward, residuals -- with its 10 Linear layers as LoRALinearNF4 (the QLoRA targets),
@@ -12,6 +13,8 @@ a30  SDXLTransformerBlock: TransformerBlock.forward (src/models/sdxl/denoiser.py
 """
 
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -52,6 +55,8 @@ class NF4Weight:
 
     def __init__(self, packed, qabsmax, absmax2, code2, offset, shape):
         self.packed, self.qabsmax, self.absmax2, self.code2, self.offset = packed, qabsmax, absmax2, code2, offset
+        self.resident = None  # bf16 base of the "resident" mode (built on first use)
+        self.resident_qkv = None  # "resident" mode, attn1.to_q only: the stacked q|k|v bases
         self.shape = tuple(int(s) for s in shape)
         self.numel = 1
         for s in self.shape:
@@ -86,20 +91,86 @@ class NF4Weight:
                                out.view(self.shape))
 
 
+# How the frozen NF4 base enters the GEMM (BASELINE config 5):
+#   "dequant"  (default) bitsandbytes' MatMul4Bit semantics (bnb 0.48.2 matmul_4bit for a multi-row input:
+#              dequantize_4bit(W) to a bf16 weight, then F.linear; its backward dequantises again): each forward and
+#              each input-gradient call dequantises W (vpt_nf4_dequant, 16-B vectorised, HBM-bound) into one
+#              per-device scratch and runs the bf16 ring / T128 GEMM with the LoRA term as a K-extension
+#              (vpt_gemm_bf16_lora). Only the NF4 state stays resident.
+#   "resident" the dequantised bf16 base kept in HBM next to its NF4 state (frozen, so it is computed once; 4.4 GB
+#              for the SDXL UNet's transformer Linears -- room the 288 GB of an MI355X has), same GEMMs.
+#   "inline"   NF4 dequantised tile by tile inside the GEMM (vpt_gemm_nf4: no bf16 weight in HBM at all; the
+#              memory-lean variant, ~1.5x slower on the config-5 shapes).
+# All three give the same dequantised values; "dequant" and "resident" give bitwise identical outputs.
+BASE_MODES = ("dequant", "resident", "inline")
+DEFAULT_BASE_MODE = os.environ.get("VPT_NF4_BASE", "dequant")
+_SCRATCH: dict = {}  # (device, "call" | "block") -> bf16 dequant scratch, grown on demand
+
+
+def _dequant_scratch(base: "NF4Weight", device) -> torch.Tensor:
+    buf = _SCRATCH.get((str(device), "call"))
+    if buf is None or buf.numel() < base.numel:
+        buf = _SCRATCH[(str(device), "call")] = torch.empty(base.numel, dtype=BF16, device=device)
+    return base.dequantize(buf[:base.numel].view(base.shape))
+
+
+def dequant_bases(lins: dict, targets, device) -> dict:
+    """{target: bf16 base} for a block's LoRA targets about to run: "dequant" mode dequantises all of them in ONE
+    launch (vpt_nf4_dequant_batch) into a shared per-device scratch (stream-ordered reuse, block after block);
+    "resident" returns the kept bf16 bases; "inline" (or a non-fused target) returns nothing (the GEMM dequantises)."""
+    ts = [t for t in targets if lins[t].fused and lins[t].base_mode != "inline"]
+    if not ts:
+        return {}
+    if lins[ts[0]].base_mode == "resident":
+        out = {t: base_weight(lins[t].base, "resident", device) for t in ts}
+        if ts[:3] == QKV:
+            q = lins[QKV[0]].base
+            if q.resident_qkv is None:  # the stacked copy of the fused q|k|v GEMMs, kept with the q base
+                q.resident_qkv = torch.cat([out[t] for t in QKV], 0)
+            out["attn1.qkv"] = q.resident_qkv
+        return out
+    total = sum(lins[t].base.numel for t in ts)
+    buf = _SCRATCH.get((str(device), "block"))
+    if buf is None or buf.numel() < total:
+        buf = _SCRATCH[(str(device), "block")] = torch.empty(total, dtype=BF16, device=device)
+    out, off = {}, 0
+    for t in ts:
+        b = lins[t].base
+        out[t] = buf[off:off + b.numel].view(b.shape)
+        off += b.numel
+    ops.nf4_dequant_batch([(lins[t].base, out[t]) for t in ts])
+    if ts[:3] == QKV:  # the three self-attention bases are side by side: the stacked [3 dim, dim] operand
+        n = lins[QKV[0]].base.numel
+        out["attn1.qkv"] = buf[:3 * n].view(3 * lins[QKV[0]].base.shape[0], lins[QKV[0]].base.shape[1])
+    return out
+
+
+def base_weight(base: "NF4Weight", mode: str, device) -> torch.Tensor:
+    """The bf16 base weight a "dequant" / "resident" GEMM reads (stream-ordered scratch reuse for "dequant")."""
+    if mode == "resident":
+        if base.resident is None:
+            base.resident = base.dequantize()
+        return base.resident
+    return _dequant_scratch(base, device)
+
+
 class LoRALinearNF4:
     """a29. `down` [r, in], `up` [out, r] bf16 trainable (grads `g_down`, `g_up` f32); `base` NF4 [out, in].
 
     forward  ds = bf16(s * x . down^T)            (one skinny GEMM, s = alpha / rank folded into its epilogue)
-             y  = bf16(x . Wd^T + b + ds . up^T)  (vpt_gemm_nf4: NF4 dequantised per tile in LDS, LoRA term as
-                                                   one extra K tile -- no bf16 weight in HBM, no LoRA add pass)
+             y  = bf16(x . Wd^T + b + ds . up^T)  (vpt_gemm_bf16_lora on the dequantised base, or vpt_gemm_nf4
+                                                   in "inline" mode: LoRA term as K-extension, no LoRA add pass)
     backward g_up += dy^T . ds;  vs = bf16(s * dy . up);  g_down += vs^T . x;
-             dx = bf16(dy . Wd + vs . down)       (vpt_gemm_nf4 in the input-gradient direction)
+             dx = bf16(dy . Wd + vs . down)       (the same two GEMMs in the input-gradient direction)
     The reference (lora.py:92-104) rounds lora_down, lora_up and their scaled sum to bf16 separately; here the
     sum is taken in f32 before one rounding (within the bf16 parity tolerance of tests/test_sdxl_gpu.py)."""
 
     def __init__(self, base: NF4Weight, bias: torch.Tensor | None, down: torch.Tensor, up: torch.Tensor,
-                 alpha: float, rank: int):
+                 alpha: float, rank: int, base_mode: str | None = None):
         self.base, self.bias = base, bias
+        self.base_mode = base_mode or DEFAULT_BASE_MODE
+        if self.base_mode not in BASE_MODES:
+            raise ValueError(f"base_mode must be one of {BASE_MODES}")
         self.down, self.up = down.to(BF16).contiguous(), up.to(BF16).contiguous()
         self.scale = alpha / rank
         self.g_down = torch.zeros(self.down.shape, dtype=F32, device=self.down.device)
@@ -117,8 +188,9 @@ class LoRALinearNF4:
         return self.base.dequantize(torch.empty(self.base.shape, dtype=BF16, device=self.down.device))
 
     def forward(self, x: torch.Tensor, save: bool = True, out: torch.Tensor | None = None,
-                resid: torch.Tensor | None = None) -> torch.Tensor:
-        """resid: a bf16 tensor added in the epilogue (the block's residual stream: bf16(resid + bf16(y)))."""
+                resid: torch.Tensor | None = None, W: torch.Tensor | None = None) -> torch.Tensor:
+        """resid: a bf16 tensor added in the epilogue (the block's residual stream: bf16(resid + bf16(y))).
+        W: the base already dequantised by the caller (dequant_bases), else this call dequantises it."""
         M = x.shape[0]
         r = self.down.shape[0]
         ds = torch.empty(M, r, dtype=BF16, device=x.device)
@@ -127,7 +199,10 @@ class LoRALinearNF4:
         else:
             ops.gemm(x, True, self.down, True, M, r, x.shape[1], ds, alpha=self.scale)
         y = out if out is not None else torch.empty(M, self.base.shape[0], dtype=BF16, device=x.device)
-        if self.fused:
+        if self.fused and self.base_mode != "inline":
+            W = base_weight(self.base, self.base_mode, x.device) if W is None else W
+            ops.gemm_lora(x, W, True, ds, self.up, M, W.shape[0], W.shape[1], y, bias=self.bias, resid=resid)
+        elif self.fused:
             ops.gemm_nf4(x, self.base, True, y, lora_a=ds, lora_b=self.up, bias=self.bias, resid=resid)
         else:
             lo = ops.gemm(ds, True, self.up, True, M, self.up.shape[0], r,
@@ -138,13 +213,30 @@ class LoRALinearNF4:
         self._saved = (x, ds) if save else None
         return y
 
-    def backward(self, dy: torch.Tensor, need_dx: bool = True) -> torch.Tensor | None:
+    def backward(self, dy: torch.Tensor, need_dx: bool = True, W: torch.Tensor | None = None) -> torch.Tensor | None:
         """Accumulates g_up, g_down; returns dx (bf16), or None with need_dx=False (an input that needs no
         gradient, e.g. the frozen text encoder's hidden states under attn2.to_k / to_v)."""
+        vs = self.backward_adapters(dy)
+        if not need_dx:
+            return None
+        x = self._saved[0]
+        M = x.shape[0]
+        dx = torch.empty(M, self.base.shape[1], dtype=BF16, device=dy.device)
+        if self.fused and self.base_mode != "inline":
+            W = base_weight(self.base, self.base_mode, dy.device) if W is None else W
+            return ops.gemm_lora(dy, W, False, vs, self.down, M, W.shape[1], W.shape[0], dx)
+        if self.fused:
+            return ops.gemm_nf4(dy, self.base, False, dx, lora_a=vs, lora_b=self.down)
+        dx_lora = ops.linear_dgrad(vs, self.down)
+        return ops.linear_dgrad(dy, self.weight(), resid=dx_lora, out=dx)
+
+    def backward_adapters(self, dy: torch.Tensor, vs_out: torch.Tensor | None = None) -> torch.Tensor:
+        """The adapter half of the backward: g_up += dy^T . ds, vs = bf16(s * dy . up), g_down += vs^T . x;
+        returns vs (into vs_out when given: a column block of a fused q|k|v gradient's LoRA operand)."""
         x, ds = self._saved
         M = x.shape[0]
         r = self.down.shape[0]
-        vs = torch.empty(M, r, dtype=BF16, device=dy.device)
+        vs = torch.empty(M, r, dtype=BF16, device=dy.device) if vs_out is None else vs_out
         if self.skinny:
             ops.lora_proj(dy, self.up, False, vs, alpha=self.scale)
             ops.lora_wgrad2(dy, ds, self.g_up, x, vs, self.g_down)
@@ -152,17 +244,12 @@ class LoRALinearNF4:
             ops.linear_wgrad(dy, ds, self.g_up, accumulate=True, splits=ops.wgrad_splits(*self.up.shape, M))
             ops.gemm(dy, True, self.up, False, M, r, self.up.shape[0], vs, alpha=self.scale)
             ops.linear_wgrad(vs, x, self.g_down, accumulate=True, splits=ops.wgrad_splits(*self.down.shape, M))
-        if not need_dx:
-            return None
-        dx = torch.empty(M, self.base.shape[1], dtype=BF16, device=dy.device)
-        if self.fused:
-            return ops.gemm_nf4(dy, self.base, False, dx, lora_a=vs, lora_b=self.down)
-        dx_lora = ops.linear_dgrad(vs, self.down)
-        return ops.linear_dgrad(dy, self.weight(), resid=dx_lora, out=dx)
+        return vs
 
 
 TARGETS = ["attn1.to_q", "attn1.to_k", "attn1.to_v", "attn1.to_out.0", "attn2.to_q", "attn2.to_k", "attn2.to_v",
            "attn2.to_out.0", "ff.net.0.proj", "ff.net.2"]
+QKV = TARGETS[:3]
 
 
 class SDXLTransformerBlock:
@@ -202,11 +289,49 @@ class SDXLTransformerBlock:
         """The attention kernels take q pre-multiplied by scale*log2(e) (include/vpt_hip.h)."""
         return ops.scale_bf16(q, ops.attn_q_scale(0.125))
 
-    def _attn_bwd(self, q, k, v, o, lse, do, B, n, nk):
+    def _fuse_qkv(self, Wb: dict) -> bool:
+        """The self-attention q / k / v projections run as one GEMM each way when their bases are stacked
+        (dequant_bases) and their adapters take the rank-16 skinny kernels."""
+        return "attn1.qkv" in Wb and all(self.lin[t].skinny for t in QKV)
+
+    def _qkv_fwd(self, h1, Wqkv, save):
+        """q|k|v = h1 . [Wq; Wk; Wv]^T + [ds_q | ds_k | ds_v] . blockdiag(up_q, up_k, up_v)^T as ONE GEMM
+        (vpt_gemm_bf16_lora_grouped; each output column block is exactly its target's LoRALinear), then q pre-scaled
+        in place for the attention kernels. Returns column views (q, k, v) of the [M, 3 dim] output."""
+        M, D, L = h1.shape[0], self.inner, self.lin
+        r = L[QKV[0]].down.shape[0]
+        ds = torch.empty(M, 3 * r, dtype=BF16, device=h1.device)
+        for g, t in enumerate(QKV):
+            dsg = ds[:, g * r:(g + 1) * r]
+            ops.lora_proj(h1, L[t].down, True, dsg, alpha=L[t].scale)
+            L[t]._saved = (h1, dsg) if save else None
+        qkv = torch.empty(M, 3 * D, dtype=BF16, device=h1.device)
+        ops.gemm_lora_grouped(h1, Wqkv, ds, [L[t].up for t in QKV], qkv)
+        q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
+        ops.scale_bf16_2d(q, ops.attn_q_scale(0.125), out=q)
+        return q, k, v
+
+    def _qkv_bwd(self, dqkv, Wqkv):
+        """dh1 = [dq | dk | dv] . [Wq; Wk; Wv] + [vs_q | vs_k | vs_v] . [down_q; down_k; down_v] as ONE GEMM (the
+        reference sums the three inputs' gradients in bf16; here one f32 sum, one rounding); the adapters'
+        gradients per target as LoRALinearNF4.backward_adapters."""
+        M, D, L = dqkv.shape[0], self.inner, self.lin
+        r = L[QKV[0]].down.shape[0]
+        vs = torch.empty(M, 3 * r, dtype=BF16, device=dqkv.device)
+        for g, t in enumerate(QKV):
+            L[t].backward_adapters(dqkv[:, g * D:(g + 1) * D], vs_out=vs[:, g * r:(g + 1) * r])
+        downs = [L[t].down for t in QKV]
+        if all(d.is_contiguous() for d in downs) and all(
+                downs[i].data_ptr() + downs[i].numel() * 2 == downs[i + 1].data_ptr() for i in range(2)):
+            stacked = torch.as_strided(downs[0], (3 * r, D), (D, 1))  # the flat layout keeps them side by side
+        else:
+            stacked = torch.cat(downs, 0)  # standalone blocks: a copy of 3 x [r, dim]
+        dh1 = torch.empty(M, D, dtype=BF16, device=dqkv.device)
+        return ops.gemm_lora(dqkv, Wqkv, False, vs, stacked, M, D, 3 * D, dh1)
+
+    def _attn_bwd(self, q, k, v, o, lse, do, B, n, nk, out=None):
         H = self.heads
-        dq = torch.empty_like(q)
-        dk = torch.empty_like(k)
-        dv = torch.empty_like(v)
+        dq, dk, dv = out if out is not None else (torch.empty_like(q), torch.empty_like(k), torch.empty_like(v))
         delta = torch.empty_like(lse)
         ops.attn_bwd(ops._t4(q, B, n, H), ops._t4(k, B, nk, H), ops._t4(v, B, nk, H), ops._t4(o, B, n, H),
                      ops._t4(do, B, n, H), lse, delta, None, ops._t4(dq, B, n, H), ops._t4(dk, B, nk, H),
@@ -216,21 +341,25 @@ class SDXLTransformerBlock:
     def forward(self, x: torch.Tensor, ctx: torch.Tensor, B: int, n: int, nc: int, save: bool = True) -> torch.Tensor:
         """x [B*n, dim] bf16, ctx [B*nc, context_dim] bf16 -> [B*n, dim] bf16 (denoiser.py:258-280)."""
         L = self.lin
+        Wb = dequant_bases(L, TARGETS, self.device)  # the block's ten bases, one launch
         h1, m1, r1 = ops.layernorm_fwd(x, *self.norm["norm1"])
-        q, k, v = (L[f"attn1.to_{c}"].forward(h1, save) for c in "qkv")
-        q = self._qs(q)
+        if self._fuse_qkv(Wb):
+            q, k, v = self._qkv_fwd(h1, Wb["attn1.qkv"], save)
+        else:
+            q, k, v = (L[f"attn1.to_{c}"].forward(h1, save, W=Wb.get(f"attn1.to_{c}")) for c in "qkv")
+            q = self._qs(q)
         o1, lse1 = self._attn_fwd(q, k, v, B, n, n)
-        x1 = L["attn1.to_out.0"].forward(o1, save, resid=x)
+        x1 = L["attn1.to_out.0"].forward(o1, save, resid=x, W=Wb.get("attn1.to_out.0"))
         h2, m2, r2 = ops.layernorm_fwd(x1, *self.norm["norm2"])
-        q2 = self._qs(L["attn2.to_q"].forward(h2, save))
-        k2 = L["attn2.to_k"].forward(ctx, save)
-        v2 = L["attn2.to_v"].forward(ctx, save)
+        q2 = self._qs(L["attn2.to_q"].forward(h2, save, W=Wb.get("attn2.to_q")))
+        k2 = L["attn2.to_k"].forward(ctx, save, W=Wb.get("attn2.to_k"))
+        v2 = L["attn2.to_v"].forward(ctx, save, W=Wb.get("attn2.to_v"))
         o2, lse2 = self._attn_fwd(q2, k2, v2, B, n, nc)
-        x2 = L["attn2.to_out.0"].forward(o2, save, resid=x1)
+        x2 = L["attn2.to_out.0"].forward(o2, save, resid=x1, W=Wb.get("attn2.to_out.0"))
         h3, m3, r3 = ops.layernorm_fwd(x2, *self.norm["norm3"])
-        x12 = L["ff.net.0.proj"].forward(h3, save)
+        x12 = L["ff.net.0.proj"].forward(h3, save, W=Wb.get("ff.net.0.proj"))
         gg = ops.geglu_fwd(x12)
-        y = L["ff.net.2"].forward(gg, save, resid=x2)
+        y = L["ff.net.2"].forward(gg, save, resid=x2, W=Wb.get("ff.net.2"))
         self._st = dict(B=B, n=n, nc=nc, x=x, x1=x1, x2=x2, m=(m1, m2, m3), r=(r1, r2, r3), q=q, k=k, v=v, o1=o1,
                         lse1=lse1, q2=q2, k2=k2, v2=v2, o2=o2, lse2=lse2, x12=x12) if save else None
         return y
@@ -248,20 +377,32 @@ class SDXLTransformerBlock:
         B, n, nc = st["B"], st["n"], st["nc"]
         m1, m2, m3 = st["m"]
         r1, r2, r3 = st["r"]
-        dgg = L["ff.net.2"].backward(dy)
+        # the bases of the input-gradient GEMMs about to run, one launch (to_k / to_v of the context only when
+        # the context needs a gradient)
+        Wb = dequant_bases(L, [t for t in TARGETS if need_dctx or t not in ("attn2.to_k", "attn2.to_v")], self.device)
+        dgg = L["ff.net.2"].backward(dy, W=Wb.get("ff.net.2"))
         dx12 = ops.geglu_bwd(dgg, st["x12"])
-        dh3 = L["ff.net.0.proj"].backward(dx12)
+        dh3 = L["ff.net.0.proj"].backward(dx12, W=Wb.get("ff.net.0.proj"))
         dx2 = ops.layernorm_bwd(dh3, st["x2"], m3, r3, self.norm["norm3"][0], dres=dy)
-        do2 = L["attn2.to_out.0"].backward(dx2)
+        do2 = L["attn2.to_out.0"].backward(dx2, W=Wb.get("attn2.to_out.0"))
         dq2, dk2, dv2 = self._attn_bwd(st["q2"], st["k2"], st["v2"], st["o2"], st["lse2"], do2, B, n, nc)
-        dh2 = L["attn2.to_q"].backward(dq2)
-        dck, dcv = L["attn2.to_k"].backward(dk2, need_dctx), L["attn2.to_v"].backward(dv2, need_dctx)
+        dh2 = L["attn2.to_q"].backward(dq2, W=Wb.get("attn2.to_q"))
+        dck = L["attn2.to_k"].backward(dk2, need_dctx, W=Wb.get("attn2.to_k"))
+        dcv = L["attn2.to_v"].backward(dv2, need_dctx, W=Wb.get("attn2.to_v"))
         dctx = ops.add_bf16(dck, dcv) if need_dctx else None
         dx1 = ops.layernorm_bwd(dh2, st["x1"], m2, r2, self.norm["norm2"][0], dres=dx2)
-        do1 = L["attn1.to_out.0"].backward(dx1)
-        dq, dk, dv = self._attn_bwd(st["q"], st["k"], st["v"], st["o1"], st["lse1"], do1, B, n, n)
-        dh1 = ops.add_bf16(ops.add_bf16(L["attn1.to_q"].backward(dq), L["attn1.to_k"].backward(dk)),
-                           L["attn1.to_v"].backward(dv))
+        do1 = L["attn1.to_out.0"].backward(dx1, W=Wb.get("attn1.to_out.0"))
+        if self._fuse_qkv(Wb):
+            dqkv = torch.empty(B * n, 3 * self.inner, dtype=BF16, device=self.device)
+            D = self.inner
+            self._attn_bwd(st["q"], st["k"], st["v"], st["o1"], st["lse1"], do1, B, n, n,
+                           out=(dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:]))
+            dh1 = self._qkv_bwd(dqkv, Wb["attn1.qkv"])
+        else:
+            dq, dk, dv = self._attn_bwd(st["q"], st["k"], st["v"], st["o1"], st["lse1"], do1, B, n, n)
+            dh1 = ops.add_bf16(ops.add_bf16(L["attn1.to_q"].backward(dq, W=Wb.get("attn1.to_q")),
+                                            L["attn1.to_k"].backward(dk, W=Wb.get("attn1.to_k"))),
+                               L["attn1.to_v"].backward(dv, W=Wb.get("attn1.to_v")))
         dx = ops.layernorm_bwd(dh1, st["x"], m1, r1, self.norm["norm1"][0], dres=dx1)
         return dx, dctx
 
@@ -276,18 +417,23 @@ class SDXLTransformerBlock:
 class NF4Linear:
     """A frozen NF4 Linear without adapters (SpatialTransformer proj_in / proj_out): vpt_gemm_nf4 both ways."""
 
-    def __init__(self, base: NF4Weight, bias: torch.Tensor | None):
+    def __init__(self, base: NF4Weight, bias: torch.Tensor | None, base_mode: str | None = None):
         self.base, self.bias = base, bias
+        self.base_mode = base_mode or DEFAULT_BASE_MODE
         if base.shape[0] % 64 or base.shape[1] % 64:
             raise NotImplementedError("NF4Linear: in / out features must be multiples of 64")
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         y = torch.empty(x.shape[0], self.base.shape[0], dtype=BF16, device=x.device)
-        return ops.gemm_nf4(x, self.base, True, y, bias=self.bias)
+        if self.base_mode == "inline":
+            return ops.gemm_nf4(x, self.base, True, y, bias=self.bias)
+        return ops.linear(x, base_weight(self.base, self.base_mode, x.device), bias=self.bias, out=y)
 
     def backward(self, dy: torch.Tensor) -> torch.Tensor:
         dx = torch.empty(dy.shape[0], self.base.shape[1], dtype=BF16, device=dy.device)
-        return ops.gemm_nf4(dy, self.base, False, dx)
+        if self.base_mode == "inline":
+            return ops.gemm_nf4(dy, self.base, False, dx)
+        return ops.linear_dgrad(dy, base_weight(self.base, self.base_mode, dy.device), out=dx)
 
 
 def _nf4_or_dense(wt, code2, device):

@@ -67,13 +67,29 @@ class SDXLStacksQLoRA:
         self.stacks_cfg = list(stacks)
         self.device = torch.device(device)
         g = torch.Generator(device=self.device).manual_seed(seed)
-        # flat adapter layout: per stack, block, target: down [r, in] then up [out, r]
+        # flat adapter layout, per stack and block: the downs of attn1.to_q / to_k / to_v side by side ([3r, in]:
+        # the stacked B2 of the fused q|k|v input-gradient GEMM, vpt.sdxl), their ups, then every other target's
+        # down [r, in] and up [out, r]
         spans, total = [], 0
         for (_, C, heads, depth, _) in self.stacks_cfg:
             for _i in range(depth):
-                for t, (o, i) in _linear_shapes(heads * 64, context_dim).items():
-                    spans.append((total, (rank, i), total + rank * i, (o, rank)))
-                    total += rank * i + o * rank
+                shp = _linear_shapes(heads * 64, context_dim)
+                qkv = ["attn1.to_q", "attn1.to_k", "attn1.to_v"]
+                off = {}
+                for t in qkv:
+                    o, i = shp[t]
+                    off[t] = [total, None]
+                    total += rank * i
+                for t in qkv:
+                    o, i = shp[t]
+                    off[t][1] = total
+                    total += o * rank
+                for t, (o, i) in shp.items():
+                    if t not in off:
+                        off[t] = [total, total + rank * i]
+                        total += rank * i + o * rank
+                for t, (o, i) in shp.items():
+                    spans.append((off[t][0], (rank, i), off[t][1], (o, rank)))
         self.params = torch.zeros(total, dtype=BF16, device=self.device)
         self.grads = torch.zeros(total, dtype=F32, device=self.device)
         code2 = dynamic_map().to(self.device)
