@@ -19,7 +19,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--time", action="store_true", help="print median ms per forward / backward launch (JSON)")
+    ap.add_argument("--rows64", type=int, default=None,
+                    help="diagnostic library (VPT_DIAG=1): vpt_attn_set_rows64 mask; 8 = the production dK/dV and dQ "
+                         "bodies as two separate launches (per-kind kernel times under rocprofv3)")
     args = ap.parse_args()
+    if args.rows64 is not None:
+        ops.lib.vpt_attn_set_rows64(args.rows64)
     dev = "cuda"
     B, H, n = 8, 12, 4170
     rows, D = n, 768

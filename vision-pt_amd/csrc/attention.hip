@@ -606,6 +606,67 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
     const char* lk = lds[cur][0];
     const char* lv = lds[cur][1];
     const bool dense = kv0 + 64 <= g.n_dense;
+    if (ABL == 8) {
+      // Explicitly ordered body: both key halves' S^T / dP^T chains back to back (the second half's row fragments
+      // read under the first chain), then the first half's exp / dS while the second chain drains, the dQ
+      // products of the first half, the second half's exp / dS, its dQ products -- so no exp waits on the
+      // chain it follows and no MFMA waits on a just-issued LDS read.
+      bf16x8 ka[4], va[4], pd[2][2];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) { ka[ks] = frag_rows(lk, 0, ks, lane); va[ks] = frag_rows(lv, 0, ks, lane); }
+      floatx16 sc[2], dp[2];
+      sc[0] = nlse; dp[0] = ndel;
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        sc[0] = mfma32(ka[ks], qf[ks], sc[0]);
+        dp[0] = mfma32(va[ks], df[ks], dp[0]);
+      }
+      __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) { ka[ks] = frag_rows(lk, 32, ks, lane); va[ks] = frag_rows(lv, 32, ks, lane); }
+      __builtin_amdgcn_sched_barrier(0);
+      sc[1] = nlse; dp[1] = ndel;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        sc[1] = mfma32(ka[ks], qf[ks], sc[1]);
+        dp[1] = mfma32(va[ks], df[ks], dp[1]);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        if (!dense) {
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) {
+            const floatx4 bias = *reinterpret_cast<const floatx4*>(&kbl[kv0 - g.kb0 + 32 * kb + 8 * g4 + 4 * h]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sc[kb][4 * g4 + e] += bias[e];
+          }
+        }
+        floatx16 d;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) d[i] = __builtin_amdgcn_exp2f(sc[kb][i]) * dp[kb][i];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) pd[kb][s2] = pack_acc(d, s2);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 tk[2];
+#pragma unroll
+          for (int db = 0; db < 2; ++db) tk[db] = frag_tr(lk, db, 2 * kb + s2, lane);
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int db = 0; db < 2; ++db) dqT[db] = mfma32(tk[db], pd[kb][s2], dqT[db]);
+          __builtin_amdgcn_s_setprio(0);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      cur ^= 1;
+      continue;
+    }
     floatx16 dS[2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
@@ -647,6 +708,7 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
 // then the dQ blocks. Each kind alone is 3,168 equal blocks at B=8 1024^2 on 512 block slots (2 per CU):
 // 6.19 waves of work run as 7, twice. In one grid the dQ blocks start on the slots the dK/dV tail frees,
 // so the pair runs in ~(work of both) / slots instead of two rounded-up launches.
+template <int DQ>
 __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs g, int nkb, int nqb, int B) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][8192];
   __shared__ __attribute__((aligned(16))) float lstat[2][2][64];
@@ -659,9 +721,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs g, int nkb, i
   } else {
     bid -= nk_blocks;
     const int bx = bid % nqb, r = bid / nqb;
-    dq_body<0, 4>(g, bx, r % g.H, r / g.H, lds, kbl);
+    dq_body<DQ, 4>(g, bx, r % g.H, r / g.H, lds, kbl);
   }
 }
+constexpr int kDqBody = 0;  // production dQ body (0 = compiler-scheduled, 8 = explicitly ordered)
 
 // Dynamic LDS of the key-bias array (fill_key_bias); n <= 32768 keeps it within 128 KB.
 size_t key_bias_lds_bytes(const AttnArgs& g) { return (size_t)((g.nk + 63) / 64 * 64 - g.kb0) * sizeof(float); }
@@ -761,7 +824,22 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
   if (const int rc = diag_attn_bwd_rows64(g, B, H, n, nk, s); rc >= 0) return rc;
 #endif
   const int nkb = (nk + 127) / 128, nqb = (n + 127) / 128;
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3((nkb + nqb) * H * B), dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
+#ifdef VPT_DIAG
+  if (g_rows64 & 32) {  // A/B: the software-pipelined dK/dV kernel (diag include), then the one-launch kernel's dQ blocks
+    if (const int rc = diag_attn_bwd_pipe(g, nkb, H, B, s); rc != VPT_OK) return rc;
+    hipLaunchKernelGGL((attn_bwd_kernel<kDqBody>), dim3(nqb * H * B), dim3(256), key_bias_lds_bytes(g), s, g, 0, nqb, B);
+    VPT_LAUNCH_CHECK();
+    return VPT_OK;
+  }
+  if (g_rows64 & 16) {  // A/B: the other dQ body in the one-launch kernel
+    hipLaunchKernelGGL((attn_bwd_kernel<8 - kDqBody>), dim3((nkb + nqb) * H * B), dim3(256), key_bias_lds_bytes(g), s, g,
+                       nkb, nqb, B);
+    VPT_LAUNCH_CHECK();
+    return VPT_OK;
+  }
+#endif
+  hipLaunchKernelGGL((attn_bwd_kernel<kDqBody>), dim3((nkb + nqb) * H * B), dim3(256), key_bias_lds_bytes(g), s, g, nkb,
+                     nqb, B);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
