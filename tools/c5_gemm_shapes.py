@@ -51,6 +51,8 @@ def main():
                 ws = torch.empty(sp * M * N, dtype=torch.float32, device=dev)
                 ms = timeit(lambda: ops.gemm(a, True, W, fwd, M, N, K, out, splits=sp, workspace=ws, geometry=256))
                 r[f"splitk{sp}_g256"] = [round(fl / ms / 1e9, 1), round(ms * 1e3, 1)]
+                ms = timeit(lambda: ops.gemm_lora(a, W, fwd, a2, b2, M, N, K, out, geometry=128, splits=sp))
+                r[f"lora_splitk{sp}_g128"] = [round(fl / ms / 1e9, 1), round(ms * 1e3, 1)]
             Wt = W.t() if fwd else W
             ms = timeit(lambda: torch.matmul(a, Wt))
             r["torch"] = [round(fl / ms / 1e9, 1), round(ms * 1e3, 1)]
