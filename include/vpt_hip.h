@@ -73,6 +73,12 @@ int vpt_gemm_bf16_lora_grouped(const void* A, long lda, const void* B, long ldb,
                                const void* const* B2s, int G, int r, void* C, long ldc, int M, int g_n, int K,
                                const void* bias, const void* resid, long ldr, int splits, void* workspace,
                                int geometry, void* stream);
+/* The same with the G bases stacked [G*g_n][K] and the G ups stacked [G*g_n][r] (B2, leading dim r), any G:
+ * the cross-attention to_k / to_v of every transformer block over one fixed text context as ONE GEMM per step
+ * (src/models/sdxl/denoiser.py:101-171; the context is the same for all 70 blocks). */
+int vpt_gemm_bf16_lora_stacked(const void* A, long lda, const void* B, long ldb, const void* A2, long lda2,
+                               const void* B2, int G, int r, void* C, long ldc, int M, int g_n, int K, int splits,
+                               void* workspace, int geometry, void* stream);
 /* nn.Linear weight and bias gradient in one call (torch autograd of F.linear for every Linear of
  * src/models/jit/denoiser.py, e.g. :318-323 attention projections, :492-504 SwiGLU, :535-543 FinalLayer):
  * dw[N][K] (=|+=) dy[M][N]^T . x[M][K] and, if db != NULL, db[N] (=|+=) sum_m dy[m][N], both f32

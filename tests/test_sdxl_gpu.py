@@ -455,6 +455,31 @@ def test_sdxl_stacks_step_binds_flat_adapters(ops):
     assert m.flops_per_step() > 0
 
 
+def test_sdxl_stacks_precomputed_ctx_kv_matches_per_block(ops, monkeypatch):
+    """SDXLStacksQLoRA.precompute_ctx_kv (every block's cross-attention k / v of the fixed context as stacked GEMMs,
+    two width classes) against the per-block projections: the same step with non-zero adapters gives the same
+    context gradient and adapter gradients to bf16 rounding of differently ordered sums (the stacked GEMM's
+    k / v are bit-identical in exact arithmetic; ds = s * ctx . down^T is one GEMM instead of lora_proj)."""
+    from vpt.sdxl_train import SDXLStacksQLoRA
+    res = []
+    for pre in (True, False):
+        m = SDXLStacksQLoRA(B=2, stacks=[("a", 640, 10, 1, 16), ("b", 1280, 20, 2, 8), ("c", 640, 10, 1, 16)],
+                            n_ctx=77, seed=3)
+        g = torch.Generator(device=DEV).manual_seed(9)
+        with torch.no_grad():
+            m.params.copy_((torch.randn(m.params.shape, device=DEV, generator=g) * 0.03).bfloat16())
+        if not pre:
+            monkeypatch.setattr(m, "precompute_ctx_kv", lambda ctx, save=True: False)
+        xs, ctx, gs = m.make_inputs(seed=4)
+        m.opt.step = lambda: None  # compare gradients, not the update
+        dctx = m.step(xs, ctx, gs)
+        torch.cuda.synchronize()
+        res.append((dctx.float().clone(), m.grads.clone()))
+    (c0, g0), (c1, g1) = res
+    assert rel(c0, c1) < 1e-2
+    assert rel(g0, g1) < 1e-2 and cos(g0, g1) > 0.9999
+
+
 @pytest.mark.parametrize("M,K,N", [(16384, 640, 5120), (1000, 1280, 2048), (924, 2048, 1280)])
 def test_lora_skinny_kernels_vs_torch(ops, M, K, N):
     """vpt_lora_proj (both W layouts) and vpt_lora_wgrad (both output layouts, accumulate) vs fp32 torch on

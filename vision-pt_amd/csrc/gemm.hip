@@ -65,7 +65,8 @@ struct GemmArgs {
   int K2;
   // grouped K-extension (forward of several LoRA targets sharing one input, outputs side by side): output
   // columns [g * g_n, (g + 1) * g_n) take their extension from A2 columns [g * K2, (g + 1) * K2) and B2g[g]
-  // ([g_n][K2], k-major); g_n = 0: ungrouped (B2). Tiles never straddle groups (g_n % tile width == 0).
+  // ([g_n][K2], k-major), or with B2g[0] null from the stacked B2 rows [g * g_n, (g + 1) * g_n); g_n = 0:
+  // ungrouped (B2). Tiles never straddle groups (g_n % tile width == 0).
   const bf16_t* B2g[4];
   int g_n;
 };
@@ -312,7 +313,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_bf16_kernel(GemmArgs g
     }
     const int e0 = (t - nkm) * BK, kv = min(BK, g.K2 - e0);
     const int grp = g.g_n > 0 ? n0 / g.g_n : 0;  // grouped extension: this tile's target
-    const bf16_t* b2 = g.g_n > 0 ? g.B2g[grp] : g.B2;
+    const bf16_t* b2 = g.g_n > 0 ? (g.B2g[0] ? g.B2g[grp] : g.B2 + (long)grp * g.g_n * g.ldb2) : g.B2;
     const int nb0 = n0 - grp * g.g_n, nrows = g.g_n > 0 ? g.g_n : g.N;
     glds_tile<AK, TM, G::NW>(buf, tile_ptr<AK>(g.A2 + grp * g.K2, g.lda2, m0, e0), g.lda2, m0, g.M, kv, wid, lane);
     glds_tile<BK_, TN, G::NW>(buf + G::A_BYTES, tile_ptr<BK_>(b2, g.ldb2, nb0, e0), g.ldb2, nb0, nrows, kv, wid, lane);
@@ -546,7 +547,7 @@ __device__ __forceinline__ void ring_issue(const GemmArgs& g, const RingItem& it
   if (k0 >= it.kend) {  // K-extension tile (A2 / B2); its k >= K2 lanes are masked like a partial last tile
     const int e0 = k0 - it.kend, kv = min(RBK, g.K2 - e0);
     const int grp = g.g_n > 0 ? it.n0 / g.g_n : 0;  // grouped extension: this tile's target
-    const bf16_t* b2 = g.g_n > 0 ? g.B2g[grp] : g.B2;
+    const bf16_t* b2 = g.g_n > 0 ? (g.B2g[0] ? g.B2g[grp] : g.B2 + (long)grp * g.g_n * g.ldb2) : g.B2;
     const int nb0 = it.n0 - grp * g.g_n, nrows = g.g_n > 0 ? g.g_n : g.N;
     const void* ab = uniform_ptr(tile_ptr<AK>(g.A2 + grp * g.K2, g.lda2, it.m0, e0));
     const void* bb = uniform_ptr(tile_ptr<BK_>(b2, g.ldb2, nb0, e0));
@@ -1224,6 +1225,22 @@ extern "C" int vpt_gemm_bf16_lora_grouped(const void* A, long lda, const void* B
                    1.f, geometry, 0, stream, nullptr, 0, nullptr, A2, lda2, B2s[0], r, r, B2s, G, g_n);
 }
 
+// Any number G of LoRA targets reading the same input, bases stacked [G * g_n][K] and adapters' ups stacked
+// [G * g_n][r] (B2, ld r): C[:, g*g_n:(g+1)*g_n] = A . W_g^T + A2[:, g*r:(g+1)*r] . up_g^T. The cross-attention
+// k / v projections of a fixed text context for every transformer block of a step as one GEMM.
+extern "C" int vpt_gemm_bf16_lora_stacked(const void* A, long lda, const void* B, long ldb, const void* A2, long lda2,
+                                          const void* B2, int G, int r, void* C, long ldc, int M, int g_n, int K,
+                                          int splits, void* workspace, int geometry, void* stream) {
+  VPT_CHECK_ARG(A2 && B2 && G > 0, "vpt_gemm_bf16_lora_stacked: null LoRA operand");
+  VPT_CHECK_ARG(K % 64 == 0 && r > 0 && r <= 64 && r % 8 == 0 && g_n % 128 == 0,
+                "vpt_gemm_bf16_lora_stacked: K % 64 == 0, r in 8..64 (r % 8 == 0), g_n % 128 == 0");
+  VPT_CHECK_ARG(lda2 % 8 == 0 && lda2 >= (long)G * r, "vpt_gemm_bf16_lora_stacked: lda2 >= G * r (16-B multiple)");
+  VPT_CHECK_ARG((long)G * g_n < (1L << 31), "vpt_gemm_bf16_lora_stacked: G * g_n < 2^31");
+  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256, "vpt_gemm_bf16_lora_stacked: geometry 0, 128, 256");
+  return gemm_impl(A, lda, 1, B, ldb, 1, C, ldc, M, G * g_n, K, nullptr, nullptr, 0, OUT_BF16, ACT_NONE, splits,
+                   workspace, 1.f, geometry, 0, stream, nullptr, 0, nullptr, A2, lda2, B2, r, r, nullptr, G, g_n);
+}
+
 extern "C" int vpt_gemm_bf16_tiled(const void* A, long lda, int a_kmajor, const void* B, long ldb, int b_kmajor,
                                    void* C, long ldc, int M, int N, int K, const void* bias, const void* resid,
                                    long ldr, int out_mode, int act, int splits, void* workspace, float alpha,
@@ -1266,6 +1283,8 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
   g.K2 = A2 ? K2 : 0;
   if (B2g && G > 0) {
     for (int i = 0; i < G; ++i) g.B2g[i] = (const bf16_t*)B2g[i];
+    g.g_n = g_n;
+  } else if (G > 0) {  // stacked groups: B2 = [G * g_n][K2]
     g.g_n = g_n;
   }
 #ifdef VPT_DIAG

@@ -133,11 +133,12 @@ def gemm(a, a_kmajor: bool, b, b_kmajor: bool, M: int, N: int, K: int, out, *, b
 _WS: dict = {}  # (device, tag) -> f32 workspace grown on demand (stream-ordered reuse on one stream)
 
 
-def workspace(dev, tag: str, nfloats: int) -> torch.Tensor:
+def workspace(dev, tag: str, n: int, dtype=F32) -> torch.Tensor:
+    """A per-(device, tag) buffer of at least n elements, grown on demand (stream-ordered reuse)."""
     buf = _WS.get((str(dev), tag))
-    if buf is None or buf.numel() < nfloats:
-        buf = _WS[(str(dev), tag)] = torch.empty(nfloats, dtype=F32, device=dev)
-    return buf
+    if buf is None or buf.numel() < n or buf.dtype != dtype:
+        buf = _WS[(str(dev), tag)] = torch.empty(n, dtype=dtype, device=dev)
+    return buf[:n]
 
 
 def lora_gemm_plan(M: int, N: int, K: int) -> tuple[int, int]:
@@ -212,6 +213,33 @@ def gemm_lora_grouped(x, w_stacked, a2, ups, out, *, bias=None, resid=None, geom
         run()
     else:
         pr.record(2.0 * M * G * gn * (K + r), run, key=f"fwd{G} M{M} N{G * gn} K{K}")
+    return out
+
+
+def gemm_lora_stacked(x, w_stacked, a2, ups_stacked, g_n: int, out, *, geometry=None, splits=None):
+    """G = ups_stacked.shape[0] / g_n LoRA targets over one input as one GEMM (vpt_gemm_bf16_lora_stacked):
+    out[:, g*g_n:(g+1)*g_n] = x . W_g^T + a2[:, g*r:(g+1)*r] . up_g^T with W, up stacked by rows."""
+    for t, n in ((x, "x"), (w_stacked, "w_stacked"), (a2, "a2"), (ups_stacked, "ups_stacked"), (out, "out")):
+        _chk(t, BF16, n)
+    M, K = x.shape
+    NG, r = ups_stacked.shape
+    G = NG // g_n
+    if G * g_n != NG or w_stacked.shape[0] != NG or ups_stacked.stride(0) != r:
+        raise ValueError("gemm_lora_stacked: stacked shapes")
+    geo, sp = lora_gemm_plan(M, NG, K)
+    geometry = geo if geometry is None else geometry
+    splits = sp if splits is None else splits
+    ws = workspace(out.device, "gemm_lora", splits * M * NG) if splits > 1 else None
+
+    def run():
+        call("vpt_gemm_bf16_lora_stacked", x.data_ptr(), x.stride(0), w_stacked.data_ptr(), w_stacked.stride(0),
+             a2.data_ptr(), a2.stride(0), ups_stacked.data_ptr(), G, r, out.data_ptr(), out.stride(0), M, g_n, K,
+             int(splits), _p(ws), int(geometry), stream())
+    pr = PROBES.get("gemm_lora")
+    if pr is None:
+        run()
+    else:
+        pr.record(2.0 * M * NG * (K + r), run, key=f"stacked{G} M{M} N{NG} K{K}")
     return out
 
 

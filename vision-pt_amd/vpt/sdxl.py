@@ -274,6 +274,9 @@ class SDXLTransformerBlock:
         self.norm = {k: (sd[f"{k}.weight"].to(device, BF16).contiguous(), sd[f"{k}.bias"].to(device, BF16).contiguous())
                      for k in ("norm1", "norm2", "norm3")}
         self._st = None
+        # (k, v) of the cross-attention, projected for the next forward by the caller (SDXLStacksQLoRA.
+        # precompute_ctx_kv: every block's over one fixed context in stacked GEMMs); None: projected here
+        self.ctx_kv = None
 
     def _attn_fwd(self, q, k, v, B, n, nk):
         """q must already be pre-scaled (`_qs`); the backward returns the gradient of the raw q."""
@@ -341,7 +344,11 @@ class SDXLTransformerBlock:
     def forward(self, x: torch.Tensor, ctx: torch.Tensor, B: int, n: int, nc: int, save: bool = True) -> torch.Tensor:
         """x [B*n, dim] bf16, ctx [B*nc, context_dim] bf16 -> [B*n, dim] bf16 (denoiser.py:258-280)."""
         L = self.lin
-        Wb = dequant_bases(L, TARGETS, self.device)  # the block's ten bases, one launch
+        kv = self.ctx_kv
+        self.ctx_kv = None
+        # the block's bases, one launch (the cross-attention k / v ones only when not projected already)
+        Wb = dequant_bases(L, TARGETS if kv is None else [t for t in TARGETS if t not in ("attn2.to_k", "attn2.to_v")],
+                           self.device)
         h1, m1, r1 = ops.layernorm_fwd(x, *self.norm["norm1"])
         if self._fuse_qkv(Wb):
             q, k, v = self._qkv_fwd(h1, Wb["attn1.qkv"], save)
@@ -352,8 +359,11 @@ class SDXLTransformerBlock:
         x1 = L["attn1.to_out.0"].forward(o1, save, resid=x, W=Wb.get("attn1.to_out.0"))
         h2, m2, r2 = ops.layernorm_fwd(x1, *self.norm["norm2"])
         q2 = self._qs(L["attn2.to_q"].forward(h2, save, W=Wb.get("attn2.to_q")))
-        k2 = L["attn2.to_k"].forward(ctx, save, W=Wb.get("attn2.to_k"))
-        v2 = L["attn2.to_v"].forward(ctx, save, W=Wb.get("attn2.to_v"))
+        if kv is not None:
+            k2, v2 = kv
+        else:
+            k2 = L["attn2.to_k"].forward(ctx, save, W=Wb.get("attn2.to_k"))
+            v2 = L["attn2.to_v"].forward(ctx, save, W=Wb.get("attn2.to_v"))
         o2, lse2 = self._attn_fwd(q2, k2, v2, B, n, nc)
         x2 = L["attn2.to_out.0"].forward(o2, save, resid=x1, W=Wb.get("attn2.to_out.0"))
         h3, m3, r3 = ops.layernorm_fwd(x2, *self.norm["norm3"])

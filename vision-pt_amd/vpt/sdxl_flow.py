@@ -119,6 +119,7 @@ class SDXLFlowMatchQLoRA:
         hA, hB = sA * sA, sB * sB
         S = [st for (_, _, _, st) in self.core.stacks]
         nc = self.n_ctx
+        self.core.precompute_ctx_kv(ctx)  # every block's cross-attention k / v of the fixed context, stacked GEMMs
         eA, eB, eU = self.e_in.fwd(sg), self.e_down.fwd(sg), self.e_up.fwd(sg)
         tok = ops.space_to_depth(z, B, 4, self.L, self.L, 2).view(B * hA, 16)
         x64 = ops.transpose_add(self._map_per_sample(self.m_in, tok, eA, hA).view(B, hA, cA), B, hA, cA)

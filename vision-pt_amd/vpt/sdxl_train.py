@@ -70,12 +70,16 @@ class SDXLStacksQLoRA:
         # flat adapter layout, per stack and block: the downs of attn1.to_q / to_k / to_v side by side ([3r, in]:
         # the stacked B2 of the fused q|k|v input-gradient GEMM, vpt.sdxl), their ups, then every other target's
         # down [r, in] and up [out, r]
+        # The cross-attention to_k / to_v adapters of ALL blocks live in three regions of their own (every down
+        # [r, context_dim] side by side; the ups side by side per width class), so that precompute_ctx_kv runs the
+        # k / v projections of the (fixed) text context for the whole step as stacked GEMMs.
+        KV = ("attn2.to_k", "attn2.to_v")
         spans, total = [], 0
         for (_, C, heads, depth, _) in self.stacks_cfg:
             for _i in range(depth):
                 shp = _linear_shapes(heads * 64, context_dim)
                 qkv = ["attn1.to_q", "attn1.to_k", "attn1.to_v"]
-                off = {}
+                off = {t: [None, None] for t in KV}
                 for t in qkv:
                     o, i = shp[t]
                     off[t] = [total, None]
@@ -89,7 +93,25 @@ class SDXLStacksQLoRA:
                         off[t] = [total, total + rank * i]
                         total += rank * i + o * rank
                 for t, (o, i) in shp.items():
-                    spans.append((off[t][0], (rank, i), off[t][1], (o, rank)))
+                    spans.append([off[t][0], (rank, i), off[t][1], (o, rank)])
+        # the k / v regions: downs of every block, then the ups of the 1280-wide and of the 640-wide blocks
+        widths = sorted({heads * 64 for (_, _, heads, _, _) in self.stacks_cfg}, reverse=True)
+        # k / v targets by width class (1280 first), then in block order, k before v: the column order of the
+        # step's ds = s * ctx . downs^T and of the stacked GEMM's output blocks
+        kv_idx = sorted((k for k, _ in enumerate(spans) if TARGETS[k % len(TARGETS)] in KV),
+                        key=lambda k: (-spans[k][3][0], k))
+        self._kv_order = kv_idx
+        self._kv_down0 = total
+        for k in kv_idx:
+            spans[k][0] = total
+            total += rank * context_dim
+        self._kv_up0 = {}
+        for w in widths:
+            self._kv_up0[w] = total
+            for k in kv_idx:
+                if spans[k][3][0] == w:
+                    spans[k][2] = total
+                    total += w * rank
         self.params = torch.zeros(total, dtype=BF16, device=self.device)
         self.grads = torch.zeros(total, dtype=F32, device=self.device)
         code2 = dynamic_map().to(self.device)
@@ -140,6 +162,46 @@ class SDXLStacksQLoRA:
     def n_adapter_params(self) -> int:
         return self.params.numel()
 
+    def precompute_ctx_kv(self, ctx: torch.Tensor, save: bool = True) -> bool:
+        """The cross-attention to_k / to_v of every block over the step's text context ctx [B*n_ctx, context_dim]:
+        their bases dequantised (16 per launch), ds = s * ctx . [all k/v downs]^T as one GEMM, then one stacked
+        base+LoRA GEMM per width class (vpt_gemm_bf16_lora_stacked). Each block's forward then takes its k / v column
+        blocks (SDXLTransformerBlock.ctx_kv) and its adapters' backward the saved (ctx, ds) column slices. Returns
+        False (nothing done: the blocks project per target) for the "inline" base mode or non-skinny adapters."""
+        from .sdxl import base_weight
+        all_lins = [blk.lin[t] for (_, _, _, st) in self.stacks for blk in st.blocks for t in TARGETS]
+        owner = {id(blk.lin[t]): (blk, t) for (_, _, _, st) in self.stacks for blk in st.blocks for t in TARGETS}
+        lins = [all_lins[k] for k in self._kv_order]
+        if any(l.base_mode == "inline" or not (l.fused and l.skinny) for l in lins):
+            return False
+        r, cd, M = self.rank, self.cdim, ctx.shape[0]
+        downs = self.params[self._kv_down0:self._kv_down0 + len(lins) * r * cd].view(len(lins) * r, cd)
+        ds = torch.empty(M, len(lins) * r, dtype=BF16, device=self.device)
+        ops.gemm(ctx, True, downs, True, M, len(lins) * r, cd, ds, alpha=lins[0].scale)
+        c0 = 0
+        for w, u0 in self._kv_up0.items():
+            group = [l for l in lins if l.base.shape[0] == w]
+            G = len(group)
+            ups = self.params[u0:u0 + G * w * r].view(G * w, r)
+            if group[0].base_mode == "resident":
+                W = self._kv_resident.get(w) if hasattr(self, "_kv_resident") else None
+                if W is None:
+                    W = torch.cat([base_weight(l.base, "resident", self.device) for l in group], 0)
+                    self._kv_resident = {**getattr(self, "_kv_resident", {}), w: W}
+            else:
+                W = ops.workspace(self.device, f"kv_base{w}", G * w * cd, BF16).view(G * w, cd)
+                ops.nf4_dequant_batch([(l.base, W[i * w:(i + 1) * w]) for i, l in enumerate(group)])
+            out = ops.workspace(self.device, f"kv_out{w}", M * G * w, BF16).view(M, G * w)
+            ops.gemm_lora_stacked(ctx, W, ds[:, c0:c0 + G * r], ups, w, out)
+            for i, l in enumerate(group):
+                l._saved = (ctx, ds[:, c0 + i * r:c0 + (i + 1) * r]) if save else None
+                blk, t = owner[id(l)]
+                kv = list(blk.ctx_kv or (None, None))
+                kv[0 if t == "attn2.to_k" else 1] = out[:, i * w:(i + 1) * w]
+                blk.ctx_kv = tuple(kv)
+            c0 += G * r
+        return True
+
     def make_inputs(self, seed: int = 1):
         """Synthetic stage activations (NCHW bf16), text context [B*231, 2048] and output gradients g_s."""
         g = torch.Generator(device=self.device).manual_seed(seed)
@@ -153,6 +215,7 @@ class SDXLStacksQLoRA:
         """One training step: forward of every stack, backward in reverse order, fused optimizer step.
         Returns the context gradient (summed over stacks), [B*231, 2048] bf16."""
         self.grads.zero_()
+        self.precompute_ctx_kv(ctx)
         for x, (_, C, HW, st) in zip(xs, self.stacks):
             st.forward(x, ctx, self.B, HW, self.n_ctx)
         dctx = None
