@@ -175,10 +175,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # VPT_DIST_BACKEND=gloo: a rehearsal of the N > 1 path with several ranks sharing the box's GPUs (RCCL needs
+    # one GPU per rank); the measured line is always nccl (= RCCL over xGMI), one rank per GPU
+    backend = os.environ.get("VPT_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
 
     from vpt import ops
     from vpt.config import JiT_B_16_Config, JiTTrainingConfig
