@@ -467,7 +467,8 @@ __device__ __forceinline__ void bare_barrier() {
 
 using GR = Geo<256, 256, 2, 4>;
 
-// ABL (timing-only ablations, wrong results): 1 = no LDS-DMA inside the loop, 2 = no vmcnt waits.
+// ABL (timing-only ablations, wrong results): 1 = no LDS-DMA inside the loop, 2 = no vmcnt waits, 3 = no
+// epilogue, 4 = epilogue stores dropped (zero-size buffer).
 // DMAC: issue tile t+3's LDS-DMA at the start of the MFMA phase C_t instead of in L_t. It overwrites
 // the stage of tile t-1, which every wave consumed by MFMAs before its previous barrier, so the
 // barriers need no lgkmcnt(0) and L_t shrinks to the ds_reads; tile t+1 is then waited for with only
@@ -986,6 +987,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
     EpiPre pre;
     if (!SW) {
       ea = epi_addr(g, it, wm, wn, lane);
+      if (ABL == 4) ea.rs = __builtin_amdgcn_make_buffer_rsrc(g.C, (short)0, 0, 0x00020000);  // stores dropped
       if (GF) {
         epi_preload<EPI, 0>(g, ea, pre);
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the first group landed (nothing else in flight)
@@ -1093,6 +1095,10 @@ int launch_ring(const GemmArgs& g, int splits, hipStream_t s) {
   return VPT_OK;
 }
 
+#ifdef VPT_DIAG
+#include "diag/gemm_ring4.inc"
+#endif
+
 template <bool AK, bool BK_>
 int launch_geo(const GemmArgs& g, int splits, int geo, hipStream_t s) {
   if (geo != 128 && geo != 2562 && g.N % 8 != 0) geo = 128;  // ring epilogue stores 8-column chunks
@@ -1107,6 +1113,10 @@ int launch_geo(const GemmArgs& g, int splits, int geo, hipStream_t s) {
   if (AK && BK_ && geo == 2566 && g.dbg) return launch_ring<AK, BK_, true, 0, false, true>(g, splits, s);  // stamps
   if (AK && BK_ && geo == 2567 && g.dbg) return launch_ring<AK, BK_, true, 0, false, false, true>(g, splits, s);
   if (geo == 2568) return launch_ring<AK, BK_, true, 3>(g, splits, s);  // no epilogue (wrong results)
+  if (AK && BK_ && geo == 2572) return launch_ring<AK, BK_, true, 4>(g, splits, s);  // stores dropped (wrong)
+  if (geo == 2569 && g.sw != 1 && !g.rsum) return launch_ring4<AK, BK_>(g, splits, s);  // 4-wave ring
+  if (AK && BK_ && geo == 2570) return launch_ring4<AK, BK_, 1>(g, splits, s);  // 4-wave, no DMA (wrong results)
+  if (AK && BK_ && geo == 2571) return launch_ring4<AK, BK_, 3>(g, splits, s);  // 4-wave, no epilogue (wrong)
   if (geo == 2562) return launch<AK, BK_, 256, 256, 2, 4>(g, splits, s);  // 2-stage BK=64 T256 (A/B only)
 #endif
   return launch<AK, BK_, 128, 128, 2, 2>(g, splits, s);
@@ -1346,8 +1356,8 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
 #ifdef VPT_DIAG
 // ---- diagnostic build only (libvpt_hip_diag.so, include/vpt_hip_diag.h): process-wide switches ----
 extern "C" int vpt_gemm_set_geometry(int geo) {
-  VPT_CHECK_ARG(geo == 0 || geo == 128 || geo == 256 || (geo >= 2561 && geo <= 2568),
-                "vpt_gemm_set_geometry: 0, 128, 256 or 2561-2568");
+  VPT_CHECK_ARG(geo == 0 || geo == 128 || geo == 256 || (geo >= 2561 && geo <= 2572),
+                "vpt_gemm_set_geometry: 0, 128, 256 or 2561-2572");
   g_geo_override = geo;
   return VPT_OK;
 }

@@ -9,6 +9,7 @@ from __future__ import annotations
 import concurrent.futures as cf
 import os
 import subprocess
+import sys
 from pathlib import Path
 
 PKG_ROOT = Path(__file__).resolve().parent.parent  # vision-pt_amd/
@@ -45,9 +46,20 @@ def _compile(src: Path, diag: bool = False) -> Path:
     return obj
 
 
+def _gen_diag_sources() -> None:
+    """csrc/diag/ring4_agpr.inc (the 4-wave ring GEMM's fixed-AGPR accessors) from its generator."""
+    gen, inc = CSRC / "diag" / "gen_ring4_agpr.py", CSRC / "diag" / "ring4_agpr.inc"
+    if not inc.exists() or inc.stat().st_mtime < gen.stat().st_mtime:
+        r = subprocess.run([sys.executable, str(gen)], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"{gen.name} failed:\n{r.stderr[-2000:]}")
+
+
 def build(verbose: bool = False, diag: bool = False) -> Path:
     """Production library (default) or its diagnostic twin (diag=True, -DVPT_DIAG)."""
     bdir, lib = (BUILD_DIAG, LIB_DIAG) if diag else (BUILD, LIB)
+    if diag:
+        _gen_diag_sources()
     bdir.mkdir(exist_ok=True)
     lib.parent.mkdir(exist_ok=True)
     srcs = sorted(CSRC.glob("*.hip"))
@@ -65,5 +77,4 @@ def build(verbose: bool = False, diag: bool = False) -> Path:
 
 
 if __name__ == "__main__":
-    import sys
     build(verbose=True, diag="--diag" in sys.argv)
