@@ -468,7 +468,7 @@ __device__ __forceinline__ void bare_barrier() {
 using GR = Geo<256, 256, 2, 4>;
 
 // ABL (timing-only ablations, wrong results): 1 = no LDS-DMA inside the loop, 2 = no vmcnt waits, 3 = no
-// epilogue, 4 = epilogue stores dropped (zero-size buffer).
+// epilogue, 4 = epilogue stores dropped (zero-size buffer), 5 = no epilogue stores (plain bf16 output).
 // DMAC: issue tile t+3's LDS-DMA at the start of the MFMA phase C_t instead of in L_t. It overwrites
 // the stage of tile t-1, which every wave consumed by MFMAs before its previous barrier, so the
 // barriers need no lgkmcnt(0) and L_t shrinks to the ds_reads; tile t+1 is then waited for with only
@@ -688,7 +688,7 @@ __device__ __forceinline__ void store_b128_padded(u32x4 v, __amdgpu_buffer_rsrc_
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int EPI, int I0, int I1>
+template <int EPI, int I0, int I1, bool NOST = false>
 __device__ __forceinline__ void epilogue_ring(const GemmArgs& g, const floatx4 (&acc)[8][4], char* stg, int lane,
                                               const EpiAddr& e, const float (&bias8)[8], const EpiPre& pre) {
   const int cw = lane & 7;
@@ -738,7 +738,8 @@ __device__ __forceinline__ void epilogue_ring(const GemmArgs& g, const floatx4 (
           for (int q = 0; q < 8; ++q) o[q] = bf2f(f2bf(o[q])) + rv[q];
         }
         const uint4 w = pack8(o);
-        store_b128_padded(u32x4{w.x, w.y, w.z, w.w}, e.rs, (int)e.voff, soff);
+        if (NOST) asm volatile("" :: "v"(w.x), "v"(w.y), "v"(w.z), "v"(w.w));  // timing ablation: no store
+        else store_b128_padded(u32x4{w.x, w.y, w.z, w.w}, e.rs, (int)e.voff, soff);
       } else {
         if (EPI == EPI_ACC) {
           const u32x4 a0 = pre.v[4 * il + 2 * p], a1 = pre.v[4 * il + 2 * p + 1];
@@ -1024,7 +1025,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
       epi_preload<EPI, 4>(g, ea, pre);
       epilogue_ring<EPI, 4, 8>(g, acc, stg, lane, ea, bias8, pre);
     } else {
-      epilogue_ring<EPI, 0, 8>(g, acc, stg, lane, ea, bias8, pre);
+      epilogue_ring<EPI, 0, 8, ABL == 5>(g, acc, stg, lane, ea, bias8, pre);
     }
     if (TL) tl_stamp(g, kth, 3, wid, lane);
     ++kth;
@@ -1033,7 +1034,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
     // X_0, which every wave reaches only after its staging reads (raw_barrier: lgkmcnt(0) first).
     item = next;
     it = nx;
-    pend = ABL == 3 ? 0 : S;  // the epilogue's S stores are younger than the next item's pre-issued tiles 0-2
+    pend = ABL == 3 || ABL == 5 ? 0 : S;  // the epilogue's S stores are younger than the next item's pre-issued tiles 0-2
   }
 }
 
@@ -1114,6 +1115,7 @@ int launch_geo(const GemmArgs& g, int splits, int geo, hipStream_t s) {
   if (AK && BK_ && geo == 2567 && g.dbg) return launch_ring<AK, BK_, true, 0, false, false, true>(g, splits, s);
   if (geo == 2568) return launch_ring<AK, BK_, true, 3>(g, splits, s);  // no epilogue (wrong results)
   if (AK && BK_ && geo == 2572) return launch_ring<AK, BK_, true, 4>(g, splits, s);  // stores dropped (wrong)
+  if (AK && BK_ && geo == 2573) return launch_ring<AK, BK_, true, 5>(g, splits, s);  // no stores (wrong)
   if (geo == 2569 && g.sw != 1 && !g.rsum) return launch_ring4<AK, BK_>(g, splits, s);  // 4-wave ring
   if (AK && BK_ && geo == 2570) return launch_ring4<AK, BK_, 1>(g, splits, s);  // 4-wave, no DMA (wrong results)
   if (AK && BK_ && geo == 2571) return launch_ring4<AK, BK_, 3>(g, splits, s);  // 4-wave, no epilogue (wrong)
@@ -1356,8 +1358,8 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
 #ifdef VPT_DIAG
 // ---- diagnostic build only (libvpt_hip_diag.so, include/vpt_hip_diag.h): process-wide switches ----
 extern "C" int vpt_gemm_set_geometry(int geo) {
-  VPT_CHECK_ARG(geo == 0 || geo == 128 || geo == 256 || (geo >= 2561 && geo <= 2572),
-                "vpt_gemm_set_geometry: 0, 128, 256 or 2561-2572");
+  VPT_CHECK_ARG(geo == 0 || geo == 128 || geo == 256 || (geo >= 2561 && geo <= 2573),
+                "vpt_gemm_set_geometry: 0, 128, 256 or 2561-2573");
   g_geo_override = geo;
   return VPT_OK;
 }
