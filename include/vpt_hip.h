@@ -284,6 +284,11 @@ int vpt_gemm_nf4(const void* A, long lda, const void* packed, const void* qabsma
  * (lora_wgrad_workspace(M, N) bytes each), summed in a fixed order (deterministic). */
 int vpt_lora_proj(const void* X, long ldx, const void* W, int w_kmajor, void* Y, long ldy, int M, int K, int r,
                   float alpha, void* stream);
+/* G lora_proj in one launch: group g reads X + g * x_goff and W + g * w_goff (elements) and writes output columns
+ * [16 g, 16 g + 16) of Y (the q / k / v adapters of one input: the downs stacked [3 * 16][K]; or of the three
+ * column blocks of the q|k|v gradient: x_goff = dim, the ups stacked [3 * dim][16]). */
+int vpt_lora_proj_grouped(const void* X, long ldx, long x_goff, const void* W, int w_kmajor, long w_goff, void* Y,
+                          long ldy, int M, int K, int r, int G, float alpha, void* stream);
 long vpt_lora_wgrad_workspace(int M, int N);
 int vpt_lora_wgrad2(const void* dY, long lddy, const void* dS, long ldds, float* g_up, int n_out, const void* X,
                     long ldx, const void* vS, long ldvs, float* g_down, int n_in, int M, int accumulate, float alpha,
@@ -302,6 +307,19 @@ int vpt_lora_wgrad_splits(int M, int N);
 int vpt_lora_wgrad2_partial(const void* dY, long lddy, const void* dS, long ldds, int n_out, const void* X, long ldx,
                             const void* vS, long ldvs, int n_in, int M, void* ws_up, void* ws_down, void* stream);
 int vpt_lora_wgrad_reduce_batch(const VptLoraReduceJob* jobs, int njobs, float alpha, int accumulate, void* stream);
+/* The slab half of up to 24 one-sided adapter-gradient jobs in ONE launch (a transformer block's ten targets,
+ * deferred to the end of its backward): job i writes the split-M slabs of X[M][N]^T . S[M][16] into part
+ * (vpt_lora_wgrad_workspace(M, N) bytes; vpt_lora_wgrad_splits(M, N) slabs), exactly as the matching side of
+ * vpt_lora_wgrad2_partial (g_up: X = dY, S = dS; g_down: X = X, S = vS); reduced by vpt_lora_wgrad_reduce_batch. */
+typedef struct {
+  const void* X;
+  long ldx;
+  const void* S;
+  long lds;
+  float* part;
+  int N, M;
+} VptLoraWgradJob;
+int vpt_lora_wgrad_partial_batch(const VptLoraWgradJob* jobs, int njobs, void* stream);
 /* SpatialTransformer (src/models/sdxl/denoiser.py:283-365) around the transformer blocks:
  * GroupNorm(G, C, eps) on NCHW bf16 [B][C][HW] (f32 statistics mean / rstd [B*G] saved for the backward;
  * output NCHW bf16), its input gradient (affine weights frozen under QLoRA; dres: + a second NCHW gradient),

@@ -517,3 +517,53 @@ def test_lora_skinny_kernels_vs_torch(ops, M, K, N):
         last = i == T - 1
         ops.lora_wgrad2(dy, dss[i], ref_u, x, vss[i], ref_d, accumulate=not last, alpha=1.0 if last else 3.0)
         assert torch.equal(gu[i], ref_u) and torch.equal(gd[i], ref_d), i
+
+
+@pytest.mark.parametrize("w_kmajor", [True, False])
+def test_lora_proj_grouped_bit_exact_vs_per_group(ops, w_kmajor):
+    """vpt_lora_proj_grouped (the q / k / v adapters of one input, or of the three column blocks of the q|k|v
+    gradient) against one vpt_lora_proj per group on the same operands: bit-identical."""
+    M, D = 1000, 1280
+    if w_kmajor:  # forward: one input, the three downs stacked [3 * 16][D]
+        x = rnd(M, D, seed=90)
+        w = rnd(3 * 16, D, scale=0.05, seed=91)
+        xs = [x, x, x]
+        ws = [w[16 * g:16 * (g + 1)] for g in range(3)]
+        x_goff, w_goff = 0, 16 * D
+    else:  # input gradient: [dq | dk | dv] [M][3D], the three ups stacked [3 * D][16]
+        x = rnd(M, 3 * D, seed=92)
+        w = rnd(3 * D, 16, scale=0.05, seed=93)
+        xs = [x[:, g * D:(g + 1) * D] for g in range(3)]
+        ws = [w[g * D:(g + 1) * D] for g in range(3)]
+        x_goff, w_goff = D, D * 16
+    out = torch.empty(M, 48, dtype=torch.bfloat16, device=DEV)
+    ops.lora_proj_grouped(x if w_kmajor else x[:, :D], x_goff, ws[0], w_goff, 3, w_kmajor, out, alpha=0.0625)
+    for g in range(3):
+        ref = torch.empty(M, 16, dtype=torch.bfloat16, device=DEV)
+        ops.lora_proj(xs[g], ws[g], w_kmajor, ref, alpha=0.0625)
+        assert torch.equal(out[:, 16 * g:16 * (g + 1)], ref), g
+
+
+def test_lora_wgrad_deferred_batch_matches_immediate(ops, monkeypatch):
+    """lora_wgrad_batch with the slab products deferred to one vpt_lora_wgrad_partial_batch launch (jobs of
+    different M and widths, as a transformer block's self-attention, cross-attention context and ff targets) is
+    bit-identical to each target's own slab launch."""
+    shapes = [(4096, 1280, 1280), (924, 1280, 2048), (4096, 10240, 1280), (4096, 1280, 5120), (1000, 640, 640)]
+    ops_in = []
+    for i, (M, n_out, n_in) in enumerate(shapes):
+        ops_in.append((rnd(M, n_out, seed=100 + i), rnd(M, 16, seed=110 + i), rnd(M, n_in, seed=120 + i),
+                       rnd(M, 16, seed=130 + i)))
+    res = []
+    for defer in (True, False):
+        monkeypatch.setattr(ops, "_LORA_DEFER", defer)
+        gs = [(torch.full((n_out, 16), 0.5, device=DEV), torch.full((16, n_in), -0.25, device=DEV))
+              for (_, n_out, n_in) in shapes]
+        with ops.lora_wgrad_batch():
+            for (dy, ds, x, vs), (gu, gd) in zip(ops_in, gs):
+                ops.lora_wgrad2(dy, ds, gu, x, vs, gd, accumulate=True, alpha=0.0625)
+        torch.cuda.synchronize()
+        res.append(gs)
+    for i, ((a_u, a_d), (b_u, b_d)) in enumerate(zip(*res)):
+        assert torch.equal(a_u, b_u) and torch.equal(a_d, b_d), shapes[i]
+    dy, ds, x, vs = ops_in[1]
+    assert rel(res[0][1][0], 0.5 + 0.0625 * dy.float().t() @ ds.float()) < 1e-5

@@ -27,7 +27,6 @@
 namespace {
 
 constexpr int BK = 64;
-constexpr int EPI_LD = 68;  // f32 staging row stride (floats), conflict-free for the column writes
 
 enum { OUT_BF16 = 0, OUT_F32 = 1, OUT_F32_ACC = 2 };
 enum { ACT_NONE = 0, ACT_SILU = 1 };
@@ -104,7 +103,9 @@ __device__ __forceinline__ void glds16(const void* sbase, uint32_t voff, uint32_
 template <bool KMAJ, int R, int NW>
 __device__ __forceinline__ void glds_tile(char* lds, const bf16_t* tile_base, long ld, int row0, int nrows, int kvalid,
                                           int wid, int lane) {
-  constexpr int PER_WAVE = R / (8 * NW);
+  // pieces of 1 KB: contiguous per wave when they divide evenly, else strided (q = i * NW + wid, R = 160)
+  constexpr bool EVEN = R % (8 * NW) == 0;
+  constexpr int PER_WAVE = EVEN ? R / (8 * NW) : (R / 8 + NW - 1) / NW;
   const unsigned long long sb = (unsigned long long)tile_base;
   // readfirstlane returns int: go through `unsigned` so the low word is zero-extended (a sign-extended
   // low word with bit 31 set would OR 1s into the high word).
@@ -113,7 +114,8 @@ __device__ __forceinline__ void glds_tile(char* lds, const bf16_t* tile_base, lo
   const bf16_t* sbase = (const bf16_t*)(((unsigned long long)hi << 32) | lo);
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
-    const int q = wid * PER_WAVE + i;
+    const int q = EVEN ? wid * PER_WAVE + i : i * NW + wid;
+    if (!EVEN && q >= R / 8) break;  // wave-uniform
     uint32_t off;
     if (KMAJ) {
       const int row = q * 8 + (lane >> 3);
@@ -182,7 +184,10 @@ struct Geo {
   static constexpr int WR = TM / WGM, WC = TN / WGN;       // wave tile
   static constexpr int MI = WR / 16, NI = WC / 16;         // MFMA fragments per wave
   static constexpr int A_BYTES = TM * BK * 2, B_BYTES = TN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  static constexpr int EPI = NW * 64 * EPI_LD * 4;
+  // epilogue staging: SLAB fragments (16 * SLAB rows) per round, f32 rows of ELD floats (WC + 4: 68 for the
+  // 64-wide wave tiles, conflict-free for the column writes)
+  static constexpr int SLAB = MI < 4 ? MI : 4, ELD = WC + 4;
+  static constexpr int EPI = NW * 16 * SLAB * ELD * 4;
   static constexpr int LDS = 2 * STAGE > EPI ? 2 * STAGE : EPI;
 };
 
@@ -210,33 +215,34 @@ __device__ __forceinline__ void mma_tile(const char* la, floatx4 (&acc)[G::MI][G
 template <typename G>
 __device__ __forceinline__ void epilogue(const GemmArgs& g, floatx4 (&acc)[G::MI][G::NI], char* smem, int wid, int lane,
                                          int m0, int n0, int wm, int wn, int split) {
-  float* st = reinterpret_cast<float*>(smem) + wid * 64 * EPI_LD;
+  constexpr int SLAB = G::SLAB, ELD = G::ELD;
+  float* st = reinterpret_cast<float*>(smem) + wid * 16 * SLAB * ELD;
   const int colw = (lane & 15) * 4;
 #pragma unroll
-  for (int h = 0; h < G::MI / 4; ++h) {
+  for (int h = 0; h < G::MI / SLAB; ++h) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < SLAB; ++i)
 #pragma unroll
       for (int j = 0; j < G::NI; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          st[(i * 16 + (lane >> 4) * 4 + r) * EPI_LD + j * 16 + (lane & 15)] = acc[4 * h + i][j][r];
+          st[(i * 16 + (lane >> 4) * 4 + r) * ELD + j * 16 + (lane & 15)] = acc[SLAB * h + i][j][r];
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own-wave LDS writes retired
     __builtin_amdgcn_wave_barrier();
     for (int cb = 0; cb < G::WC; cb += 64) {
       const int col = n0 + wn * G::WC + cb + colw;
-      const bool col_ok = col < g.N;
+      const bool col_ok = cb + colw < G::WC && col < g.N;  // (an 80-wide wave tile: 16 columns in round 2)
       float bias4[4] = {0.f, 0.f, 0.f, 0.f};
       if (g.bias && col_ok) {
         const uint2 bv = *reinterpret_cast<const uint2*>(g.bias + col);
         bias4[0] = __uint_as_float(bv.x << 16); bias4[1] = __uint_as_float(bv.x & 0xffff0000u);
         bias4[2] = __uint_as_float(bv.y << 16); bias4[3] = __uint_as_float(bv.y & 0xffff0000u);
       }
-      for (int pass = 0; pass < 16; ++pass) {
+      for (int pass = 0; pass < 4 * SLAB; ++pass) {
         const int lr = pass * 4 + (lane >> 4);
-        const int row = m0 + wm * G::WR + h * 64 + lr;
+        const int row = m0 + wm * G::WR + h * 16 * SLAB + lr;
         if (row >= g.M || !col_ok) continue;
-        floatx4 v = *reinterpret_cast<const floatx4*>(st + lr * EPI_LD + cb + colw);
+        floatx4 v = *reinterpret_cast<const floatx4*>(st + lr * ELD + cb + colw);
         float o[4] = {v[0] * g.alpha + bias4[0], v[1] * g.alpha + bias4[1], v[2] * g.alpha + bias4[2],
                       v[3] * g.alpha + bias4[3]};
         if (g.act == ACT_SILU) {
@@ -1120,6 +1126,9 @@ int launch_geo(const GemmArgs& g, int splits, int geo, hipStream_t s) {
   if (AK && BK_ && geo == 2570) return launch_ring4<AK, BK_, 1>(g, splits, s);  // 4-wave, no DMA (wrong results)
   if (AK && BK_ && geo == 2571) return launch_ring4<AK, BK_, 3>(g, splits, s);  // 4-wave, no epilogue (wrong)
   if (geo == 2562) return launch<AK, BK_, 256, 256, 2, 4>(g, splits, s);  // 2-stage BK=64 T256 (A/B only)
+  // 128x160 tiles (M = 4096, N = 1280: 256 tiles, one per CU), k-major B only: 4 waves of 64x80 / 8 of 32x80
+  if (AK && BK_ && geo == 1601) return launch<AK, BK_, 128, 160, 2, 2>(g, splits, s);
+  if (AK && BK_ && geo == 1602) return launch<AK, BK_, 128, 160, 4, 2>(g, splits, s);
 #endif
   return launch<AK, BK_, 128, 128, 2, 2>(g, splits, s);
 }
@@ -1358,7 +1367,7 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
 #ifdef VPT_DIAG
 // ---- diagnostic build only (libvpt_hip_diag.so, include/vpt_hip_diag.h): process-wide switches ----
 extern "C" int vpt_gemm_set_geometry(int geo) {
-  VPT_CHECK_ARG(geo == 0 || geo == 128 || geo == 256 || (geo >= 2561 && geo <= 2573),
+  VPT_CHECK_ARG(geo == 0 || geo == 128 || geo == 256 || (geo >= 2561 && geo <= 2573) || geo == 1601 || geo == 1602,
                 "vpt_gemm_set_geometry: 0, 128, 256 or 2561-2573");
   g_geo_override = geo;
   return VPT_OK;
@@ -1722,12 +1731,17 @@ constexpr int LKP = LKC + 8;     // padded LDS row (bf16): conflict-free b128 ro
 // W = up [K][16]: each chunk transposed through the wave's LDS image.
 constexpr int LPD = 4;
 constexpr int LKS = 4;
-__global__ __launch_bounds__(64 * LKS) void lora_proj_kernel(const bf16_t* __restrict__ X, long ldx,
-                                                             const bf16_t* __restrict__ W, int w_kmajor,
+// Grouped (blockIdx.y = group gy): X + gy * xgoff, W + gy * wgoff, output columns 16 gy .. 16 gy + 15 -- the
+// q / k / v projections of one input (or of the three column blocks of one gradient) in one launch.
+__global__ __launch_bounds__(64 * LKS) void lora_proj_kernel(const bf16_t* __restrict__ X, long ldx, long xgoff,
+                                                             const bf16_t* __restrict__ W, int w_kmajor, long wgoff,
                                                              bf16_t* __restrict__ Y, long ldy, int M, int K, float alpha) {
   __shared__ __attribute__((aligned(16))) bf16_t wsa[LKS][16 * LKP];
   __shared__ __attribute__((aligned(16))) floatx4 red[LKS][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
+  X += blockIdx.y * xgoff;
+  W += blockIdx.y * wgoff;
+  Y += blockIdx.y * 16;
   bf16_t* ws = wsa[wid];
   const int row = blockIdx.x * 16 + j;
   const bf16_t* xr = X + (long)min(row, M - 1) * ldx + 8 * g;
@@ -1815,14 +1829,13 @@ struct LoraWgradJob {
 // gets column i of 4 rows), 128 rows per stage with the next stage's loads in flight in registers.
 constexpr int LXS = 72;  // X stage row stride (bf16): 64 columns + 16 B padding (spreads the tr reads' banks)
 constexpr int LSS = 24;  // S stage row stride (bf16): 16 columns + 16 B
-__global__ __launch_bounds__(256) void lora_wgrad_kernel(LoraWgradJob j0, LoraWgradJob j1, int M) {
-  const LoraWgradJob jb = blockIdx.z ? j1 : j0;
-  if ((int)blockIdx.x >= jb.N / 64 || (int)blockIdx.y >= jb.splits) return;
+// Column block bx (64 columns) of split `split` of one job.
+__device__ __forceinline__ void lora_wgrad_body(const LoraWgradJob& jb, int M, int bx, int split) {
   __shared__ __attribute__((aligned(16))) bf16_t xt[LMC * LXS];  // [m][n]
   __shared__ __attribute__((aligned(16))) bf16_t st[LMC * LSS];  // [m][j]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int n0 = blockIdx.x * 64;
-  const int mb = blockIdx.y * jb.mchunk, me = min(M, mb + jb.mchunk);
+  const int n0 = bx * 64;
+  const int mb = split * jb.mchunk, me = min(M, mb + jb.mchunk);
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
   const int mr = tid >> 3, c = tid & 7;   // X: rows mr + 32u (u = 0..3), 16-B chunk c of the 64 columns
   const int sm = tid >> 1, hh = tid & 1;  // S: row sm, 16-B half hh of the 16 columns
@@ -1855,9 +1868,32 @@ __global__ __launch_bounds__(256) void lora_wgrad_kernel(LoraWgradJob j0, LoraWg
     __syncthreads();
   }
   // D[n][j]: rows n = n0 + 16 wid + 4g + r, column j = lane & 15 -> part[split][n][j]
-  float* pp = jb.part + ((long)blockIdx.y * jb.N + n0 + wid * 16 + 4 * g) * 16 + (lane & 15);
+  float* pp = jb.part + ((long)split * jb.N + n0 + wid * 16 + 4 * g) * 16 + (lane & 15);
 #pragma unroll
   for (int r = 0; r < 4; ++r) pp[r * 16] = acc[r];
+}
+
+__global__ __launch_bounds__(256) void lora_wgrad_kernel(LoraWgradJob j0, LoraWgradJob j1, int M) {
+  const LoraWgradJob jb = blockIdx.z ? j1 : j0;
+  if ((int)blockIdx.x >= jb.N / 64 || (int)blockIdx.y >= jb.splits) return;
+  lora_wgrad_body(jb, M, blockIdx.x, blockIdx.y);
+}
+
+// The slab launches of many jobs (several LoRA targets' up and down gradients, each with its own M) as one
+// grid: job i owns the blocks [first[i], first[i + 1]), (N / 64) x splits of them, column block fastest.
+constexpr int kLoraWgJobs = 24;
+struct LoraWgBatch {
+  LoraWgradJob j[kLoraWgJobs];
+  int M[kLoraWgJobs];
+  int first[kLoraWgJobs + 1];
+  int njobs;
+};
+__global__ __launch_bounds__(256) void lora_wgrad_batch_kernel(LoraWgBatch b) {
+  const int blk = blockIdx.x;
+  int i = 0;
+  while (i + 1 < b.njobs && blk >= b.first[i + 1]) ++i;  // wave-uniform scan over <= 24 entries
+  const int local = blk - b.first[i], nbx = b.j[i].N / 64;
+  lora_wgrad_body(b.j[i], b.M[i], local % nbx, local / nbx);
 }
 
 // G (+)= alpha * (sum of the split slabs in split order): deterministic; blockIdx.y selects the job.
@@ -1900,7 +1936,19 @@ extern "C" int vpt_lora_proj(const void* X, long ldx, const void* W, int w_kmajo
   VPT_CHECK_ARG(r == 16, "vpt_lora_proj: rank 16 (the C5 configuration) only");
   VPT_CHECK_ARG(M > 0 && K > 0 && K % LKC == 0 && ldx % 8 == 0, "vpt_lora_proj: K % 128 == 0, 16-B leading dim");
   hipLaunchKernelGGL(lora_proj_kernel, dim3((M + 15) / 16), dim3(64 * LKS), 0, (hipStream_t)stream, (const bf16_t*)X, ldx,
-                     (const bf16_t*)W, w_kmajor, (bf16_t*)Y, ldy, M, K, alpha);
+                     0L, (const bf16_t*)W, w_kmajor, 0L, (bf16_t*)Y, ldy, M, K, alpha);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_lora_proj_grouped(const void* X, long ldx, long x_goff, const void* W, int w_kmajor, long w_goff,
+                                     void* Y, long ldy, int M, int K, int r, int G, float alpha, void* stream) {
+  VPT_CHECK_ARG(X && W && Y, "vpt_lora_proj_grouped: null pointer");
+  VPT_CHECK_ARG(r == 16 && G >= 1 && G <= 64, "vpt_lora_proj_grouped: rank 16, 1..64 groups");
+  VPT_CHECK_ARG(M > 0 && K > 0 && K % LKC == 0 && ldx % 8 == 0 && x_goff % 8 == 0 && w_goff % 8 == 0 && ldy >= 16 * G,
+                "vpt_lora_proj_grouped: K % 128 == 0, 16-B leading dim / group offsets, ldy >= 16 G");
+  hipLaunchKernelGGL(lora_proj_kernel, dim3((M + 15) / 16, G), dim3(64 * LKS), 0, (hipStream_t)stream,
+                     (const bf16_t*)X, ldx, x_goff, (const bf16_t*)W, w_kmajor, w_goff, (bf16_t*)Y, ldy, M, K, alpha);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
@@ -1968,6 +2016,26 @@ extern "C" int vpt_lora_wgrad2_partial(const void* dY, long lddy, const void* dS
   float* const placeholder = reinterpret_cast<float*>(ws_up);
   return lora_wgrad2_impl(dY, lddy, dS, ldds, placeholder, n_out, X, ldx, vS, ldvs, placeholder, n_in, M, 1, 1.f, ws_up,
                           ws_down, true, stream);
+}
+
+extern "C" int vpt_lora_wgrad_partial_batch(const VptLoraWgradJob* jobs, int njobs, void* stream) {
+  VPT_CHECK_ARG(jobs && njobs > 0 && njobs <= kLoraWgJobs, "vpt_lora_wgrad_partial_batch: 1..24 jobs");
+  LoraWgBatch b = {};
+  int total = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const VptLoraWgradJob& q = jobs[i];
+    VPT_CHECK_ARG(q.X && q.S && q.part && q.M > 0 && q.N > 0 && q.N % 64 == 0 && q.ldx % 8 == 0 && q.lds % 8 == 0,
+                  "vpt_lora_wgrad_partial_batch: bad job (widths % 64, 16-B leading dims)");
+    b.j[i] = lora_job(q.X, q.ldx, q.S, q.lds, nullptr, 0, q.M, q.N, q.part);
+    b.M[i] = q.M;
+    b.first[i] = total;
+    total += (q.N / 64) * b.j[i].splits;
+  }
+  b.first[njobs] = total;
+  b.njobs = njobs;
+  hipLaunchKernelGGL(lora_wgrad_batch_kernel, dim3(total), dim3(256), 0, (hipStream_t)stream, b);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
 }
 
 extern "C" int vpt_lora_wgrad_reduce_batch(const VptLoraReduceJob* jobs, int njobs, float alpha, int accumulate,

@@ -85,6 +85,8 @@ SIGNATURES: dict[str, list] = {
     "vpt_lora_wgrad_splits": [I, I],
     "vpt_lora_wgrad2_partial": [P, L, P, L, I, P, L, P, L, I, I, P, P, P],
     "vpt_lora_wgrad_reduce_batch": [P, I, F, I, P],
+    "vpt_lora_wgrad_partial_batch": [P, I, P],
+    "vpt_lora_proj_grouped": [P, L, L, P, I, L, P, L, I, I, I, I, F, P],
     "vpt_ema_update": [P, P, L, F, F, I, P],
     "vpt_gemm_nf4": [P, L, P, P, P, P, P, L, I, P, L, P, L, I, P, L, I, I, I, P, P, L, I, F, P],
     "vpt_nf4_quantize": [P, L, P, P, P, P, P, P, P],

@@ -828,6 +828,20 @@ def gemm_nf4(a, w, forward: bool, out, *, lora_a=None, lora_b=None, bias=None, r
     return out
 
 
+def lora_proj_grouped(x, x_goff: int, w, w_goff: int, G: int, w_kmajor: bool, out, alpha=1.0):
+    """out[:, 16g:16g+16] = alpha * X_g . W_g^T for g < G in one launch, X_g = the [M, K] view at x + g * x_goff and
+    W_g = the down [16, K] / up [K, 16] at w + g * w_goff (element offsets; csrc/gemm.hip lora_proj, grouped)."""
+    _chk(x, BF16, "x")
+    _chk(w, BF16, "w")
+    M = x.shape[0]
+    K = w.shape[1] if w_kmajor else w.shape[0]
+    if x.stride(1) != 1 or out.stride(1) != 1 or out.shape[1] < 16 * G:
+        raise ValueError("lora_proj_grouped: row-major x / out with 16 G output columns")
+    call("vpt_lora_proj_grouped", x.data_ptr(), x.stride(0), int(x_goff), w.data_ptr(), int(w_kmajor), int(w_goff),
+         out.data_ptr(), out.stride(0), M, K, 16, G, float(alpha), stream())
+    return out
+
+
 def lora_proj(x, w, w_kmajor: bool, out, alpha=1.0):
     """out[M, 16] = alpha * x[M, K] . W^T, W = down [16, K] (w_kmajor) or up [K, 16] (csrc/gemm.hip lora_proj)."""
     _chk(x, BF16, "x")
@@ -854,12 +868,22 @@ class _LoraReduceJob(ctypes.Structure):
                 ("trans", ctypes.c_int), ("reserved", ctypes.c_int)]
 
 
+class _LoraWgradJob(ctypes.Structure):
+    """VptLoraWgradJob (include/vpt_hip.h)."""
+    _fields_ = [("X", ctypes.c_void_p), ("ldx", ctypes.c_long), ("S", ctypes.c_void_p), ("lds", ctypes.c_long),
+                ("part", ctypes.c_void_p), ("N", ctypes.c_int), ("M", ctypes.c_int)]
+
+
 class _LoraBatch:
-    """Adapter-gradient reduces collected by lora_wgrad_batch(): one vpt_lora_wgrad_reduce_batch launch per
-    32 jobs (2 per LoRA target) instead of one reduce launch per target."""
+    """Adapter gradients collected by lora_wgrad_batch(): the slab products of every target deferred to the end of
+    the block and launched as one grid (vpt_lora_wgrad_partial_batch, up to 24 one-sided jobs), then one
+    vpt_lora_wgrad_reduce_batch launch per 32 jobs (2 per LoRA target) -- instead of two launches per target.
+    The operand tensors are held until the flush (their memory is not reused before the slab launch)."""
 
     def __init__(self):
         self.jobs: list = []
+        self.pjobs: list = []  # deferred slab jobs
+        self.keep: list = []   # their operand tensors
         self.key = None  # (alpha, accumulate) of the pending jobs
         self.nws = 0     # workspaces handed out since the last flush
 
@@ -878,7 +902,16 @@ class _LoraBatch:
         assert len(self.jobs) + len(jobs) <= 32
         self.jobs.extend(jobs)
 
+    def defer(self, pjobs, tensors):
+        self.pjobs.extend(pjobs)
+        self.keep.extend(tensors)
+
     def flush(self):
+        for i in range(0, len(self.pjobs), 24):
+            chunk = self.pjobs[i:i + 24]
+            arr = (_LoraWgradJob * len(chunk))(*chunk)
+            call("vpt_lora_wgrad_partial_batch", ctypes.addressof(arr), len(chunk), stream())
+        self.pjobs, self.keep = [], []
         if self.jobs:
             arr = (_LoraReduceJob * len(self.jobs))(*self.jobs)
             call("vpt_lora_wgrad_reduce_batch", ctypes.addressof(arr), len(self.jobs), float(self.key[0]),
@@ -887,6 +920,8 @@ class _LoraBatch:
 
 
 _LORA_BATCH: _LoraBatch | None = None
+# A/B knob: 0 = each target's slab launch at its call (round-2 behaviour); default: deferred to the block's end
+_LORA_DEFER = os.environ.get("VPT_LORA_DEFER", "1") != "0"
 
 
 @contextlib.contextmanager
@@ -925,8 +960,17 @@ def lora_wgrad2(dy, ds, g_up, x, vs, g_down, accumulate=True, alpha=1.0):
     b.reserve((float(alpha), int(accumulate)), 2)
     ws_up = b.ws(dy.device, int(lib.vpt_lora_wgrad_workspace(M, n_out)))
     ws_dn = b.ws(dy.device, int(lib.vpt_lora_wgrad_workspace(M, n_in)))
-    call("vpt_lora_wgrad2_partial", dy.data_ptr(), dy.stride(0), ds.data_ptr(), ds.stride(0), n_out, x.data_ptr(),
-         x.stride(0), vs.data_ptr(), vs.stride(0), n_in, M, ws_up.data_ptr(), ws_dn.data_ptr(), stream())
+    if _LORA_DEFER:
+        for t in (dy, ds, x, vs):
+            if t.stride(1) != 1 or t.stride(0) % 8:
+                raise ValueError("lora_wgrad2: row-major operands with 16-B leading dims")
+        b.defer([_LoraWgradJob(dy.data_ptr(), dy.stride(0), ds.data_ptr(), ds.stride(0), ws_up.data_ptr(), n_out, M),
+                 _LoraWgradJob(x.data_ptr(), x.stride(0), vs.data_ptr(), vs.stride(0), ws_dn.data_ptr(), n_in, M)],
+                (dy, ds, x, vs))
+    else:
+        call("vpt_lora_wgrad2_partial", dy.data_ptr(), dy.stride(0), ds.data_ptr(), ds.stride(0), n_out,
+             x.data_ptr(), x.stride(0), vs.data_ptr(), vs.stride(0), n_in, M, ws_up.data_ptr(), ws_dn.data_ptr(),
+             stream())
     b.add([_LoraReduceJob(ws_up.data_ptr(), g_up.data_ptr(), n_out, call("vpt_lora_wgrad_splits", M, n_out), 0, 0),
            _LoraReduceJob(ws_dn.data_ptr(), g_down.data_ptr(), n_in, call("vpt_lora_wgrad_splits", M, n_in), 1, 0)])
 

@@ -230,21 +230,30 @@ class LoRALinearNF4:
         dx_lora = ops.linear_dgrad(vs, self.down)
         return ops.linear_dgrad(dy, self.weight(), resid=dx_lora, out=dx)
 
-    def backward_adapters(self, dy: torch.Tensor, vs_out: torch.Tensor | None = None) -> torch.Tensor:
+    def backward_adapters(self, dy: torch.Tensor, vs_out: torch.Tensor | None = None,
+                          vs_ready: bool = False) -> torch.Tensor:
         """The adapter half of the backward: g_up += dy^T . ds, vs = bf16(s * dy . up), g_down += vs^T . x;
-        returns vs (into vs_out when given: a column block of a fused q|k|v gradient's LoRA operand)."""
+        returns vs (into vs_out when given: a column block of a fused q|k|v gradient's LoRA operand; vs_ready: the
+        caller already wrote vs there, ops.lora_proj_grouped)."""
         x, ds = self._saved
         M = x.shape[0]
         r = self.down.shape[0]
         vs = torch.empty(M, r, dtype=BF16, device=dy.device) if vs_out is None else vs_out
         if self.skinny:
-            ops.lora_proj(dy, self.up, False, vs, alpha=self.scale)
+            if not vs_ready:
+                ops.lora_proj(dy, self.up, False, vs, alpha=self.scale)
             ops.lora_wgrad2(dy, ds, self.g_up, x, vs, self.g_down)
         else:
             ops.linear_wgrad(dy, ds, self.g_up, accumulate=True, splits=ops.wgrad_splits(*self.up.shape, M))
             ops.gemm(dy, True, self.up, False, M, r, self.up.shape[0], vs, alpha=self.scale)
             ops.linear_wgrad(vs, x, self.g_down, accumulate=True, splits=ops.wgrad_splits(*self.down.shape, M))
         return vs
+
+
+def _adjacent(ts) -> bool:
+    """Contiguous tensors laid out back to back (the flat adapter layout of SDXLStacksQLoRA)."""
+    return all(t.is_contiguous() for t in ts) and all(
+        ts[i].data_ptr() + ts[i].numel() * ts[i].element_size() == ts[i + 1].data_ptr() for i in range(len(ts) - 1))
 
 
 TARGETS = ["attn1.to_q", "attn1.to_k", "attn1.to_v", "attn1.to_out.0", "attn2.to_q", "attn2.to_k", "attn2.to_v",
@@ -304,9 +313,14 @@ class SDXLTransformerBlock:
         M, D, L = h1.shape[0], self.inner, self.lin
         r = L[QKV[0]].down.shape[0]
         ds = torch.empty(M, 3 * r, dtype=BF16, device=h1.device)
+        downs = [L[t].down for t in QKV]
+        grouped = _adjacent(downs) and len({L[t].scale for t in QKV}) == 1
+        if grouped:  # the flat layout: ds_q | ds_k | ds_v in one launch
+            ops.lora_proj_grouped(h1, 0, downs[0], downs[0].numel(), 3, True, ds, alpha=L[QKV[0]].scale)
         for g, t in enumerate(QKV):
             dsg = ds[:, g * r:(g + 1) * r]
-            ops.lora_proj(h1, L[t].down, True, dsg, alpha=L[t].scale)
+            if not grouped:
+                ops.lora_proj(h1, L[t].down, True, dsg, alpha=L[t].scale)
             L[t]._saved = (h1, dsg) if save else None
         qkv = torch.empty(M, 3 * D, dtype=BF16, device=h1.device)
         ops.gemm_lora_grouped(h1, Wqkv, ds, [L[t].up for t in QKV], qkv)
@@ -321,11 +335,14 @@ class SDXLTransformerBlock:
         M, D, L = dqkv.shape[0], self.inner, self.lin
         r = L[QKV[0]].down.shape[0]
         vs = torch.empty(M, 3 * r, dtype=BF16, device=dqkv.device)
+        ups = [L[t].up for t in QKV]
+        grouped = _adjacent(ups) and len({L[t].scale for t in QKV}) == 1
+        if grouped:  # vs_q | vs_k | vs_v = s * [dq | dk | dv] . blockdiag(up_q, up_k, up_v), one launch
+            ops.lora_proj_grouped(dqkv, D, ups[0], ups[0].numel(), 3, False, vs, alpha=L[QKV[0]].scale)
         for g, t in enumerate(QKV):
-            L[t].backward_adapters(dqkv[:, g * D:(g + 1) * D], vs_out=vs[:, g * r:(g + 1) * r])
+            L[t].backward_adapters(dqkv[:, g * D:(g + 1) * D], vs_out=vs[:, g * r:(g + 1) * r], vs_ready=grouped)
         downs = [L[t].down for t in QKV]
-        if all(d.is_contiguous() for d in downs) and all(
-                downs[i].data_ptr() + downs[i].numel() * 2 == downs[i + 1].data_ptr() for i in range(2)):
+        if _adjacent(downs):
             stacked = torch.as_strided(downs[0], (3 * r, D), (D, 1))  # the flat layout keeps them side by side
         else:
             stacked = torch.cat(downs, 0)  # standalone blocks: a copy of 3 x [r, dim]
