@@ -236,6 +236,12 @@ int vpt_sf_init(const void* y, float* z, float* v, long n, void* stream);
  * backward dx = dres + LN'(dy), per-block dw/db partials [vpt_layernorm_bwd_blocks(M)][D]. D <= 2048. */
 int vpt_layernorm_fwd(const void* x, long ldx, const void* w, const void* b, void* y, long ldy, float* mean,
                       float* rstd, int M, int D, float eps, void* stream);
+/* LayerNorm (as vpt_layernorm_fwd, bit-identical y / mean / rstd) and, in the same launch, the rank-16 LoRA
+ * down-projections of its output: ds[m][16 g + j] = bf16(alpha * y[m] . down_g[j]) for g < G (<= 3), down_g =
+ * down + g * w_goff ([16][D] each) -- bit-identical to vpt_lora_proj(_grouped) on y. D % 128 == 0. */
+int vpt_layernorm_lora_fwd(const void* x, long ldx, const void* w, const void* b, void* y, long ldy, float* mean,
+                           float* rstd, int M, int D, float eps, const void* down, long w_goff, int G, void* ds,
+                           long ldds, float alpha, void* stream);
 int vpt_layernorm_bwd_blocks(int M);
 int vpt_layernorm_bwd(const void* dy, long lddy, const void* x, long ldx, const float* mean, const float* rstd,
                       const void* w, const void* dres, long ldr, void* dx, long lddx, float* dw_part, float* db_part,

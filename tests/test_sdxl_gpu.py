@@ -567,3 +567,42 @@ def test_lora_wgrad_deferred_batch_matches_immediate(ops, monkeypatch):
         assert torch.equal(a_u, b_u) and torch.equal(a_d, b_d), shapes[i]
     dy, ds, x, vs = ops_in[1]
     assert rel(res[0][1][0], 0.5 + 0.0625 * dy.float().t() @ ds.float()) < 1e-5
+
+
+@pytest.mark.parametrize("M,D,G", [(4100, 1280, 3), (1000, 640, 1), (77, 1280, 1)])
+def test_layernorm_lora_fwd_bit_exact(ops, M, D, G):
+    """vpt_layernorm_lora_fwd: y / mean / rstd bit-identical to vpt_layernorm_fwd and ds to vpt_lora_proj(_grouped) on
+    that y (the separate launches it replaces), M not a multiple of the kernel's 16 rows."""
+    x = rnd(M, D, seed=140)
+    w, b = rnd(D, scale=0.5, seed=141) + 1.0, rnd(D, scale=0.1, seed=142)
+    w = w.to(torch.bfloat16)
+    down = rnd(16 * G, D, scale=0.05, seed=143)
+    ds = torch.empty(M, 16 * G, dtype=torch.bfloat16, device=DEV)
+    y, m, r = ops.layernorm_lora_fwd(x, w, b, down, G, 0.0625, ds)
+    y0, m0, r0 = ops.layernorm_fwd(x, w, b)
+    assert torch.equal(y, y0) and torch.equal(m, m0) and torch.equal(r, r0)
+    ref = torch.empty(M, 16 * G, dtype=torch.bfloat16, device=DEV)
+    ops.lora_proj_grouped(y0, 0, down[:16], 16 * D, G, True, ref, alpha=0.0625)
+    assert torch.equal(ds, ref)
+
+
+def test_sdxl_block_fused_ln_lora_bitwise(ops, monkeypatch):
+    """The blocks with their LayerNorms fused to the LoRA down-projections (norm1 -> q|k|v, norm2 -> attn2.to_q,
+    norm3 -> ff.net.0.proj) give a step bit-identical to the unfused one: context gradient and every adapter
+    gradient (flat adapter layout of SDXLStacksQLoRA, where the q|k|v downs are adjacent), both widths."""
+    from vpt import sdxl
+    from vpt.sdxl_train import SDXLStacksQLoRA
+    res = []
+    for fused in (True, False):
+        monkeypatch.setattr(sdxl, "FUSED_LN_LORA", fused)
+        m = SDXLStacksQLoRA(B=2, stacks=[("a", 640, 10, 1, 16), ("b", 1280, 20, 1, 8)], n_ctx=77, seed=3)
+        g = torch.Generator(device=DEV).manual_seed(9)
+        with torch.no_grad():
+            m.params.copy_((torch.randn(m.params.shape, device=DEV, generator=g) * 0.03).bfloat16())
+        xs, ctx, gs = m.make_inputs(seed=4)
+        m.opt.step = lambda: None  # compare gradients, not the update
+        dctx = m.step(xs, ctx, gs)
+        torch.cuda.synchronize()
+        res.append((dctx.clone(), m.grads.clone()))
+    (c0, g0), (c1, g1) = res
+    assert torch.equal(c0, c1) and torch.equal(g0, g1)

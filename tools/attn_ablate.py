@@ -30,6 +30,10 @@ def timeit(fn, iters=10):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--vars", default="0,4,5,6,7,8", help="vpt_attn_set_variant values (diag dispatcher)")
+    args = ap.parse_args()
     dev = "cuda"
     B, H, n = 8, 12, 4170
     rows, D = n, 768
@@ -48,15 +52,16 @@ def main():
     ops.attn_fwd(q4, k4, v4, o4, lse, kb, B, H, rows, n, n_dense)
     res = {}
     for r in range(3):
-        for var in (0, 4, 5, 6, 7, 8):
+        for var in [int(v) for v in args.vars.split(",")]:
             ops.lib.vpt_attn_set_variant(var)
             ms = timeit(lambda: ops.attn_bwd(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, kb,
                                              *(ops._t4(t, B, rows, H) for t in gr), B, H, rows, n, n_dense))
             res.setdefault(var, []).append(ms)
     ops.lib.vpt_attn_set_variant(0)
-    names = {0: "production", 4: "no_exp2", 5: "quarter_dvdk_mfma", 6: "no_tr_lds_reads", 7: "no_row_lds_reads",
-             8: "compiler_scheduled"}
-    print(json.dumps({names[k]: round(sorted(v)[1], 4) for k, v in res.items()}, indent=1))
+    # current diag dispatcher (diag_attn_bwd_variants): 0 production one-launch; split pair: 7 compiler-scheduled
+    # dK/dV (correct), 1 no next-tile staging in either loop (wrong), 2 row reads for the transposes (wrong),
+    # 3-6 dK/dV ablations (wrong)
+    print(json.dumps({f"variant{k}": round(sorted(v)[1], 4) for k, v in res.items()}, indent=1))
 
 
 if __name__ == "__main__":

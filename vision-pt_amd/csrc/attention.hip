@@ -708,21 +708,30 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
 // then the dQ blocks. Each kind alone is 3,168 equal blocks at B=8 1024^2 on 512 block slots (2 per CU):
 // 6.19 waves of work run as 7, twice. In one grid the dQ blocks start on the slots the dK/dV tail frees,
 // so the pair runs in ~(work of both) / slots instead of two rounded-up launches.
-template <int DQ>
+// DKDV: the dK/dV body (8 = explicitly ordered, 0 = compiler-scheduled). ORDER 1 (diagnostic A/B): per (batch,
+// head) its nkb dK/dV blocks then its nqb dQ blocks, heads in sequence (a head's Q / dO / K / V shared in time).
+template <int DQ, int DKDV = 8, int ORDER = 0>
 __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs g, int nkb, int nqb, int B) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][8192];
   __shared__ __attribute__((aligned(16))) float lstat[2][2][64];
   extern __shared__ __attribute__((aligned(16))) float kbl[];
-  const int nk_blocks = nkb * g.H * B;
   int bid = blockIdx.x;
-  if (bid < nk_blocks) {
-    const int bx = bid % nkb, r = bid / nkb;
-    dkdv_body<8, 4>(g, bx, r % g.H, r / g.H, lds, lstat);
+  bool kv;
+  int bx, r;
+  if (ORDER == 1) {
+    r = bid / (nkb + nqb);
+    const int j = bid - r * (nkb + nqb);
+    kv = j < nkb;
+    bx = kv ? j : j - nkb;
   } else {
-    bid -= nk_blocks;
-    const int bx = bid % nqb, r = bid / nqb;
-    dq_body<DQ, 4>(g, bx, r % g.H, r / g.H, lds, kbl);
+    const int nk_blocks = nkb * g.H * B;
+    kv = bid < nk_blocks;
+    if (!kv) bid -= nk_blocks;
+    bx = kv ? bid % nkb : bid % nqb;
+    r = kv ? bid / nkb : bid / nqb;
   }
+  if (kv) dkdv_body<DKDV, 4>(g, bx, r % g.H, r / g.H, lds, lstat);
+  else dq_body<DQ, 4>(g, bx, r % g.H, r / g.H, lds, kbl);
 }
 constexpr int kDqBody = 0;  // production dQ body (0 = compiler-scheduled, 8 = explicitly ordered)
 
@@ -828,6 +837,17 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
   if (g_rows64 & 32) {  // A/B: the software-pipelined dK/dV kernel (diag include), then the one-launch kernel's dQ blocks
     if (const int rc = diag_attn_bwd_pipe(g, nkb, H, B, s); rc != VPT_OK) return rc;
     hipLaunchKernelGGL((attn_bwd_kernel<kDqBody>), dim3(nqb * H * B), dim3(256), key_bias_lds_bytes(g), s, g, 0, nqb, B);
+    VPT_LAUNCH_CHECK();
+    return VPT_OK;
+  }
+  if (g_rows64 & (64 | 128)) {  // A/B: compiler-scheduled dK/dV body (64) / head-interleaved block order (128)
+    const dim3 grid((nkb + nqb) * H * B);
+    if ((g_rows64 & 192) == 64)
+      hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, 0, 0>), grid, dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
+    else if ((g_rows64 & 192) == 128)
+      hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, 8, 1>), grid, dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
+    else
+      hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, 0, 1>), grid, dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
     VPT_LAUNCH_CHECK();
     return VPT_OK;
   }

@@ -63,6 +63,131 @@ __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const bf16_t* __rest
   }
 }
 
+// LayerNorm + the LoRA down-projections of its output (the q|k|v adapters of norm1's output, attn2.to_q's of
+// norm2's, ff.net.0.proj's of norm3's): ds[m][16 gi + j] = bf16(alpha * y[m] . down_gi[j]) for gi < G, written
+// by the same launch that writes y -- the separate vpt_lora_proj launch (one per use, ~8 us) gone. Each block
+// owns 16 rows: every wave normalises 4 rows exactly as layernorm_fwd_kernel (same arithmetic) into y and into an
+// LDS image of the 16 bf16 rows; then the projection runs in lora_proj's order (csrc/gemm.hip lora_proj_kernel,
+// w_kmajor: wave w takes the 128-wide K chunks w, w + 4, ..., four 16x16x32 MFMAs per chunk; the waves' sums
+// added in wave order), so ds is bit-identical to layernorm_fwd + vpt_lora_proj(_grouped).
+constexpr int LNL_KC = 128;  // K chunk (lora_proj's LKC)
+constexpr int LNL_MAXG = 3;
+__global__ __launch_bounds__(256) void layernorm_lora_fwd_kernel(const bf16_t* __restrict__ x, long ldx,
+                                                                 const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
+                                                                 bf16_t* __restrict__ y, long ldy, float* __restrict__ mean_out,
+                                                                 float* __restrict__ rstd_out, int M, int D, float eps,
+                                                                 const bf16_t* __restrict__ down, long w_goff, int G,
+                                                                 bf16_t* __restrict__ ds, long ldds, float alpha) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t lnl_tile[];  // [16][D + 8]
+  __shared__ __attribute__((aligned(16))) floatx4 red[4][LNL_MAXG][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g4 = lane >> 4, j = lane & 15;
+  const int TS = D + 8;  // padded row (bf16): 16-B offset per row spreads the fragment reads over the banks
+  const int nch = D >> 3;
+  const long row0 = (long)blockIdx.x * 16;
+  // the wave's 4 rows loaded up front (one memory latency for all of them), then normalised one by one
+  uint4 raw[4][MAXC];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const long row = row0 + wid * 4 + rr;
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = lane + 64 * i;
+      raw[rr][i] = row < M && c < nch ? *reinterpret_cast<const uint4*>(x + row * ldx + c * 8) : make_uint4(0, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int lr = wid * 4 + rr;  // tile row
+    const long row = row0 + lr;
+    bf16_t* trow = lnl_tile + lr * TS;
+    if (row >= M) {  // past the end: zeros (their projections are never stored)
+      for (int c = lane; c < nch; c += 64) *reinterpret_cast<uint4*>(trow + c * 8) = make_uint4(0, 0, 0, 0);
+      continue;
+    }
+    float f[MAXC][8];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        unpack8(raw[rr][i], f[i]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += f[i][e];
+      }
+    }
+    const float mean = wave_sum(s) / (float)D;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      if (lane + 64 * i < nch) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = f[i][e] - mean;
+          ss += d * d;
+        }
+      }
+    }
+    const float r = rsqrtf(wave_sum(ss) / (float)D + eps);
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        float wf[8], bf[8], o[8];
+        unpack8(*reinterpret_cast<const uint4*>(w + c * 8), wf);
+        unpack8(*reinterpret_cast<const uint4*>(b + c * 8), bf);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (f[i][e] - mean) * r * wf[e] + bf[e];
+        const uint4 pk = pack8(o);
+        *reinterpret_cast<uint4*>(y + row * ldy + c * 8) = pk;
+        *reinterpret_cast<uint4*>(trow + c * 8) = pk;
+      }
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = r;
+    }
+  }
+  __syncthreads();
+  // projections: wave wid takes K chunks wid, wid + 4, ... (<= 4 of them: D <= 2048)
+  const int nkc = D / LNL_KC;
+  const int ncw = (nkc - wid + 3) / 4;
+  for (int gi = 0; gi < G; ++gi) {
+    const bf16_t* wr = down + gi * w_goff + (long)j * D + 8 * g4;  // down_gi row j
+    uint4 wb[4][LNL_KC / 32];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (u < ncw)
+#pragma unroll
+        for (int s2 = 0; s2 < LNL_KC / 32; ++s2)
+          wb[u][s2] = *reinterpret_cast<const uint4*>(wr + (wid + 4 * u) * LNL_KC + 32 * s2);
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (u < ncw) {
+        const int c = wid + 4 * u;
+#pragma unroll
+        for (int s2 = 0; s2 < LNL_KC / 32; ++s2) {
+          const uint4 xa = *reinterpret_cast<const uint4*>(lnl_tile + j * TS + c * LNL_KC + 32 * s2 + 8 * g4);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(xa), as_frag(wb[u][s2]), acc, 0, 0, 0);
+        }
+      }
+    red[wid][gi][lane] = acc;
+  }
+  __syncthreads();
+  if (wid != 0) return;
+  for (int gi = 0; gi < G; ++gi) {
+    floatx4 acc = red[0][gi][lane];
+#pragma unroll
+    for (int w2 = 1; w2 < 4; ++w2) acc += red[w2][gi][lane];
+    // D[m][j]: lane holds rows 4 g4 .. 4 g4 + 3 of the 16, column j
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long m = row0 + 4 * g4 + r;
+      if (m < M) ds[m * ldds + 16 * gi + j] = f2bf(acc[r] * alpha);
+    }
+  }
+}
+
 // dx = dres + rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * w; per-block partials of
 // dw = sum dy * xhat and db = sum dy (reduced by vpt_reduce_rows).
 __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16_t* __restrict__ dy, long lddy,
@@ -468,6 +593,22 @@ extern "C" int vpt_layernorm_fwd(const void* x, long ldx, const void* w, const v
   if (M == 0) return VPT_OK;
   hipLaunchKernelGGL(layernorm_fwd_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
                      ldx, (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y, ldy, mean, rstd, M, D, eps);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_layernorm_lora_fwd(const void* x, long ldx, const void* w, const void* b, void* y, long ldy,
+                                      float* mean, float* rstd, int M, int D, float eps, const void* down, long w_goff,
+                                      int G, void* ds, long ldds, float alpha, void* stream) {
+  VPT_CHECK_ARG(x && w && b && y && mean && rstd && down && ds, "vpt_layernorm_lora_fwd: null pointer");
+  VPT_CHECK_ARG(D % LNL_KC == 0 && D <= 2048 && M >= 0 && ldx % 8 == 0 && ldy % 8 == 0,
+                "vpt_layernorm_lora_fwd: D % 128 == 0, D <= 2048, 16-B leading dims");
+  VPT_CHECK_ARG(G >= 1 && G <= LNL_MAXG && ldds >= 16 * G && w_goff % 8 == 0, "vpt_layernorm_lora_fwd: 1..3 groups");
+  if (M == 0) return VPT_OK;
+  const size_t lds = (size_t)16 * (D + 8) * sizeof(bf16_t);
+  hipLaunchKernelGGL(layernorm_lora_fwd_kernel, dim3((M + 15) / 16), dim3(256), lds, (hipStream_t)stream,
+                     (const bf16_t*)x, ldx, (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y, ldy, mean, rstd, M, D, eps,
+                     (const bf16_t*)down, w_goff, G, (bf16_t*)ds, ldds, alpha);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

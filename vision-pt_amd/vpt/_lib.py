@@ -67,6 +67,7 @@ SIGNATURES: dict[str, list] = {
     "vpt_copy_rows": [P, L, I, I, I, P, L, I, I, I, P],
     "vpt_silu": [P, P, P, L, I, P],
     "vpt_layernorm_fwd": [P, L, P, P, P, L, P, P, I, I, F, P],
+    "vpt_layernorm_lora_fwd": [P, L, P, P, P, L, P, P, I, I, F, P, L, I, P, L, F, P],
     "vpt_layernorm_bwd_blocks": [I],
     "vpt_layernorm_bwd": [P, L, P, L, P, P, P, P, L, P, L, P, P, I, I, P],
     "vpt_geglu_fwd": [P, L, I, L, P, P],

@@ -652,6 +652,22 @@ def layernorm_fwd(x, w, b, out=None, mean=None, rstd=None, eps=1e-5):
     return out, mean, rstd
 
 
+def layernorm_lora_fwd(x, w, b, down, G: int, alpha: float, ds, eps=1e-5):
+    """layernorm_fwd and, in the same launch, ds[:, 16g:16g+16] = bf16(alpha * y . down_g^T) for g < G, down_g the
+    g-th [16, D] block of `down` (the flat layout's adjacent downs; csrc/sdxl.hip layernorm_lora_fwd_kernel)."""
+    M, D = x.shape
+    _chk(down, BF16, "down")
+    if down.stride(-1) != 1 or ds.stride(1) != 1 or ds.shape[1] < 16 * G:
+        raise ValueError("layernorm_lora_fwd: row-major down / ds with 16 G columns")
+    out = torch.empty(M, D, dtype=BF16, device=x.device)
+    mean = torch.empty(M, dtype=F32, device=x.device)
+    rstd = torch.empty(M, dtype=F32, device=x.device)
+    call("vpt_layernorm_lora_fwd", x.data_ptr(), x.stride(0), w.data_ptr(), b.data_ptr(), out.data_ptr(), out.stride(0),
+         mean.data_ptr(), rstd.data_ptr(), M, D, eps, down.data_ptr(), 16 * D, G, ds.data_ptr(), ds.stride(0),
+         float(alpha), stream())
+    return out, mean, rstd
+
+
 def layernorm_bwd(dy, x, mean, rstd, w, dres=None, dx=None, dw_part=None, db_part=None):
     """dx = dres + LayerNorm'(dy); optional per-block dw/db partials [layernorm_bwd_blocks(M), D]."""
     M, D = x.shape

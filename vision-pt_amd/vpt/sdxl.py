@@ -188,15 +188,20 @@ class LoRALinearNF4:
         return self.base.dequantize(torch.empty(self.base.shape, dtype=BF16, device=self.down.device))
 
     def forward(self, x: torch.Tensor, save: bool = True, out: torch.Tensor | None = None,
-                resid: torch.Tensor | None = None, W: torch.Tensor | None = None) -> torch.Tensor:
+                resid: torch.Tensor | None = None, W: torch.Tensor | None = None,
+                ds: torch.Tensor | None = None) -> torch.Tensor:
         """resid: a bf16 tensor added in the epilogue (the block's residual stream: bf16(resid + bf16(y))).
-        W: the base already dequantised by the caller (dequant_bases), else this call dequantises it."""
+        W: the base already dequantised by the caller (dequant_bases), else this call dequantises it.
+        ds: s * x . down^T already computed by the caller (the fused LayerNorm, ops.layernorm_lora_fwd)."""
         M = x.shape[0]
         r = self.down.shape[0]
-        ds = torch.empty(M, r, dtype=BF16, device=x.device)
-        if self.skinny:
+        if ds is not None:
+            pass
+        elif self.skinny:
+            ds = torch.empty(M, r, dtype=BF16, device=x.device)
             ops.lora_proj(x, self.down, True, ds, alpha=self.scale)
         else:
+            ds = torch.empty(M, r, dtype=BF16, device=x.device)
             ops.gemm(x, True, self.down, True, M, r, x.shape[1], ds, alpha=self.scale)
         y = out if out is not None else torch.empty(M, self.base.shape[0], dtype=BF16, device=x.device)
         if self.fused and self.base_mode != "inline":
@@ -213,10 +218,12 @@ class LoRALinearNF4:
         self._saved = (x, ds) if save else None
         return y
 
-    def backward(self, dy: torch.Tensor, need_dx: bool = True, W: torch.Tensor | None = None) -> torch.Tensor | None:
+    def backward(self, dy: torch.Tensor, need_dx: bool = True, W: torch.Tensor | None = None,
+                 vs: torch.Tensor | None = None) -> torch.Tensor | None:
         """Accumulates g_up, g_down; returns dx (bf16), or None with need_dx=False (an input that needs no
-        gradient, e.g. the frozen text encoder's hidden states under attn2.to_k / to_v)."""
-        vs = self.backward_adapters(dy)
+        gradient, e.g. the frozen text encoder's hidden states under attn2.to_k / to_v). vs: s * dy . up already
+        computed by the caller (ops.lora_proj_grouped over adjacent targets)."""
+        vs = self.backward_adapters(dy, vs_out=vs, vs_ready=vs is not None)
         if not need_dx:
             return None
         x = self._saved[0]
@@ -248,6 +255,10 @@ class LoRALinearNF4:
             ops.gemm(dy, True, self.up, False, M, r, self.up.shape[0], vs, alpha=self.scale)
             ops.linear_wgrad(vs, x, self.g_down, accumulate=True, splits=ops.wgrad_splits(*self.down.shape, M))
         return vs
+
+
+# A/B knob: 0 = LayerNorm and the LoRA down-projections of its output as separate launches
+FUSED_LN_LORA = os.environ.get("VPT_LN_LORA", "1") != "0"
 
 
 def _adjacent(ts) -> bool:
@@ -306,17 +317,34 @@ class SDXLTransformerBlock:
         (dequant_bases) and their adapters take the rank-16 skinny kernels."""
         return "attn1.qkv" in Wb and all(self.lin[t].skinny for t in QKV)
 
-    def _qkv_fwd(self, h1, Wqkv, save):
+    def _ln_lora(self, x, norm: str, targets) -> tuple:
+        """LayerNorm `norm` of x and the LoRA down-projections of its output for `targets` (adjacent downs, one
+        scale, rank-16 skinny) in one launch (ops.layernorm_lora_fwd): (y, mean, rstd, ds [M, 16 len(targets)]);
+        ds None where the fused form does not apply (the projections then run in LoRALinearNF4.forward)."""
+        L = self.lin
+        downs = [L[t].down for t in targets]
+        if FUSED_LN_LORA and all(L[t].skinny for t in targets) and _adjacent(downs) \
+                and len({L[t].scale for t in targets}) == 1 and x.shape[1] % 128 == 0:
+            ds = torch.empty(x.shape[0], 16 * len(targets), dtype=BF16, device=x.device)
+            y, m, r = ops.layernorm_lora_fwd(x, *self.norm[norm], downs[0], len(targets), L[targets[0]].scale, ds)
+            return y, m, r, ds
+        return (*ops.layernorm_fwd(x, *self.norm[norm]), None)
+
+    def _qkv_fwd(self, h1, Wqkv, save, ds=None):
         """q|k|v = h1 . [Wq; Wk; Wv]^T + [ds_q | ds_k | ds_v] . blockdiag(up_q, up_k, up_v)^T as ONE GEMM
         (vpt_gemm_bf16_lora_grouped; each output column block is exactly its target's LoRALinear), then q pre-scaled
         in place for the attention kernels. Returns column views (q, k, v) of the [M, 3 dim] output."""
         M, D, L = h1.shape[0], self.inner, self.lin
         r = L[QKV[0]].down.shape[0]
-        ds = torch.empty(M, 3 * r, dtype=BF16, device=h1.device)
         downs = [L[t].down for t in QKV]
         grouped = _adjacent(downs) and len({L[t].scale for t in QKV}) == 1
-        if grouped:  # the flat layout: ds_q | ds_k | ds_v in one launch
+        if ds is not None:  # computed with the LayerNorm (ops.layernorm_lora_fwd)
+            grouped = True
+        elif grouped:  # the flat layout: ds_q | ds_k | ds_v in one launch
+            ds = torch.empty(M, 3 * r, dtype=BF16, device=h1.device)
             ops.lora_proj_grouped(h1, 0, downs[0], downs[0].numel(), 3, True, ds, alpha=L[QKV[0]].scale)
+        else:
+            ds = torch.empty(M, 3 * r, dtype=BF16, device=h1.device)
         for g, t in enumerate(QKV):
             dsg = ds[:, g * r:(g + 1) * r]
             if not grouped:
@@ -366,16 +394,17 @@ class SDXLTransformerBlock:
         # the block's bases, one launch (the cross-attention k / v ones only when not projected already)
         Wb = dequant_bases(L, TARGETS if kv is None else [t for t in TARGETS if t not in ("attn2.to_k", "attn2.to_v")],
                            self.device)
-        h1, m1, r1 = ops.layernorm_fwd(x, *self.norm["norm1"])
         if self._fuse_qkv(Wb):
-            q, k, v = self._qkv_fwd(h1, Wb["attn1.qkv"], save)
+            h1, m1, r1, ds1 = self._ln_lora(x, "norm1", QKV)
+            q, k, v = self._qkv_fwd(h1, Wb["attn1.qkv"], save, ds=ds1)
         else:
+            h1, m1, r1 = ops.layernorm_fwd(x, *self.norm["norm1"])
             q, k, v = (L[f"attn1.to_{c}"].forward(h1, save, W=Wb.get(f"attn1.to_{c}")) for c in "qkv")
             q = self._qs(q)
         o1, lse1 = self._attn_fwd(q, k, v, B, n, n)
         x1 = L["attn1.to_out.0"].forward(o1, save, resid=x, W=Wb.get("attn1.to_out.0"))
-        h2, m2, r2 = ops.layernorm_fwd(x1, *self.norm["norm2"])
-        q2 = self._qs(L["attn2.to_q"].forward(h2, save, W=Wb.get("attn2.to_q")))
+        h2, m2, r2, ds2 = self._ln_lora(x1, "norm2", ["attn2.to_q"])
+        q2 = self._qs(L["attn2.to_q"].forward(h2, save, W=Wb.get("attn2.to_q"), ds=ds2))
         if kv is not None:
             k2, v2 = kv
         else:
@@ -383,8 +412,8 @@ class SDXLTransformerBlock:
             v2 = L["attn2.to_v"].forward(ctx, save, W=Wb.get("attn2.to_v"))
         o2, lse2 = self._attn_fwd(q2, k2, v2, B, n, nc)
         x2 = L["attn2.to_out.0"].forward(o2, save, resid=x1, W=Wb.get("attn2.to_out.0"))
-        h3, m3, r3 = ops.layernorm_fwd(x2, *self.norm["norm3"])
-        x12 = L["ff.net.0.proj"].forward(h3, save, W=Wb.get("ff.net.0.proj"))
+        h3, m3, r3, ds3 = self._ln_lora(x2, "norm3", ["ff.net.0.proj"])
+        x12 = L["ff.net.0.proj"].forward(h3, save, W=Wb.get("ff.net.0.proj"), ds=ds3)
         gg = ops.geglu_fwd(x12)
         y = L["ff.net.2"].forward(gg, save, resid=x2, W=Wb.get("ff.net.2"))
         self._st = dict(B=B, n=n, nc=nc, x=x, x1=x1, x2=x2, m=(m1, m2, m3), r=(r1, r2, r3), q=q, k=k, v=v, o1=o1,
@@ -412,10 +441,20 @@ class SDXLTransformerBlock:
         dh3 = L["ff.net.0.proj"].backward(dx12, W=Wb.get("ff.net.0.proj"))
         dx2 = ops.layernorm_bwd(dh3, st["x2"], m3, r3, self.norm["norm3"][0], dres=dy)
         do2 = L["attn2.to_out.0"].backward(dx2, W=Wb.get("attn2.to_out.0"))
-        dq2, dk2, dv2 = self._attn_bwd(st["q2"], st["k2"], st["v2"], st["o2"], st["lse2"], do2, B, n, nc)
+        D = self.inner
+        dkv2 = torch.empty(B * nc, 2 * D, dtype=BF16, device=self.device)  # [dk2 | dv2]: one grouped vs launch
+        dq2, dk2, dv2 = self._attn_bwd(st["q2"], st["k2"], st["v2"], st["o2"], st["lse2"], do2, B, n, nc,
+                                       out=(torch.empty_like(st["q2"]), dkv2[:, :D], dkv2[:, D:]))
         dh2 = L["attn2.to_q"].backward(dq2, W=Wb.get("attn2.to_q"))
-        dck = L["attn2.to_k"].backward(dk2, need_dctx, W=Wb.get("attn2.to_k"))
-        dcv = L["attn2.to_v"].backward(dv2, need_dctx, W=Wb.get("attn2.to_v"))
+        KVT = ("attn2.to_k", "attn2.to_v")
+        vs_kv = None
+        if all(L[t].skinny for t in KVT) and _adjacent([L[t].up for t in KVT]) and L[KVT[0]].scale == L[KVT[1]].scale:
+            vs_kv = torch.empty(B * nc, 32, dtype=BF16, device=self.device)
+            ops.lora_proj_grouped(dkv2, D, L[KVT[0]].up, L[KVT[0]].up.numel(), 2, False, vs_kv, alpha=L[KVT[0]].scale)
+        dck = L["attn2.to_k"].backward(dk2, need_dctx, W=Wb.get("attn2.to_k"),
+                                       vs=None if vs_kv is None else vs_kv[:, :16])
+        dcv = L["attn2.to_v"].backward(dv2, need_dctx, W=Wb.get("attn2.to_v"),
+                                       vs=None if vs_kv is None else vs_kv[:, 16:])
         dctx = ops.add_bf16(dck, dcv) if need_dctx else None
         dx1 = ops.layernorm_bwd(dh2, st["x1"], m2, r2, self.norm["norm2"][0], dres=dx2)
         do1 = L["attn1.to_out.0"].backward(dx1, W=Wb.get("attn1.to_out.0"))
