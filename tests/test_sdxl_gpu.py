@@ -606,3 +606,20 @@ def test_sdxl_block_fused_ln_lora_bitwise(ops, monkeypatch):
         res.append((dctx.clone(), m.grads.clone()))
     (c0, g0), (c1, g1) = res
     assert torch.equal(c0, c1) and torch.equal(g0, g1)
+
+
+def test_nf4_dequant_batch_bit_exact(ops):
+    """vpt_nf4_dequant_batch (several tensors of different sizes in one launch, the last block of each partial)
+    against the oracle's dequantisation of each: bit-identical."""
+    from vpt.sdxl import NF4Weight
+    g = torch.Generator().manual_seed(11)
+    shapes = [(1280, 640), (640, 2048), (1280, 1280), (320, 64), (2560, 640)]
+    pairs, refs = [], []
+    for (o, i) in shapes:
+        st = SO.nf4_quantize(torch.randn(o, i, generator=g) * 0.05)
+        refs.append(SO.nf4_dequantize(st).to(torch.bfloat16))
+        w = NF4Weight.from_state(dict(st, shape=torch.tensor([o, i])))
+        pairs.append((w, torch.full((o, i), float("nan"), dtype=torch.bfloat16, device=DEV)))
+    outs = ops.nf4_dequant_batch(pairs)
+    for out, ref in zip(outs, refs):
+        assert torch.equal(out.cpu(), ref)
