@@ -623,3 +623,21 @@ def test_nf4_dequant_batch_bit_exact(ops):
     outs = ops.nf4_dequant_batch(pairs)
     for out, ref in zip(outs, refs):
         assert torch.equal(out.cpu(), ref)
+
+
+@pytest.mark.parametrize("M,D", [(4100, 1280), (333, 640)])
+def test_layernorm_bwd_no_partials_bit_exact(ops, M, D):
+    """The frozen-affine LayerNorm backward (no dw / db partials: one row per wave, dres in flight with x and dy)
+    gives dx bit-identical to the partial-producing form."""
+    x, dy, dres = rnd(M, D, seed=170), rnd(M, D, seed=171), rnd(M, D, seed=172)
+    w = (rnd(D, scale=0.5, seed=173) + 1.0).to(torch.bfloat16)
+    b = rnd(D, scale=0.1, seed=174)
+    _, mean, rstd = ops.layernorm_fwd(x, w, b)
+    nb = ops.layernorm_bwd_blocks(M)
+    dwp = torch.empty(nb, D, device=DEV)
+    dbp = torch.empty(nb, D, device=DEV)
+    dx0 = ops.layernorm_bwd(dy, x, mean, rstd, w, dres=dres, dw_part=dwp, db_part=dbp)
+    dx1 = ops.layernorm_bwd(dy, x, mean, rstd, w, dres=dres)
+    dx2 = ops.layernorm_bwd(dy, x, mean, rstd, w)
+    dx3 = ops.layernorm_bwd(dy, x, mean, rstd, w, dw_part=dwp, db_part=dbp)
+    assert torch.equal(dx0, dx1) and torch.equal(dx2, dx3)
