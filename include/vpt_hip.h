@@ -246,6 +246,12 @@ int vpt_layernorm_bwd_blocks(int M);
 int vpt_layernorm_bwd(const void* dy, long lddy, const void* x, long ldx, const float* mean, const float* rstd,
                       const void* w, const void* dres, long ldr, void* dx, long lddx, float* dw_part, float* db_part,
                       int M, int D, void* stream);
+/* LayerNorm backward with frozen affine weights (as vpt_layernorm_bwd without partials: bit-identical dx) and, in the
+ * same launch, the rank-16 LoRA projection of dx through an up matrix: vs[m][j] = bf16(alpha * dx[m] . up[:, j]),
+ * up [D][16] -- bit-identical to vpt_lora_proj(dx, up, w_kmajor = 0). D % 128 == 0. */
+int vpt_layernorm_bwd_lora(const void* dy, long lddy, const void* x, long ldx, const float* mean, const float* rstd,
+                           const void* w, const void* dres, long ldr, void* dx, long lddx, int M, int D, const void* up,
+                           void* vs, long ldvs, float alpha, void* stream);
 /* GeGLU (denoiser.py:174-186): out[M,F] = h * gelu_erf(gate), (h | gate) = x12[M, 2F] halves; backward
  * writes d(h) | d(gate) into dx12 [M, 2F]; bf16 rounding of the reference's bf16 tensor graph. */
 int vpt_geglu_fwd(const void* x12, long ldx, int F, long M, void* out, void* stream);

@@ -641,3 +641,21 @@ def test_layernorm_bwd_no_partials_bit_exact(ops, M, D):
     dx2 = ops.layernorm_bwd(dy, x, mean, rstd, w)
     dx3 = ops.layernorm_bwd(dy, x, mean, rstd, w, dw_part=dwp, db_part=dbp)
     assert torch.equal(dx0, dx1) and torch.equal(dx2, dx3)
+
+
+@pytest.mark.parametrize("M,D,res", [(4100, 1280, True), (333, 640, False)])
+def test_layernorm_bwd_lora_bit_exact(ops, M, D, res):
+    """vpt_layernorm_bwd_lora: dx bit-identical to vpt_layernorm_bwd and vs to vpt_lora_proj(dx, up, w_kmajor=0)."""
+    x, dy = rnd(M, D, seed=180), rnd(M, D, seed=181)
+    dres = rnd(M, D, seed=182) if res else None
+    w = (rnd(D, scale=0.5, seed=183) + 1.0).to(torch.bfloat16)
+    b = rnd(D, scale=0.1, seed=184)
+    up = rnd(D, 16, scale=0.05, seed=185)
+    _, mean, rstd = ops.layernorm_fwd(x, w, b)
+    vs = torch.empty(M, 16, dtype=torch.bfloat16, device=DEV)
+    dx = ops.layernorm_bwd_lora(dy, x, mean, rstd, w, up, 0.0625, vs, dres=dres)
+    dx0 = ops.layernorm_bwd(dy, x, mean, rstd, w, dres=dres)
+    assert torch.equal(dx, dx0)
+    ref = torch.empty(M, 16, dtype=torch.bfloat16, device=DEV)
+    ops.lora_proj(dx0, up, False, ref, alpha=0.0625)
+    assert torch.equal(vs, ref)

@@ -266,6 +266,139 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16_t* __rest
   }
 }
 
+// LayerNorm backward (frozen affine weights: no dw / db partials) and, in the same launch, the rank-16 LoRA
+// up-side projection of its output -- vs[m][j] = bf16(alpha * dx[m] . up[:, j]), up [D][16]: the input-gradient
+// operand of the LoRALinear that consumes dx as its output gradient (attn1.to_out.0 after norm2, attn2.to_out.0
+// after norm3). 16 rows per block: every wave computes 4 rows exactly as layernorm_bwd_kernel (same arithmetic) into
+// dx and an LDS image; each 128-row chunk of up is transposed through the wave's LDS image (as lora_proj's up
+// path); the projection then runs in lora_proj's order (wave w: 128-wide K chunks w, w + 4, ...; four 16x16x32 MFMAs per chunk; waves summed in order)
+// -- dx and vs bit-identical to vpt_layernorm_bwd + vpt_lora_proj(w_kmajor = 0).
+template <int NC>  // 16-B chunks per lane: D <= 512 NC
+__global__ __launch_bounds__(256) void layernorm_bwd_lora_kernel(const bf16_t* __restrict__ dy, long lddy,
+                                                                 const bf16_t* __restrict__ x, long ldx,
+                                                                 const float* __restrict__ mean_in,
+                                                                 const float* __restrict__ rstd_in,
+                                                                 const bf16_t* __restrict__ w,
+                                                                 const bf16_t* __restrict__ dres, long ldr,
+                                                                 bf16_t* __restrict__ dx, long lddx, int M, int D,
+                                                                 const bf16_t* __restrict__ up, bf16_t* __restrict__ vs,
+                                                                 long ldvs, float alpha) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t lbl_smem[];  // tile [16][D + 8]
+  __shared__ __attribute__((aligned(16))) bf16_t wsa[4][16 * (LNL_KC + 8)];  // per-wave transposed up chunk
+  __shared__ __attribute__((aligned(16))) floatx4 red[4][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g4 = lane >> 4, j = lane & 15;
+  const int TS = D + 8;
+  bf16_t* tile = lbl_smem;
+  bf16_t* ws = wsa[wid];
+  const int nch = D >> 3;
+  const long row0 = (long)blockIdx.x * 16;
+  // the wave's four rows of x / dy (/ dres) in flight before any arithmetic (one block = 16 rows = 1 wave per SIMD:
+  // latency, not bandwidth, bounds a row at a time)
+  uint4 rx[4][NC], rd[4][NC], rr_[4][NC];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const long row = row0 + wid * 4 + q;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = lane + 64 * i;
+      if (row < M && c < nch) {
+        rx[q][i] = *reinterpret_cast<const uint4*>(x + row * ldx + c * 8);
+        rd[q][i] = *reinterpret_cast<const uint4*>(dy + row * lddy + c * 8);
+        if (dres) rr_[q][i] = *reinterpret_cast<const uint4*>(dres + row * ldr + c * 8);
+      }
+    }
+  }
+  float wf[NC][8];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) unpack8(*reinterpret_cast<const uint4*>(w + c * 8), wf[i]);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int lr = wid * 4 + q;
+    const long row = row0 + lr;
+    bf16_t* trow = tile + lr * TS;
+    if (row >= M) {
+      for (int c = lane; c < nch; c += 64) *reinterpret_cast<uint4*>(trow + c * 8) = make_uint4(0, 0, 0, 0);
+      continue;
+    }
+    const float mu = mean_in[row], r = rstd_in[row];
+    float xh[NC][8], gg[NC][8];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        float fx[8], fd[8];
+        unpack8(rx[q][i], fx);
+        unpack8(rd[q][i], fd);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          xh[i][e] = (fx[e] - mu) * r;
+          gg[i][e] = fd[e] * wf[i][e];
+          sg += gg[i][e];
+          sgx += gg[i][e] * xh[i][e];
+        }
+      }
+    }
+    const float mg = wave_sum(sg) / (float)D, mgx = wave_sum(sgx) / (float)D;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        float o[8], fr[8];
+        if (dres) unpack8(rr_[q][i], fr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = r * (gg[i][e] - mg - xh[i][e] * mgx);
+          o[e] = dres ? fr[e] + bf2f(f2bf(d)) : d;
+        }
+        const uint4 pk = pack8(o);
+        *reinterpret_cast<uint4*>(dx + row * lddx + c * 8) = pk;
+        *reinterpret_cast<uint4*>(trow + c * 8) = pk;
+      }
+    }
+  }
+  __syncthreads();
+  const int ncw = (D / LNL_KC - wid + 3) / 4;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int u = 0; u < ncw; ++u) {
+    const int c = wid + 4 * u;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // up rows c*128 + kr, kr < 128 -> ws [16][128 + 8] (lora_proj's up path)
+      const int kr = lane + 64 * h;
+      const uint4 a0 = *reinterpret_cast<const uint4*>(up + (long)(c * LNL_KC + kr) * 16);
+      const uint4 a1 = *reinterpret_cast<const uint4*>(up + (long)(c * LNL_KC + kr) * 16 + 8);
+      const uint32_t v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        ws[(2 * e) * (LNL_KC + 8) + kr] = (bf16_t)(v[e] & 0xffff);
+        ws[(2 * e + 1) * (LNL_KC + 8) + kr] = (bf16_t)(v[e] >> 16);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int s2 = 0; s2 < LNL_KC / 32; ++s2) {
+      const uint4 xa = *reinterpret_cast<const uint4*>(tile + j * TS + c * LNL_KC + 32 * s2 + 8 * g4);
+      const uint4 wb = *reinterpret_cast<const uint4*>(ws + j * (LNL_KC + 8) + 32 * s2 + 8 * g4);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(xa), as_frag(wb), acc, 0, 0, 0);
+    }
+  }
+  red[wid][lane] = acc;
+  __syncthreads();
+  if (wid != 0) return;
+#pragma unroll
+  for (int w2 = 1; w2 < 4; ++w2) acc += red[w2][lane];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const long m = row0 + 4 * g4 + r;
+    if (m < M) vs[m * ldvs + j] = f2bf(acc[r] * alpha);
+  }
+}
+
 // ---------------------------------------------------------------- GeGLU
 __device__ __forceinline__ float rbf(float v) { return bf2f(f2bf(v)); }
 __device__ __forceinline__ float gelu_erf(float g) { return 0.5f * g * (1.f + erff(g * 0.70710678118654752f)); }
@@ -641,6 +774,23 @@ extern "C" int vpt_layernorm_bwd(const void* dy, long lddy, const void* x, long 
   hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(vpt_layernorm_bwd_blocks(M)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, mean, rstd, (const bf16_t*)w,
                      (const bf16_t*)dres, ldr, (bf16_t*)dx, lddx, dw_part, db_part, M, D);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_layernorm_bwd_lora(const void* dy, long lddy, const void* x, long ldx, const float* mean,
+                                      const float* rstd, const void* w, const void* dres, long ldr, void* dx, long lddx,
+                                      int M, int D, const void* up, void* vs, long ldvs, float alpha, void* stream) {
+  VPT_CHECK_ARG(dy && x && mean && rstd && w && dx && up && vs, "vpt_layernorm_bwd_lora: null pointer");
+  VPT_CHECK_ARG(D % LNL_KC == 0 && D <= 2048 && lddy % 8 == 0 && ldx % 8 == 0 && lddx % 8 == 0 && (!dres || ldr % 8 == 0)
+                    && ldvs >= 16, "vpt_layernorm_bwd_lora: D % 128 == 0, D <= 2048, 16-B leading dims");
+  if (M == 0) return VPT_OK;
+  const size_t lds = (size_t)16 * (D + 8) * sizeof(bf16_t);
+  const int nc = (D / 8 + 63) / 64;
+  auto k = nc <= 2 ? layernorm_bwd_lora_kernel<2> : nc == 3 ? layernorm_bwd_lora_kernel<3> : layernorm_bwd_lora_kernel<4>;
+  hipLaunchKernelGGL(k, dim3((M + 15) / 16), dim3(256), lds, (hipStream_t)stream, (const bf16_t*)dy, lddy,
+                     (const bf16_t*)x, ldx, mean, rstd, (const bf16_t*)w, (const bf16_t*)dres, ldr, (bf16_t*)dx, lddx, M,
+                     D, (const bf16_t*)up, (bf16_t*)vs, ldvs, alpha);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

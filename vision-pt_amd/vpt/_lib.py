@@ -70,6 +70,7 @@ SIGNATURES: dict[str, list] = {
     "vpt_layernorm_lora_fwd": [P, L, P, P, P, L, P, P, I, I, F, P, L, I, P, L, F, P],
     "vpt_layernorm_bwd_blocks": [I],
     "vpt_layernorm_bwd": [P, L, P, L, P, P, P, P, L, P, L, P, P, I, I, P],
+    "vpt_layernorm_bwd_lora": [P, L, P, L, P, P, P, P, L, P, L, I, I, P, P, L, F, P],
     "vpt_geglu_fwd": [P, L, I, L, P, P],
     "vpt_geglu_bwd": [P, P, L, I, L, P, L, P],
     "vpt_nf4_dequant": [P, P, P, P, P, L, P, P],

@@ -678,6 +678,20 @@ def layernorm_bwd(dy, x, mean, rstd, w, dres=None, dx=None, dw_part=None, db_par
     return dx
 
 
+def layernorm_bwd_lora(dy, x, mean, rstd, w, up, alpha: float, vs, dres=None):
+    """layernorm_bwd (no partials) and, in the same launch, vs = bf16(alpha * dx . up) (up [D, 16];
+    csrc/sdxl.hip layernorm_bwd_lora_kernel). Returns dx."""
+    M, D = x.shape
+    _chk(up, BF16, "up")
+    if not up.is_contiguous() or vs.stride(1) != 1 or vs.shape[1] < 16:
+        raise ValueError("layernorm_bwd_lora: contiguous up, row-major vs with 16 columns")
+    dx = torch.empty(M, D, dtype=BF16, device=x.device)
+    call("vpt_layernorm_bwd_lora", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), mean.data_ptr(),
+         rstd.data_ptr(), w.data_ptr(), _p(dres), 0 if dres is None else dres.stride(0), dx.data_ptr(), dx.stride(0),
+         M, D, up.data_ptr(), vs.data_ptr(), vs.stride(0), float(alpha), stream())
+    return dx
+
+
 def layernorm_bwd_blocks(M: int) -> int:
     return lib.vpt_layernorm_bwd_blocks(M)
 

@@ -257,8 +257,9 @@ class LoRALinearNF4:
         return vs
 
 
-# A/B knob: 0 = LayerNorm and the LoRA down-projections of its output as separate launches
+# A/B knob: 0 = LayerNorm (forward / backward) and the LoRA projections of its output as separate launches
 FUSED_LN_LORA = os.environ.get("VPT_LN_LORA", "1") != "0"
+FUSED_LN_BWD_LORA = os.environ.get("VPT_LN_BWD_LORA", "1") != "0"  # the backward half alone (A/B)
 
 
 def _adjacent(ts) -> bool:
@@ -329,6 +330,17 @@ class SDXLTransformerBlock:
             y, m, r = ops.layernorm_lora_fwd(x, *self.norm[norm], downs[0], len(targets), L[targets[0]].scale, ds)
             return y, m, r, ds
         return (*ops.layernorm_fwd(x, *self.norm[norm]), None)
+
+    def _ln_bwd_lora(self, dy, x, mean, rstd, norm: str, dres, target: str):
+        """LayerNorm backward of `norm` and the input-gradient LoRA operand vs = s * dx . up of `target` (the
+        LoRALinear that consumes dx as its output gradient) in one launch (ops.layernorm_bwd_lora): (dx, vs); vs None
+        where the fused form does not apply."""
+        lin = self.lin[target]
+        if FUSED_LN_LORA and FUSED_LN_BWD_LORA and lin.skinny and lin.up.is_contiguous() and x.shape[1] % 128 == 0:
+            vs = torch.empty(x.shape[0], 16, dtype=BF16, device=x.device)
+            dx = ops.layernorm_bwd_lora(dy, x, mean, rstd, self.norm[norm][0], lin.up, lin.scale, vs, dres=dres)
+            return dx, vs
+        return ops.layernorm_bwd(dy, x, mean, rstd, self.norm[norm][0], dres=dres), None
 
     def _qkv_fwd(self, h1, Wqkv, save, ds=None):
         """q|k|v = h1 . [Wq; Wk; Wv]^T + [ds_q | ds_k | ds_v] . blockdiag(up_q, up_k, up_v)^T as ONE GEMM
@@ -439,8 +451,8 @@ class SDXLTransformerBlock:
         dgg = L["ff.net.2"].backward(dy, W=Wb.get("ff.net.2"))
         dx12 = ops.geglu_bwd(dgg, st["x12"])
         dh3 = L["ff.net.0.proj"].backward(dx12, W=Wb.get("ff.net.0.proj"))
-        dx2 = ops.layernorm_bwd(dh3, st["x2"], m3, r3, self.norm["norm3"][0], dres=dy)
-        do2 = L["attn2.to_out.0"].backward(dx2, W=Wb.get("attn2.to_out.0"))
+        dx2, vs_o2 = self._ln_bwd_lora(dh3, st["x2"], m3, r3, "norm3", dy, "attn2.to_out.0")
+        do2 = L["attn2.to_out.0"].backward(dx2, W=Wb.get("attn2.to_out.0"), vs=vs_o2)
         D = self.inner
         dkv2 = torch.empty(B * nc, 2 * D, dtype=BF16, device=self.device)  # [dk2 | dv2]: one grouped vs launch
         dq2, dk2, dv2 = self._attn_bwd(st["q2"], st["k2"], st["v2"], st["o2"], st["lse2"], do2, B, n, nc,
@@ -456,8 +468,8 @@ class SDXLTransformerBlock:
         dcv = L["attn2.to_v"].backward(dv2, need_dctx, W=Wb.get("attn2.to_v"),
                                        vs=None if vs_kv is None else vs_kv[:, 16:])
         dctx = ops.add_bf16(dck, dcv) if need_dctx else None
-        dx1 = ops.layernorm_bwd(dh2, st["x1"], m2, r2, self.norm["norm2"][0], dres=dx2)
-        do1 = L["attn1.to_out.0"].backward(dx1, W=Wb.get("attn1.to_out.0"))
+        dx1, vs_o1 = self._ln_bwd_lora(dh2, st["x1"], m2, r2, "norm2", dx2, "attn1.to_out.0")
+        do1 = L["attn1.to_out.0"].backward(dx1, W=Wb.get("attn1.to_out.0"), vs=vs_o1)
         if self._fuse_qkv(Wb):
             dqkv = torch.empty(B * n, 3 * self.inner, dtype=BF16, device=self.device)
             D = self.inner
