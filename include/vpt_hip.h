@@ -73,6 +73,18 @@ int vpt_gemm_bf16_lora_grouped(const void* A, long lda, const void* B, long ldb,
                                const void* const* B2s, int G, int r, void* C, long ldc, int M, int g_n, int K,
                                const void* bias, const void* resid, long ldr, int splits, void* workspace,
                                int geometry, void* stream);
+/* vpt_gemm_bf16_lora / vpt_gemm_bf16_lora_grouped (splits = 1) with an output scale: alpha multiplies the f32
+ * result (base + extension) of output columns [0, alpha_cols) -- every column when alpha_cols = 0; otherwise a
+ * multiple of 128 -- before bias / residual and the one bf16 rounding: the attention q projection emitted already
+ * multiplied by vpt_attn_q_scale (the attention kernels' pre-scaled q) instead of a separate scaling pass. */
+int vpt_gemm_bf16_lora_scaled(const void* A, long lda, const void* B, long ldb, int b_kmajor, const void* A2, long lda2,
+                              const void* B2, long ldb2, int K2, void* C, long ldc, int M, int N, int K,
+                              const void* bias, const void* resid, long ldr, int geometry, float alpha, int alpha_cols,
+                              void* stream);
+int vpt_gemm_bf16_lora_grouped_scaled(const void* A, long lda, const void* B, long ldb, const void* A2, long lda2,
+                                      const void* const* B2s, int G, int r, void* C, long ldc, int M, int g_n, int K,
+                                      const void* bias, const void* resid, long ldr, int geometry, float alpha,
+                                      int alpha_cols, void* stream);
 /* The same with the G bases stacked [G*g_n][K] and the G ups stacked [G*g_n][r] (B2, leading dim r), any G:
  * the cross-attention to_k / to_v of every transformer block over one fixed text context as ONE GEMM per step
  * (src/models/sdxl/denoiser.py:101-171; the context is the same for all 70 blocks). */

@@ -659,3 +659,35 @@ def test_layernorm_bwd_lora_bit_exact(ops, M, D, res):
     ref = torch.empty(M, 16, dtype=torch.bfloat16, device=DEV)
     ops.lora_proj(dx0, up, False, ref, alpha=0.0625)
     assert torch.equal(vs, ref)
+
+
+@pytest.mark.parametrize("gn,geometry", [(1280, 128), (1280, 256), (640, 128)])
+def test_gemm_lora_scaled_columns(ops, gn, geometry):
+    """vpt_gemm_bf16_lora(_grouped)_scaled: alpha = 2^-3 on columns [0, gn) is exact scaling, so the output equals
+    the unscaled GEMM's with the first column block times 2^-3 and the rest untouched (bit-exact); a general alpha
+    (the attention q scale) matches fp32 math within one bf16 rounding."""
+    M, K, r = 700, 1280, 16
+    x = rnd(M, K, seed=150)
+    Ws = [rnd(gn, K, scale=0.03, seed=151 + g) for g in range(3)]
+    ups = [rnd(gn, r, scale=0.1, seed=155 + g) for g in range(3)]
+    ds = rnd(M, 3 * r, scale=0.5, seed=159)
+    W = torch.cat(Ws, 0)
+    base = torch.empty(M, 3 * gn, dtype=torch.bfloat16, device=DEV)
+    ops.gemm_lora_grouped(x, W, ds, ups, base, geometry=geometry)
+    out = torch.empty_like(base)
+    ops.gemm_lora_grouped(x, W, ds, ups, out, geometry=geometry, alpha=0.125, alpha_cols=gn)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:, :gn], (base[:, :gn].float() * 0.125).bfloat16())
+    assert torch.equal(out[:, gn:], base[:, gn:])
+    # single target, every column scaled
+    one = torch.empty(M, gn, dtype=torch.bfloat16, device=DEV)
+    ops.gemm_lora(x, Ws[0], True, ds[:, :r].contiguous(), ups[0], M, gn, K, one, geometry=geometry, alpha=0.125)
+    torch.cuda.synchronize()
+    assert torch.equal(one, out[:, :gn])
+    # general alpha vs fp32
+    a = ops.attn_q_scale(0.125)
+    ops.gemm_lora(x, Ws[0], True, ds[:, :r].contiguous(), ups[0], M, gn, K, one, geometry=geometry, alpha=a)
+    y = (x.float() @ Ws[0].float().t() + ds[:, :r].float() @ ups[0].float().t()) * a
+    torch.cuda.synchronize()
+    assert rel(one, y) < 1e-2
+    assert (one.float() - y).abs().max().item() <= y.abs().max().item() * 2 ** -7

@@ -68,6 +68,9 @@ struct GemmArgs {
   // ungrouped (B2). Tiles never straddle groups (g_n % tile width == 0).
   const bf16_t* B2g[4];
   int g_n;
+  // alpha_cols > 0: alpha scales output columns [0, alpha_cols) only, the rest take 1 (the attention q block of a
+  // fused q|k|v GEMM pre-scaled in its epilogue); a multiple of the ring tile width (256) or the T128 path is used
+  int alpha_cols;
 };
 
 // ---- LDS images -----------------------------------------------------------------------------
@@ -233,6 +236,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, floatx4 (&acc)[G::MI
       const int col = n0 + wn * G::WC + cb + colw;
       const bool col_ok = cb + colw < G::WC && col < g.N;  // (an 80-wide wave tile: 16 columns in round 2)
       float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+      const float alpha = g.alpha_cols > 0 && col >= g.alpha_cols ? 1.f : g.alpha;
       if (g.bias && col_ok) {
         const uint2 bv = *reinterpret_cast<const uint2*>(g.bias + col);
         bias4[0] = __uint_as_float(bv.x << 16); bias4[1] = __uint_as_float(bv.x & 0xffff0000u);
@@ -243,8 +247,8 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, floatx4 (&acc)[G::MI
         const int row = m0 + wm * G::WR + h * 16 * SLAB + lr;
         if (row >= g.M || !col_ok) continue;
         floatx4 v = *reinterpret_cast<const floatx4*>(st + lr * ELD + cb + colw);
-        float o[4] = {v[0] * g.alpha + bias4[0], v[1] * g.alpha + bias4[1], v[2] * g.alpha + bias4[2],
-                      v[3] * g.alpha + bias4[3]};
+        float o[4] = {v[0] * alpha + bias4[0], v[1] * alpha + bias4[1], v[2] * alpha + bias4[2],
+                      v[3] * alpha + bias4[3]};
         if (g.act == ACT_SILU) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = o[e] / (1.f + __expf(-o[e]));
@@ -588,6 +592,7 @@ struct EpiAddr {
   uint32_t voff, rvoff, avoff;
   int rstride, rrstride, rastride;
   bool col_ok;
+  float alpha;  // the output scale of this tile (GemmArgs::alpha / alpha_cols)
 };
 
 __device__ __forceinline__ EpiAddr epi_addr(const GemmArgs& g, const RingItem& it, int wm, int wn, int lane) {
@@ -598,6 +603,7 @@ __device__ __forceinline__ EpiAddr epi_addr(const GemmArgs& g, const RingItem& i
   e.rs = __builtin_amdgcn_make_buffer_rsrc(cbase, (short)0, rows_here * (int)g.ldc * es, 0x00020000);
   const int tcol = wn * 64 + (lane & 7) * 8;  // column within the tile
   e.col_ok = it.n0 + tcol < g.N;
+  e.alpha = g.alpha_cols > 0 && it.n0 >= g.alpha_cols ? 1.f : g.alpha;
   const int lrow = wm * 128 + (lane >> 3);  // tile row of (fragment 0, p = 0)
   // lane part of the store offset; fragment i / half p add the wave-uniform soffset (i*16 + p*8) rows
   e.voff = e.col_ok ? (uint32_t)((lrow * (int)g.ldc + tcol) * es) : 0x80000000u;
@@ -715,7 +721,7 @@ __device__ __forceinline__ void epilogue_ring(const GemmArgs& g, const floatx4 (
       const floatx4 x1 = *reinterpret_cast<const floatx4*>(stg + stg_off(lr, cw * 8 + 4));
       float o[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
 #pragma unroll
-      for (int q = 0; q < 8; ++q) o[q] = o[q] * g.alpha + bias8[q];
+      for (int q = 0; q < 8; ++q) o[q] = o[q] * e.alpha + bias8[q];
       if (g.act == ACT_SILU) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) o[q] = o[q] / (1.f + __expf(-o[q]));
@@ -1200,7 +1206,7 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
               void* workspace, float alpha, int geo_req, int ring_grid, void* stream, float* rsum_out = nullptr,
               int rsum_acc = 0, bool* rsum_done = nullptr, const void* A2 = nullptr, long lda2 = 0,
               const void* B2 = nullptr, long ldb2 = 0, int K2 = 0, const void* const* B2g = nullptr, int G = 0,
-              int g_n = 0);
+              int g_n = 0, int alpha_cols = 0);
 
 }  // namespace
 
@@ -1246,6 +1252,38 @@ extern "C" int vpt_gemm_bf16_lora_grouped(const void* A, long lda, const void* B
                    1.f, geometry, 0, stream, nullptr, 0, nullptr, A2, lda2, B2s[0], r, r, B2s, G, g_n);
 }
 
+// vpt_gemm_bf16_lora / vpt_gemm_bf16_lora_grouped with an output scale: alpha multiplies the f32 result (base +
+// extension) of columns [0, alpha_cols) before bias / residual and the one bf16 rounding (alpha_cols = 0: every
+// column; otherwise a multiple of 128) -- the attention q projection emitted pre-scaled for the attention kernels.
+// splits must be 1.
+extern "C" int vpt_gemm_bf16_lora_scaled(const void* A, long lda, const void* B, long ldb, int b_kmajor, const void* A2,
+                                         long lda2, const void* B2, long ldb2, int K2, void* C, long ldc, int M, int N,
+                                         int K, const void* bias, const void* resid, long ldr, int geometry, float alpha,
+                                         int alpha_cols, void* stream) {
+  VPT_CHECK_ARG(A2 && B2, "vpt_gemm_bf16_lora_scaled: null LoRA operand");
+  VPT_CHECK_ARG(K % 64 == 0 && K2 > 0 && K2 <= 256 && K2 % 8 == 0, "vpt_gemm_bf16_lora_scaled: K % 64 == 0, K2 in 8..256, K2 % 8 == 0");
+  VPT_CHECK_ARG(lda2 % 8 == 0 && ldb2 % 8 == 0 && lda2 >= K2 && (b_kmajor ? ldb2 >= K2 : ldb2 >= N),
+                "vpt_gemm_bf16_lora_scaled: LoRA leading dims (16-B multiples, >= K2 / N)");
+  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256, "vpt_gemm_bf16_lora_scaled: geometry 0, 128 or 256");
+  return gemm_impl(A, lda, 1, B, ldb, b_kmajor, C, ldc, M, N, K, bias, resid, ldr, OUT_BF16, ACT_NONE, 1, nullptr,
+                   alpha, geometry, 0, stream, nullptr, 0, nullptr, A2, lda2, B2, ldb2, K2, nullptr, 0, 0, alpha_cols);
+}
+
+extern "C" int vpt_gemm_bf16_lora_grouped_scaled(const void* A, long lda, const void* B, long ldb, const void* A2,
+                                                 long lda2, const void* const* B2s, int G, int r, void* C, long ldc,
+                                                 int M, int g_n, int K, const void* bias, const void* resid, long ldr,
+                                                 int geometry, float alpha, int alpha_cols, void* stream) {
+  VPT_CHECK_ARG(A2 && B2s && G > 0 && G <= 4, "vpt_gemm_bf16_lora_grouped_scaled: 1..4 groups");
+  for (int i = 0; i < G; ++i) VPT_CHECK_ARG(B2s[i], "vpt_gemm_bf16_lora_grouped_scaled: null up");
+  VPT_CHECK_ARG(K % 64 == 0 && r > 0 && r <= 64 && r % 8 == 0 && g_n % 128 == 0,
+                "vpt_gemm_bf16_lora_grouped_scaled: K % 64 == 0, r in 8..64 (r % 8 == 0), g_n % 128 == 0");
+  VPT_CHECK_ARG(lda2 % 8 == 0 && lda2 >= G * r, "vpt_gemm_bf16_lora_grouped_scaled: lda2 >= G * r (16-B multiple)");
+  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256,
+                "vpt_gemm_bf16_lora_grouped_scaled: geometry 0, 128, 256");
+  return gemm_impl(A, lda, 1, B, ldb, 1, C, ldc, M, G * g_n, K, bias, resid, ldr, OUT_BF16, ACT_NONE, 1, nullptr,
+                   alpha, geometry, 0, stream, nullptr, 0, nullptr, A2, lda2, B2s[0], r, r, B2s, G, g_n, alpha_cols);
+}
+
 // Any number G of LoRA targets reading the same input, bases stacked [G * g_n][K] and adapters' ups stacked
 // [G * g_n][r] (B2, ld r): C[:, g*g_n:(g+1)*g_n] = A . W_g^T + A2[:, g*r:(g+1)*r] . up_g^T. The cross-attention
 // k / v projections of a fixed text context for every transformer block of a step as one GEMM.
@@ -1279,8 +1317,9 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
               int N, int K, const void* bias, const void* resid, long ldr, int out_mode, int act, int splits,
               void* workspace, float alpha, int geo_req, int ring_grid, void* stream, float* rsum_out, int rsum_acc,
               bool* rsum_done, const void* A2, long lda2, const void* B2, long ldb2, int K2,
-              const void* const* B2g, int G, int g_n) {
+              const void* const* B2g, int G, int g_n, int alpha_cols) {
   VPT_CHECK_ARG(A && B && C, "vpt_gemm_bf16: null operand");
+  VPT_CHECK_ARG(alpha_cols >= 0 && alpha_cols % 128 == 0, "vpt_gemm_bf16: alpha_cols a multiple of 128");
   VPT_CHECK_ARG(M > 0 && N > 0 && K > 0, "vpt_gemm_bf16: empty shape");
   VPT_CHECK_ARG(N % 4 == 0, "vpt_gemm_bf16: N%4 required");
   VPT_CHECK_ARG((!a_kmajor && !b_kmajor) || K % 8 == 0, "vpt_gemm_bf16: k-major operands need K%8==0");
@@ -1298,6 +1337,7 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
   g.M = M; g.N = N; g.K = K;
   g.act = act;
   g.alpha = alpha;
+  g.alpha_cols = alpha_cols < N ? alpha_cols : 0;
   g.ring_grid = ring_grid;
   g.A2 = (const bf16_t*)A2; g.lda2 = lda2;
   g.B2 = (const bf16_t*)B2; g.ldb2 = ldb2;
@@ -1339,6 +1379,7 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
   }
   int geo = pick_geo(M, N, splits, geo_req);
   if (g.g_n > 0 && g.g_n % 256 != 0) geo = 128;  // grouped extension: a 256-wide tile would straddle two groups
+  if (g.alpha_cols % 256 != 0) geo = 128;         // the ring applies alpha per 256-wide tile
   const bool rs = rsum_out && !a_kmajor && geo == 256 && N % 8 == 0 && workspace != nullptr;
   if (rsum_done) *rsum_done = rs;
   float* rpart = nullptr;

@@ -77,6 +77,8 @@ SIGNATURES: dict[str, list] = {
     "vpt_nf4_dequant_batch": [P, I, P],
     "vpt_scale_bf16_2d": [P, L, L, I, F, P, L, P],
     "vpt_gemm_bf16_lora_grouped": [P, L, P, L, P, L, P, I, I, P, L, I, I, I, P, P, L, I, P, I, P],
+    "vpt_gemm_bf16_lora_scaled": [P, L, P, L, I, P, L, P, L, I, P, L, I, I, I, P, P, L, I, F, I, P],
+    "vpt_gemm_bf16_lora_grouped_scaled": [P, L, P, L, P, L, P, I, I, P, L, I, I, I, P, P, L, I, F, I, P],
     "vpt_gemm_bf16_lora_stacked": [P, L, P, L, P, L, P, I, I, P, L, I, I, I, I, P, I, P],
     "vpt_groupnorm_fwd": [P, P, P, P, P, P, I, I, I, L, F, P],
     "vpt_groupnorm_bwd": [P, P, P, P, P, P, P, I, I, I, L, P],

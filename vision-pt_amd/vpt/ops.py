@@ -155,11 +155,12 @@ def lora_gemm_plan(M: int, N: int, K: int) -> tuple[int, int]:
 
 
 def gemm_lora(a, b, b_kmajor: bool, a2, b2, M: int, N: int, K: int, out, *, bias=None, resid=None, geometry=None,
-              splits=None):
+              splits=None, alpha: float = 1.0, alpha_cols: int = 0):
     """out[M,N] = A . B (+bias) (+resid) + a2 . B2 with one rounding (vpt_gemm_bf16_lora): the base GEMM of a
     LoRALinear with its adapter term as a K-extension. Forward: a = x [M,K], b = W [N,K] (b_kmajor), a2 = ds [M,r],
     b2 = up [N,r]; input gradient: a = dy [M,N_out] (K = N_out), b = W [N_out, K_in] (not b_kmajor, N = K_in),
-    a2 = vs [M,r], b2 = down [r, K_in]."""
+    a2 = vs [M,r], b2 = down [r, K_in]. alpha != 1: the f32 result of columns [0, alpha_cols) (all when 0) times alpha
+    before the rounding (vpt_gemm_bf16_lora_scaled; no K split)."""
     for t, n in ((a, "a"), (b, "b"), (a2, "a2"), (b2, "b2")):
         _chk(t, BF16, n)
     _chk(out, BF16, "out")
@@ -171,9 +172,18 @@ def gemm_lora(a, b, b_kmajor: bool, a2, b2, M: int, N: int, K: int, out, *, bias
     geo, sp = lora_gemm_plan(M, N, K)
     geometry = geo if geometry is None else geometry
     splits = sp if splits is None else splits
+    scaled = alpha != 1.0
+    if scaled:
+        splits = 1
     ws = workspace(out.device, "gemm_lora", splits * M * N) if splits > 1 else None
 
     def run():
+        if scaled:
+            call("vpt_gemm_bf16_lora_scaled", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), int(b_kmajor),
+                 a2.data_ptr(), a2.stride(0), b2.data_ptr(), b2.stride(0), K2, out.data_ptr(), out.stride(0), M, N, K,
+                 _p(bias), _p(resid), 0 if resid is None else resid.stride(0), int(geometry), float(alpha),
+                 int(alpha_cols), stream())
+            return
         call("vpt_gemm_bf16_lora", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), int(b_kmajor), a2.data_ptr(),
              a2.stride(0), b2.data_ptr(), b2.stride(0), K2, out.data_ptr(), out.stride(0), M, N, K, _p(bias), _p(resid),
              0 if resid is None else resid.stride(0), OUT_BF16, int(splits), _p(ws), int(geometry), stream())
@@ -185,9 +195,11 @@ def gemm_lora(a, b, b_kmajor: bool, a2, b2, M: int, N: int, K: int, out, *, bias
     return out
 
 
-def gemm_lora_grouped(x, w_stacked, a2, ups, out, *, bias=None, resid=None, geometry=None, splits=None):
+def gemm_lora_grouped(x, w_stacked, a2, ups, out, *, bias=None, resid=None, geometry=None, splits=None,
+                      alpha: float = 1.0, alpha_cols: int = 0):
     """G LoRA targets reading x as one GEMM (vpt_gemm_bf16_lora_grouped): out[:, g*n:(g+1)*n] = x . W_g^T +
-    a2[:, g*r:(g+1)*r] . ups[g]^T, W_g = w_stacked[g*n:(g+1)*n] (the dequantised bases side by side)."""
+    a2[:, g*r:(g+1)*r] . ups[g]^T, W_g = w_stacked[g*n:(g+1)*n] (the dequantised bases side by side). alpha != 1:
+    columns [0, alpha_cols) (all when 0) times alpha before the rounding (vpt_gemm_bf16_lora_grouped_scaled)."""
     for t, n in ((x, "x"), (w_stacked, "w_stacked"), (a2, "a2"), (out, "out")):
         _chk(t, BF16, n)
     G = len(ups)
@@ -200,10 +212,19 @@ def gemm_lora_grouped(x, w_stacked, a2, ups, out, *, bias=None, resid=None, geom
     geo, sp = lora_gemm_plan(M, G * gn, K)
     geometry = geo if geometry is None else geometry
     splits = sp if splits is None else splits
+    scaled = alpha != 1.0
+    if scaled:
+        splits = 1
     ws = workspace(out.device, "gemm_lora", splits * M * G * gn) if splits > 1 else None
     ptrs = (ctypes.c_void_p * G)(*[u.data_ptr() for u in ups])
 
     def run():
+        if scaled:
+            call("vpt_gemm_bf16_lora_grouped_scaled", x.data_ptr(), x.stride(0), w_stacked.data_ptr(),
+                 w_stacked.stride(0), a2.data_ptr(), a2.stride(0), ctypes.cast(ptrs, ctypes.c_void_p), G, r,
+                 out.data_ptr(), out.stride(0), M, gn, K, _p(bias), _p(resid), 0 if resid is None else resid.stride(0),
+                 int(geometry), float(alpha), int(alpha_cols), stream())
+            return
         call("vpt_gemm_bf16_lora_grouped", x.data_ptr(), x.stride(0), w_stacked.data_ptr(), w_stacked.stride(0),
              a2.data_ptr(), a2.stride(0), ctypes.cast(ptrs, ctypes.c_void_p), G, r, out.data_ptr(), out.stride(0), M, gn,
              K, _p(bias), _p(resid), 0 if resid is None else resid.stride(0), int(splits), _p(ws), int(geometry),

@@ -189,10 +189,14 @@ class LoRALinearNF4:
 
     def forward(self, x: torch.Tensor, save: bool = True, out: torch.Tensor | None = None,
                 resid: torch.Tensor | None = None, W: torch.Tensor | None = None,
-                ds: torch.Tensor | None = None) -> torch.Tensor:
+                ds: torch.Tensor | None = None, out_scale: float = 1.0) -> torch.Tensor:
         """resid: a bf16 tensor added in the epilogue (the block's residual stream: bf16(resid + bf16(y))).
         W: the base already dequantised by the caller (dequant_bases), else this call dequantises it.
-        ds: s * x . down^T already computed by the caller (the fused LayerNorm, ops.layernorm_lora_fwd)."""
+        ds: s * x . down^T already computed by the caller (the fused LayerNorm, ops.layernorm_lora_fwd).
+        out_scale: y = bf16(out_scale * (x . Wd^T + ds . up^T)) -- the attention q emitted pre-scaled (a Linear
+        without bias or residual); folded into the GEMM epilogue on the dequant and inline paths."""
+        if out_scale != 1.0 and (self.bias is not None or resid is not None):
+            raise ValueError("out_scale: a Linear without bias / residual only")
         M = x.shape[0]
         r = self.down.shape[0]
         if ds is not None:
@@ -206,15 +210,18 @@ class LoRALinearNF4:
         y = out if out is not None else torch.empty(M, self.base.shape[0], dtype=BF16, device=x.device)
         if self.fused and self.base_mode != "inline":
             W = base_weight(self.base, self.base_mode, x.device) if W is None else W
-            ops.gemm_lora(x, W, True, ds, self.up, M, W.shape[0], W.shape[1], y, bias=self.bias, resid=resid)
+            ops.gemm_lora(x, W, True, ds, self.up, M, W.shape[0], W.shape[1], y, bias=self.bias, resid=resid,
+                          alpha=out_scale)
         elif self.fused:
-            ops.gemm_nf4(x, self.base, True, y, lora_a=ds, lora_b=self.up, bias=self.bias, resid=resid)
+            ops.gemm_nf4(x, self.base, True, y, lora_a=ds, lora_b=self.up, bias=self.bias, resid=resid, alpha=out_scale)
         else:
             lo = ops.gemm(ds, True, self.up, True, M, self.up.shape[0], r,
                           torch.empty(M, self.up.shape[0], dtype=BF16, device=x.device))
             ops.linear(x, self.weight(), bias=self.bias, resid=lo, out=y)
             if resid is not None:
                 y = ops.add_bf16(resid, y)
+            if out_scale != 1.0:
+                y = ops.scale_bf16(y, out_scale)
         self._saved = (x, ds) if save else None
         return y
 
@@ -260,6 +267,9 @@ class LoRALinearNF4:
 # A/B knob: 0 = LayerNorm (forward / backward) and the LoRA projections of its output as separate launches
 FUSED_LN_LORA = os.environ.get("VPT_LN_LORA", "1") != "0"
 FUSED_LN_BWD_LORA = os.environ.get("VPT_LN_BWD_LORA", "1") != "0"  # the backward half alone (A/B)
+# 1 = the attention q projections emit q * scale * log2(e) from their GEMM epilogue (one rounding);
+# 0 = a bf16 q, then a separate scaling pass (two roundings, one more launch per q)
+FOLD_Q_SCALE = os.environ.get("VPT_FOLD_Q_SCALE", "1") != "0"
 
 
 def _adjacent(ts) -> bool:
@@ -309,6 +319,11 @@ class SDXLTransformerBlock:
         return o, lse
 
     @staticmethod
+    def _q_out_scale() -> float:
+        """The q projections' output scale when it is folded into their GEMM epilogue (FOLD_Q_SCALE), else 1."""
+        return ops.attn_q_scale(0.125) if FOLD_Q_SCALE else 1.0
+
+    @staticmethod
     def _qs(q):
         """The attention kernels take q pre-multiplied by scale*log2(e) (include/vpt_hip.h)."""
         return ops.scale_bf16(q, ops.attn_q_scale(0.125))
@@ -344,8 +359,8 @@ class SDXLTransformerBlock:
 
     def _qkv_fwd(self, h1, Wqkv, save, ds=None):
         """q|k|v = h1 . [Wq; Wk; Wv]^T + [ds_q | ds_k | ds_v] . blockdiag(up_q, up_k, up_v)^T as ONE GEMM
-        (vpt_gemm_bf16_lora_grouped; each output column block is exactly its target's LoRALinear), then q pre-scaled
-        in place for the attention kernels. Returns column views (q, k, v) of the [M, 3 dim] output."""
+        (vpt_gemm_bf16_lora_grouped; each output column block is exactly its target's LoRALinear), q pre-scaled for
+        the attention kernels in the same epilogue (FOLD_Q_SCALE; else in place afterwards). Returns column views (q, k, v) of the [M, 3 dim] output."""
         M, D, L = h1.shape[0], self.inner, self.lin
         r = L[QKV[0]].down.shape[0]
         downs = [L[t].down for t in QKV]
@@ -363,9 +378,13 @@ class SDXLTransformerBlock:
                 ops.lora_proj(h1, L[t].down, True, dsg, alpha=L[t].scale)
             L[t]._saved = (h1, dsg) if save else None
         qkv = torch.empty(M, 3 * D, dtype=BF16, device=h1.device)
-        ops.gemm_lora_grouped(h1, Wqkv, ds, [L[t].up for t in QKV], qkv)
+        if FOLD_Q_SCALE:
+            ops.gemm_lora_grouped(h1, Wqkv, ds, [L[t].up for t in QKV], qkv, alpha=ops.attn_q_scale(0.125), alpha_cols=D)
+        else:
+            ops.gemm_lora_grouped(h1, Wqkv, ds, [L[t].up for t in QKV], qkv)
         q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
-        ops.scale_bf16_2d(q, ops.attn_q_scale(0.125), out=q)
+        if not FOLD_Q_SCALE:
+            ops.scale_bf16_2d(q, ops.attn_q_scale(0.125), out=q)
         return q, k, v
 
     def _qkv_bwd(self, dqkv, Wqkv):
@@ -411,12 +430,14 @@ class SDXLTransformerBlock:
             q, k, v = self._qkv_fwd(h1, Wb["attn1.qkv"], save, ds=ds1)
         else:
             h1, m1, r1 = ops.layernorm_fwd(x, *self.norm["norm1"])
-            q, k, v = (L[f"attn1.to_{c}"].forward(h1, save, W=Wb.get(f"attn1.to_{c}")) for c in "qkv")
-            q = self._qs(q)
+            q, k, v = (L[f"attn1.to_{c}"].forward(h1, save, W=Wb.get(f"attn1.to_{c}"),
+                                                  out_scale=self._q_out_scale() if c == "q" else 1.0) for c in "qkv")
+            q = q if FOLD_Q_SCALE else self._qs(q)
         o1, lse1 = self._attn_fwd(q, k, v, B, n, n)
         x1 = L["attn1.to_out.0"].forward(o1, save, resid=x, W=Wb.get("attn1.to_out.0"))
         h2, m2, r2, ds2 = self._ln_lora(x1, "norm2", ["attn2.to_q"])
-        q2 = self._qs(L["attn2.to_q"].forward(h2, save, W=Wb.get("attn2.to_q"), ds=ds2))
+        q2 = L["attn2.to_q"].forward(h2, save, W=Wb.get("attn2.to_q"), ds=ds2, out_scale=self._q_out_scale())
+        q2 = q2 if FOLD_Q_SCALE else self._qs(q2)
         if kv is not None:
             k2, v2 = kv
         else:
