@@ -268,6 +268,11 @@ int vpt_layernorm_bwd_lora(const void* dy, long lddy, const void* x, long ldx, c
  * writes d(h) | d(gate) into dx12 [M, 2F]; bf16 rounding of the reference's bf16 tensor graph. */
 int vpt_geglu_fwd(const void* x12, long ldx, int F, long M, void* out, void* stream);
 int vpt_geglu_bwd(const void* dy, const void* x12, long ldx, int F, long M, void* dx12, long lddx, void* stream);
+/* vpt_geglu_bwd (bit-identical dx12, dy [M][F] dense) and, in the same launch, the rank-16 LoRA projection of dx12
+ * through up [2F][16] (the ff.net.0.proj adapter): vs[m][j] = bf16(alpha * dx12[m] . up[:, j]) -- within bf16
+ * rounding of vpt_lora_proj(dx12, up, w_kmajor = 0) (16 partial sums instead of 4). F % 128 == 0. */
+int vpt_geglu_bwd_lora(const void* dy, const void* x12, long ldx, int F, int M, void* dx12, long lddx, const void* up,
+                       void* vs, long ldvs, float alpha, void* stream);
 /* NF4 weights in the bitsandbytes 0.48.2 layout (quant_type nf4, blocksize 64, compress_statistics):
  * packed uint8 [n/2] (first element in the high nibble), qabsmax uint8 [n/64], absmax2 f32 [ceil(n/64/256)],
  * code2 f32 [256] (signed dynamic map), offset f32 [1]. Dequant -> bf16 [n] in the original [out][in]

@@ -691,3 +691,22 @@ def test_gemm_lora_scaled_columns(ops, gn, geometry):
     torch.cuda.synchronize()
     assert rel(one, y) < 1e-2
     assert (one.float() - y).abs().max().item() <= y.abs().max().item() * 2 ** -7
+
+
+@pytest.mark.parametrize("M,F", [(4100, 5120), (333, 2560)])
+def test_geglu_bwd_lora(ops, M, F):
+    """vpt_geglu_bwd_lora: dx12 bit-identical to vpt_geglu_bwd; vs = alpha * dx12 . up within bf16 rounding of
+    vpt_lora_proj (another f32 summation order) and of fp32 math."""
+    dy, x12 = rnd(M, F, seed=190), rnd(M, 2 * F, seed=191)
+    up = rnd(2 * F, 16, scale=0.05, seed=192)
+    vs = torch.empty(M, 16, dtype=torch.bfloat16, device=DEV)
+    dx12 = ops.geglu_bwd_lora(dy, x12, up, 0.0625, vs)
+    ref = ops.geglu_bwd(dy, x12)
+    torch.cuda.synchronize()
+    assert torch.equal(dx12, ref)
+    vref = torch.empty(M, 16, dtype=torch.bfloat16, device=DEV)
+    ops.lora_proj(ref, up, False, vref, alpha=0.0625)
+    y = (ref.float() @ up.float()) * 0.0625
+    torch.cuda.synchronize()
+    assert rel(vs, y) < 5e-3 and rel(vs, vref) < 5e-3
+    assert (vs.float() - vref.float()).abs().max().item() <= y.abs().max().item() * 2 ** -6

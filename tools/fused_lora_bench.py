@@ -40,6 +40,16 @@ def main():
             "fused": timeit(lambda: ops.layernorm_lora_fwd(x, w, b, down, G, 0.0625, ds)),
             "pair": timeit(lambda: ops.lora_proj_grouped(ops.layernorm_fwd(x, w, b)[0], 0, down, 16 * D, G, True, ds)),
             "ln_only": timeit(lambda: ops.layernorm_fwd(x, w, b))}
+    for M, F in [(4096, 5120), (16384, 2560)]:
+        dy = torch.randn(M, F, device=dev).bfloat16()
+        x12 = torch.randn(M, 2 * F, device=dev).bfloat16()
+        up = (torch.randn(2 * F, 16, device=dev) * 0.05).bfloat16()
+        vs = torch.empty(M, 16, dtype=torch.bfloat16, device=dev)
+        dx12 = torch.empty_like(x12)
+        res[f"geglu_bwd_M{M}_F{F}"] = {
+            "fused": timeit(lambda: ops.geglu_bwd_lora(dy, x12, up, 0.0625, vs, dx12=dx12)),
+            "pair": timeit(lambda: ops.lora_proj(ops.geglu_bwd(dy, x12, dx12), up, False, vs, alpha=0.0625)),
+            "geglu_bwd_only": timeit(lambda: ops.geglu_bwd(dy, x12, dx12))}
     print(json.dumps(res, indent=1))
 
 

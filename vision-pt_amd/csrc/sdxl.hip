@@ -445,6 +445,106 @@ __global__ void geglu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __
   *reinterpret_cast<uint4*>(dx12 + m * lddx + F + c * 8) = pack8(og);
 }
 
+// GeGLU backward (as geglu_bwd_kernel: bit-identical dx12) and, in the same launch, the rank-16 LoRA projection of
+// its output through the up of the Linear that produced x12 (ff.net.0.proj): vs[m][j] = bf16(alpha * dx12[m] .
+// up[:, j]), up [2F][16] -- the input-gradient operand of that Linear's backward, without re-reading dx12 (2F wide).
+// 16 rows per block, GBW = 16 waves (4 per SIMD: the erf-heavy body needs the occupancy); wave w takes the
+// 128-column chunk pairs c = w, w + GBW, ... (columns [128c, +128) of dh and of dgate). Each lane computes exactly the
+// 8 elements of its MFMA A fragment (row lane & 15, columns 32s + 8 (lane >> 4) of k step s), so dx12 goes from
+// registers to memory and into the MFMAs with no LDS image; the two up chunks are transposed in turn through the
+// wave's LDS image as in lora_proj. The waves' partial sums meet in LDS in wave order (deterministic; a different
+// f32 summation order than vpt_lora_proj -- within bf16 rounding of it).
+constexpr int GBW = 16;
+constexpr int GBP = 136;  // padded transposed-up row (bf16)
+
+// up rows [r0, r0 + 128) ([K][16]) -> the wave's image ws [16][GBP] (two rows per lane)
+__device__ __forceinline__ void gb_up_chunk(const bf16_t* __restrict__ up, long r0, bf16_t* ws, int lane) {
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const int kr = lane + 64 * hh;
+    const bf16_t* ur = up + (r0 + kr) * 16;
+    const uint4 a0 = *reinterpret_cast<const uint4*>(ur);
+    const uint4 a1 = *reinterpret_cast<const uint4*>(ur + 8);
+    const uint32_t v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      ws[(2 * e) * GBP + kr] = (bf16_t)(v[e] & 0xffff);
+      ws[(2 * e + 1) * GBP + kr] = (bf16_t)(v[e] >> 16);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+  __builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(64 * GBW) void geglu_bwd_lora_kernel(const bf16_t* __restrict__ dy,
+                                                                 const bf16_t* __restrict__ x12, long ldx, int F, int M,
+                                                                 bf16_t* __restrict__ dx12, long lddx,
+                                                                 const bf16_t* __restrict__ up, bf16_t* __restrict__ vs,
+                                                                 long ldvs, float alpha) {
+  __shared__ __attribute__((aligned(16))) bf16_t wsa[GBW][16 * GBP];
+  __shared__ __attribute__((aligned(16))) floatx4 red[GBW][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g4 = lane >> 4, i = lane & 15;
+  bf16_t* ws = wsa[wid];
+  const long row0 = (long)blockIdx.x * 16;
+  const long row = row0 + i;
+  const bool row_ok = row < M;
+  const long rowc = row_ok ? row : (long)M - 1;
+  const bf16_t* dyr = dy + rowc * F + 8 * g4;
+  const bf16_t* xr = x12 + rowc * ldx + 8 * g4;
+  bf16_t* dxr = dx12 + rowc * lddx + 8 * g4;
+  const int nchp = F / 128;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int c = wid; c < nchp; c += GBW) {
+    uint4 d[4], h[4], gt[4], ph[4], pg[4];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int col = c * 128 + 32 * s2;
+      d[s2] = *reinterpret_cast<const uint4*>(dyr + col);
+      h[s2] = *reinterpret_cast<const uint4*>(xr + col);
+      gt[s2] = *reinterpret_cast<const uint4*>(xr + F + col);
+    }
+    gb_up_chunk(up, (long)c * 128, ws, lane);  // the dh half's up rows, while the loads above land
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      float fd[8], fh[8], fg[8], oh[8], og[8];
+      unpack8(d[s2], fd);
+      unpack8(h[s2], fh);
+      unpack8(gt[s2], fg);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        oh[e] = fd[e] * rbf(gelu_erf(fg[e]));
+        og[e] = rbf(fd[e] * fh[e]) * gelu_erf_grad(fg[e]);
+      }
+      ph[s2] = pack8(oh);
+      pg[s2] = pack8(og);
+      const int col = c * 128 + 32 * s2;
+      if (row_ok) {
+        *reinterpret_cast<uint4*>(dxr + col) = ph[s2];
+        *reinterpret_cast<uint4*>(dxr + F + col) = pg[s2];
+      }
+      const uint4 bh = *reinterpret_cast<const uint4*>(&ws[i * GBP + 32 * s2 + 8 * g4]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(ph[s2]), as_frag(bh), acc, 0, 0, 0);
+    }
+    gb_up_chunk(up, (long)F + c * 128, ws, lane);  // the dgate half's
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const uint4 bg = *reinterpret_cast<const uint4*>(&ws[i * GBP + 32 * s2 + 8 * g4]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(pg[s2]), as_frag(bg), acc, 0, 0, 0);
+    }
+  }
+  red[wid][lane] = acc;
+  __syncthreads();
+  if (wid != 0) return;
+#pragma unroll
+  for (int w2 = 1; w2 < GBW; ++w2) acc += red[w2][lane];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const long m = row0 + 4 * g4 + r;
+    if (m < M) vs[m * ldvs + i] = f2bf(acc[r] * alpha);
+  }
+}
+
 // ---------------------------------------------------------------- NF4
 __constant__ float kNF4[16] = {-1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f,
                                -0.28444138169288635f, -0.18477343022823334f, -0.09105003625154495f, 0.0f,
@@ -800,6 +900,19 @@ extern "C" int vpt_geglu_fwd(const void* x12, long ldx, int F, long M, void* out
   if (M == 0) return VPT_OK;
   hipLaunchKernelGGL(geglu_fwd_kernel, grid1(M * (F / 8)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x12, ldx,
                      F, M, (bf16_t*)out);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_geglu_bwd_lora(const void* dy, const void* x12, long ldx, int F, int M, void* dx12, long lddx,
+                                  const void* up, void* vs, long ldvs, float alpha, void* stream) {
+  VPT_CHECK_ARG(dy && x12 && dx12 && up && vs, "vpt_geglu_bwd_lora: null pointer");
+  VPT_CHECK_ARG(F > 0 && F % 128 == 0 && ldx % 8 == 0 && lddx % 8 == 0 && ldx >= 2L * F && lddx >= 2L * F && ldvs >= 16,
+                "vpt_geglu_bwd_lora: F % 128 == 0, 16-B leading dims >= 2F");
+  if (M <= 0) return VPT_OK;
+  hipLaunchKernelGGL(geglu_bwd_lora_kernel, dim3((M + 15) / 16), dim3(64 * GBW), 0, (hipStream_t)stream,
+                     (const bf16_t*)dy, (const bf16_t*)x12, ldx, F, M, (bf16_t*)dx12, lddx, (const bf16_t*)up,
+                     (bf16_t*)vs, ldvs, alpha);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

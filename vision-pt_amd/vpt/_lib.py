@@ -73,6 +73,7 @@ SIGNATURES: dict[str, list] = {
     "vpt_layernorm_bwd_lora": [P, L, P, L, P, P, P, P, L, P, L, I, I, P, P, L, F, P],
     "vpt_geglu_fwd": [P, L, I, L, P, P],
     "vpt_geglu_bwd": [P, P, L, I, L, P, L, P],
+    "vpt_geglu_bwd_lora": [P, P, L, I, I, P, L, P, P, L, F, P],
     "vpt_nf4_dequant": [P, P, P, P, P, L, P, P],
     "vpt_nf4_dequant_batch": [P, I, P],
     "vpt_scale_bf16_2d": [P, L, L, I, F, P, L, P],

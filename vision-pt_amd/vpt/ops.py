@@ -732,6 +732,20 @@ def geglu_bwd(dy, x12, dx12=None):
     return dx12
 
 
+def geglu_bwd_lora(dy, x12, up, alpha: float, vs, dx12=None):
+    """geglu_bwd and, in the same launch, vs = bf16(alpha * dx12 . up) (up [2F, 16]; csrc/sdxl.hip
+    geglu_bwd_lora_kernel). Returns dx12."""
+    M, F2 = x12.shape
+    _chk(up, BF16, "up")
+    if not (dy.is_contiguous() and up.is_contiguous() and up.shape == (F2, 16) and vs.stride(1) == 1
+            and vs.shape[1] >= 16):
+        raise ValueError("geglu_bwd_lora: dense dy [M, F], contiguous up [2F, 16], row-major vs with 16 columns")
+    dx12 = torch.empty_like(x12) if dx12 is None else dx12
+    call("vpt_geglu_bwd_lora", dy.data_ptr(), x12.data_ptr(), x12.stride(0), F2 // 2, M, dx12.data_ptr(),
+         dx12.stride(0), up.data_ptr(), vs.data_ptr(), vs.stride(0), float(alpha), stream())
+    return dx12
+
+
 def groupnorm_fwd(x, w, b, B, C, G, HW, out=None, mean=None, rstd=None, eps=1e-6):
     """x NCHW bf16 [B, C, HW] -> GroupNorm(G, C) output NCHW bf16; mean / rstd [B*G] f32 (for the backward)."""
     out = torch.empty_like(x) if out is None else out

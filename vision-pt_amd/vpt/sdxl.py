@@ -270,6 +270,8 @@ FUSED_LN_BWD_LORA = os.environ.get("VPT_LN_BWD_LORA", "1") != "0"  # the backwar
 # 1 = the attention q projections emit q * scale * log2(e) from their GEMM epilogue (one rounding);
 # 0 = a bf16 q, then a separate scaling pass (two roundings, one more launch per q)
 FOLD_Q_SCALE = os.environ.get("VPT_FOLD_Q_SCALE", "1") != "0"
+# 1 = the GeGLU backward also emits ff.net.0.proj's input-gradient LoRA operand (ops.geglu_bwd_lora)
+FUSED_GEGLU_LORA = os.environ.get("VPT_GEGLU_LORA", "1") != "0"
 
 
 def _adjacent(ts) -> bool:
@@ -470,8 +472,16 @@ class SDXLTransformerBlock:
         # the context needs a gradient)
         Wb = dequant_bases(L, [t for t in TARGETS if need_dctx or t not in ("attn2.to_k", "attn2.to_v")], self.device)
         dgg = L["ff.net.2"].backward(dy, W=Wb.get("ff.net.2"))
-        dx12 = ops.geglu_bwd(dgg, st["x12"])
-        dh3 = L["ff.net.0.proj"].backward(dx12, W=Wb.get("ff.net.0.proj"))
+        f0 = L["ff.net.0.proj"]
+        # fused at the 1280-channel stages (F = 5120: 52 vs 73 us for the pair, M = 4096); at F = 2560 its 20 chunk
+        # pairs over 16 waves run slower than the pair (128 vs 120 us, M = 16384; profiles/r03/r03zn_*)
+        if FUSED_GEGLU_LORA and f0.skinny and st["x12"].shape[1] % 256 == 0 and st["x12"].shape[1] >= 8192:
+            vs_f0 = torch.empty(dgg.shape[0], 16, dtype=BF16, device=self.device)
+            dx12 = ops.geglu_bwd_lora(dgg, st["x12"], f0.up, f0.scale, vs_f0)
+        else:
+            vs_f0 = None
+            dx12 = ops.geglu_bwd(dgg, st["x12"])
+        dh3 = f0.backward(dx12, W=Wb.get("ff.net.0.proj"), vs=vs_f0)
         dx2, vs_o2 = self._ln_bwd_lora(dh3, st["x2"], m3, r3, "norm3", dy, "attn2.to_out.0")
         do2 = L["attn2.to_out.0"].backward(dx2, W=Wb.get("attn2.to_out.0"), vs=vs_o2)
         D = self.inner
