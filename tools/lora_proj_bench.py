@@ -37,7 +37,7 @@ def main():
         up = (torch.randn(K, 16, device=dev) * 0.05).bfloat16()
         y = torch.empty(M, 16, dtype=torch.bfloat16, device=dev)
         for name, w, km in (("down", down, True), ("up", up, False)):
-            warm = timeit(lambda: ops.lora_proj(x, w, km, y))
+            warm = sorted(timeit(lambda: ops.lora_proj(x, w, km, y)) for _ in range(5))[2]
 
             def cold():
                 flush.zero_()
