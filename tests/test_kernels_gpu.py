@@ -577,6 +577,36 @@ def test_embedding(ops):
 
 
 # ------------------------------------------------------------------------------------ RAdamScheduleFree
+@pytest.mark.parametrize("gb", [False, True])
+@pytest.mark.parametrize("adam", [0, 1])
+def test_radam_sf_step_vector_path_bitwise_equals_scalar(ops, gb, adam):
+    """radam_sf_step runs 4 elements per thread when y / z / v / grad are aligned for it and one per thread
+    otherwise: the same update on the same values, once aligned and once at a 1-element offset (scalar path),
+    must agree bit for bit -- weight decay, both clippings, grad_scale and a ragged tail included."""
+    n = 100_003
+    g0 = torch.Generator().manual_seed(11)
+    y = (torch.randn(n, generator=g0) * 0.1).to(torch.bfloat16)
+    z = torch.randn(n, generator=g0) * 0.1
+    v = torch.rand(n, generator=g0) * 1e-3
+    g = torch.randn(n, generator=g0)
+    gdt = torch.bfloat16 if gb else torch.float32
+    coef = torch.tensor([0.7], device=DEV)
+    outs = []
+    for off in (0, 1):
+        def place(t, dt):
+            buf = torch.zeros(n + 1, dtype=dt, device=DEV)
+            buf[off:off + n] = t.to(dt).to(DEV)
+            return buf[off:off + n]
+        yy, zz, vv, gg = place(y, torch.bfloat16), place(z, torch.float32), place(v, torch.float32), place(g, gdt)
+        ops.radam_sf_step(yy, gg, zz, vv, beta2=0.999, bias_correction2=0.3, eps=1e-8, ckp1=0.2, adaptive_y_lr=-1e-3,
+                          lr=2e-3, decay=0.01, grad_scale=0.5, adam=adam, clip_coef=coef, clip_value=0.3)
+        outs.append((yy.cpu(), zz.cpu(), vv.cpu()))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a.view(torch.int32),
+                           b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32))
+
+
 @pytest.mark.parametrize("decay,silent", [(0.0, True), (0.05, False)])
 def test_radam_schedulefree_steps_vs_restatement(ops, decay, silent):
     """The fused optimizer (vpt.optim over radam_sf_step / sf_lerp / sf_init kernels) against the CPU

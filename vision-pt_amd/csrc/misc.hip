@@ -448,27 +448,78 @@ struct SfScalars {
   const float* clip_coef;  // device scalar (global-norm clip coefficient) or null
   float clip_value;        // clamp(g, -clip_value, clip_value) when > 0
 };
+// One element of the update (shared by the scalar and the 4-wide kernel, so both round identically).
+__device__ __forceinline__ void sf_elem(float g, float& vv, float& yy, float& zz, const SfScalars& s) {
+  g *= s.grad_scale;
+  // after_backward (for_training.py:98-109): clip_grad_norm_ then clip_grad_value_ on the (mean) gradient
+  if (s.clip_coef) g *= *s.clip_coef;
+  if (s.clip_value > 0.f) g = fminf(fmaxf(g, -s.clip_value), s.clip_value);
+  vv = vv * s.beta2 + (1.f - s.beta2) * g * g;
+  if (s.adam) g = g / (sqrtf(vv / s.bias_correction2) + s.eps);
+  if (s.decay != 0.f) g += s.decay * yy;
+  const float z0 = zz;
+  yy = bf2f(f2bf(yy + s.ckp1 * (z0 - yy)));  // y.lerp_(z, ckp1) on the bf16 parameter
+  yy = yy + s.adaptive_y_lr * g;
+  zz = z0 - s.lr * g;
+}
 // GB: the gradient arrives as bf16 (the all-reduced bf16 wire buffer, vpt.ddp.GradSync wire="bf16").
+template <bool GB>
+__device__ __forceinline__ float sf_grad(const void* grad, long i) {
+  return GB ? bf2f(reinterpret_cast<const bf16_t*>(grad)[i]) : reinterpret_cast<const float*>(grad)[i];
+}
 template <bool GB>
 __global__ void radam_sf_step_kernel(bf16_t* __restrict__ y, const void* __restrict__ grad, float* __restrict__ z,
                                      float* __restrict__ v, long n, SfScalars s) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  float g = (GB ? bf2f(reinterpret_cast<const bf16_t*>(grad)[i]) : reinterpret_cast<const float*>(grad)[i]) *
-            s.grad_scale;
-  // after_backward (for_training.py:98-109): clip_grad_norm_ then clip_grad_value_ on the (mean) gradient
-  if (s.clip_coef) g *= *s.clip_coef;
-  if (s.clip_value > 0.f) g = fminf(fmaxf(g, -s.clip_value), s.clip_value);
-  float vv = v[i] * s.beta2 + (1.f - s.beta2) * g * g;
+  float vv = v[i], yy = bf2f(y[i]), zz = z[i];
+  sf_elem(sf_grad<GB>(grad, i), vv, yy, zz, s);
   v[i] = vv;
-  if (s.adam) g = g / (sqrtf(vv / s.bias_correction2) + s.eps);
-  float yy = bf2f(y[i]);
-  if (s.decay != 0.f) g += s.decay * yy;
-  float zz = z[i];
-  yy = bf2f(f2bf(yy + s.ckp1 * (zz - yy)));  // y.lerp_(z, ckp1) on the bf16 parameter
-  yy = yy + s.adaptive_y_lr * g;
-  z[i] = zz - s.lr * g;
+  z[i] = zz;
   y[i] = f2bf(yy);
+}
+// 4 elements per thread (16-B z / v / f32-grad, 8-B y / bf16-grad accesses) when every base is aligned for
+// them: one element per lane moved 2-B y pieces and ran at ~4.4 TB/s. The last n % 4 go element-wise.
+template <bool GB>
+__global__ void radam_sf_step4_kernel(bf16_t* __restrict__ y, const void* __restrict__ grad, float* __restrict__ z,
+                                      float* __restrict__ v, long n, SfScalars s) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= n) return;
+  if (i + 4 > n) {
+    for (long j = i; j < n; ++j) {
+      float vv = v[j], yy = bf2f(y[j]), zz = z[j];
+      sf_elem(sf_grad<GB>(grad, j), vv, yy, zz, s);
+      v[j] = vv;
+      z[j] = zz;
+      y[j] = f2bf(yy);
+    }
+    return;
+  }
+  floatx4 g;
+  if (GB) {
+    const uint2 w = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(grad) + i);
+    g[0] = __uint_as_float(w.x << 16); g[1] = __uint_as_float(w.x & 0xffff0000u);
+    g[2] = __uint_as_float(w.y << 16); g[3] = __uint_as_float(w.y & 0xffff0000u);
+  } else {
+    g = *reinterpret_cast<const floatx4*>(reinterpret_cast<const float*>(grad) + i);
+  }
+  floatx4 vv = *reinterpret_cast<const floatx4*>(v + i), zz = *reinterpret_cast<const floatx4*>(z + i);
+  const uint2 yw = *reinterpret_cast<const uint2*>(y + i);
+  floatx4 yy;
+  yy[0] = __uint_as_float(yw.x << 16); yy[1] = __uint_as_float(yw.x & 0xffff0000u);
+  yy[2] = __uint_as_float(yw.y << 16); yy[3] = __uint_as_float(yw.y & 0xffff0000u);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float a = vv[e], b = yy[e], c = zz[e];
+    sf_elem(g[e], a, b, c, s);
+    vv[e] = a; yy[e] = b; zz[e] = c;
+  }
+  *reinterpret_cast<floatx4*>(v + i) = vv;
+  *reinterpret_cast<floatx4*>(z + i) = zz;
+  uint2 o;
+  o.x = (uint32_t)f2bf(yy[0]) | ((uint32_t)f2bf(yy[1]) << 16);
+  o.y = (uint32_t)f2bf(yy[2]) | ((uint32_t)f2bf(yy[3]) << 16);
+  *reinterpret_cast<uint2*>(y + i) = o;
 }
 
 __global__ void lerp_to_z_kernel(bf16_t* __restrict__ y, const float* __restrict__ z, long n, float w) {
@@ -738,12 +789,17 @@ extern "C" int vpt_radam_sf_step(void* y, const void* grad, int grad_bf16, float
   VPT_CHECK_ARG(y && grad && z && v && n >= 0 && clip_value >= 0.f, "vpt_radam_sf_step: bad args");
   if (n == 0) return VPT_OK;
   SfScalars s{beta2, bias_correction2, eps, ckp1, adaptive_y_lr, lr, decay, grad_scale, adam, clip_coef, clip_value};
-  if (grad_bf16)
-    hipLaunchKernelGGL(radam_sf_step_kernel<true>, grid1(n), dim3(256), 0, (hipStream_t)stream, (bf16_t*)y, grad, z, v,
-                       n, s);
+  auto al = [](const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; };
+  const bool vec = al(y, 8) && al(z, 16) && al(v, 16) && al(grad, grad_bf16 ? 8 : 16);
+  hipStream_t st = (hipStream_t)stream;
+  if (vec && grad_bf16)
+    hipLaunchKernelGGL(radam_sf_step4_kernel<true>, grid1((n + 3) / 4), dim3(256), 0, st, (bf16_t*)y, grad, z, v, n, s);
+  else if (vec)
+    hipLaunchKernelGGL(radam_sf_step4_kernel<false>, grid1((n + 3) / 4), dim3(256), 0, st, (bf16_t*)y, grad, z, v, n, s);
+  else if (grad_bf16)
+    hipLaunchKernelGGL(radam_sf_step_kernel<true>, grid1(n), dim3(256), 0, st, (bf16_t*)y, grad, z, v, n, s);
   else
-    hipLaunchKernelGGL(radam_sf_step_kernel<false>, grid1(n), dim3(256), 0, (hipStream_t)stream, (bf16_t*)y, grad, z,
-                       v, n, s);
+    hipLaunchKernelGGL(radam_sf_step_kernel<false>, grid1(n), dim3(256), 0, st, (bf16_t*)y, grad, z, v, n, s);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
