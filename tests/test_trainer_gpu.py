@@ -91,3 +91,12 @@ def test_ema_kernel_matches_bf16_reference_arithmetic(decay):
         ref = decay * ref + (1 - decay) * p  # get_ema_avg_fn on bf16 tensors (swa_utils)
     torch.cuda.synchronize()
     assert torch.equal(ema, ref)
+    # a 1-element offset takes the element-wise kernel (the 16-B path needs aligned bases): same result
+    buf_e = torch.zeros(p.numel() + 1, dtype=torch.bfloat16, device=DEV)
+    buf_p = torch.zeros_like(buf_e)
+    buf_e[1:] = ref
+    buf_p[1:] = p
+    ops.ema_update(ema, p, decay, False)
+    ops.ema_update(buf_e[1:], buf_p[1:], decay, False)
+    torch.cuda.synchronize()
+    assert torch.equal(ema, buf_e[1:])
