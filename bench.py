@@ -95,25 +95,23 @@ def make_batches(B: int, device, seed: int, buckets=BUCKETS):
     return out
 
 
-def cpu_baseline(budget_s: float = 20.0, buckets=BUCKETS, max_steps: int = 4):
-    """Times the CPU oracle (oracle/jit_oracle.py, a parity-pinned fp32 restatement of the
-    reference step; AdamW stands in for schedulefree which is not installed) on host cores."""
+def _cpu_leg(oc, B: int, buckets, n_classes: int, steps: int, budget_s: float):
+    """One CPU-oracle leg: 1 warm-up step, then up to `steps` timed steps (stopping early past budget_s) of the
+    fp32 restatement's training step (forward, x-loss, backward, AdamW: schedulefree is not installed)."""
     from oracle import jit_oracle as O
-    threads = torch.get_num_threads()
-    oc = O.jit_b16()
     model = O.OracleJiT(oc)
-    emb = torch.nn.Parameter(torch.randn(N_CLASSES + 1, 768) * 0.02)
+    emb = torch.nn.Parameter(torch.randn(n_classes + 1, oc.hidden_size) * 0.02)
     opt = torch.optim.AdamW(list(model.parameters()) + [emb], lr=1e-4)
     g = torch.Generator().manual_seed(0)
 
     def one(W, H):
-        batch = dict(image=(torch.rand(1, 3, H, W, generator=g) * 2 - 1).half(),
-                     noise=torch.randn(1, 3, H, W, generator=g).half(),
-                     t=(torch.randn(1, generator=g) * 0.8 - 0.8).sigmoid(),
-                     ids=torch.randint(0, N_CLASSES, (1, N_CTX), generator=g),
-                     mask=torch.ones(1, N_CTX, dtype=torch.long),
-                     original_size=torch.tensor([[H, W]]), target_size=torch.tensor([[H, W]]),
-                     crop_coords=torch.zeros(1, 2, dtype=torch.long))
+        batch = dict(image=(torch.rand(B, 3, H, W, generator=g) * 2 - 1).half(),
+                     noise=torch.randn(B, 3, H, W, generator=g).half(),
+                     t=(torch.randn(B, generator=g) * 0.8 - 0.8).sigmoid(),
+                     ids=torch.randint(0, n_classes, (B, N_CTX), generator=g),
+                     mask=torch.ones(B, N_CTX, dtype=torch.long),
+                     original_size=torch.tensor([[H, W]] * B), target_size=torch.tensor([[H, W]] * B),
+                     crop_coords=torch.zeros(B, 2, dtype=torch.long))
         loss, _ = O.train_step_loss(model, emb, batch, "image")
         loss.backward()
         opt.step()
@@ -121,17 +119,38 @@ def cpu_baseline(budget_s: float = 20.0, buckets=BUCKETS, max_steps: int = 4):
 
     one(*buckets[0])  # warm-up at the sample's own size (allocator, threads)
     n, t0 = 0, time.perf_counter()
-    while True:
+    while n < steps:
         W, H = buckets[n % len(buckets)]
         one(W, H)
         n += 1
-        if time.perf_counter() - t0 > budget_s or n >= max_steps:
+        if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
-    area = "1024^2-area buckets" if buckets is BUCKETS else f"{buckets[0][0]}x{buckets[0][1]}"
-    return dict(value=round(n / dt, 5), unit="img/s", cores=threads, kind="port",
-                sample=f"{n} JiT-B/16 training steps (B=1, {area}, fp32, AdamW) on the CPU oracle, "
-                       f"{dt:.1f} s, torch threads={threads}")
+    return n, dt
+
+
+def cpu_baseline(workload: str = "c3"):
+    """Times the CPU oracle (oracle/jit_oracle.py, a parity-pinned fp32 restatement of the reference step; AdamW
+    stands in for schedulefree, which is not installed) on the host cores, BASELINE.md §4.3's three legs: C1 (JiT
+    tiny 256^2, B=4), JiT-B/16 512^2 B=1 and JiT-B/16 at the 1024^2-area buckets B=1, each 1 warm-up + 3 timed steps.
+    `value` is the leg of the benched workload (c3: the 1024^2 buckets; c2: 512^2), in img/s."""
+    from oracle import jit_oracle as O
+    from tests.golden import golden_configs as GC
+    threads = torch.get_num_threads()
+    legs = {}
+    for name, oc, B, bk, ncls, budget in (("c1_tiny_256sq_b4", GC.c1_config(), 4, [(256, 256)], 1000, 10.0),
+                                          ("jit_b16_512sq_b1", O.jit_b16(), 1, BUCKETS_C2, N_CLASSES, 10.0),
+                                          ("jit_b16_1024area_b1", O.jit_b16(), 1, BUCKETS, N_CLASSES, 25.0)):
+        n, dt = _cpu_leg(oc, B, bk, ncls, steps=3, budget_s=budget)
+        legs[name] = dict(value=round(n * B / dt, 5), unit="img/s", steps=n, seconds=round(dt, 2), batch=B,
+                          buckets_wh=bk)
+    main = legs["jit_b16_512sq_b1" if workload == "c2" else "jit_b16_1024area_b1"]
+    area = "512^2" if workload == "c2" else "1024^2-area buckets"
+    return dict(value=main["value"], unit="img/s", cores=threads, kind="port",
+                sample=f"{main['steps']} JiT-B/16 training steps (B=1, {area}, fp32, AdamW) on the CPU oracle after 1 "
+                       f"warm-up, {main['seconds']} s, torch threads={threads}; legs = BASELINE.md §4.3's C1 / 512^2 / "
+                       f"1024^2 samples",
+                legs=legs)
 
 
 def roofline_entry(name: str, st: dict, workload: str = "c3"):
@@ -151,8 +170,8 @@ def roofline_entry(name: str, st: dict, workload: str = "c3"):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)    # >= 10 warm-up, >= 50 timed steps
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: 8 for c3, 16 for c2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--breakdown", default=None, help="write per-shape GEMM probe totals (JSON) to this file")
@@ -305,7 +324,7 @@ def main():
         "final_loss": round(loss, 5),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(buckets=buckets)
+        result["cpu_baseline"] = cpu_baseline(args.workload)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -314,34 +333,40 @@ def main():
 
 
 def bench_c5(args):
-    """BASELINE config 5 on one GPU: the SDXL flow-matching QLoRA step (train/sdxl/flow_match.py:109-174) at
-    1024^2 (latents 4 x 128 x 128), batch 4 (configs/sdxl/flow_match/config.yml): t ~ scale_shift_sigmoid,
-    noising, the UNet's 11 SpatialTransformers (70 blocks, 700 LoRA r=16 targets over NF4 bases, dequantised per
-    call as bitsandbytes' MatMul4Bit does -- vpt.sdxl.BASE_MODES, VPT_NF4_BASE) inside a frozen skeleton of the UNet's topology (its ResNet / conv path is outside SURVEY §8),
-    velocity MSE, backward, RAdamScheduleFree on the adapters (vpt/sdxl_flow.py)."""
+    """BASELINE config 5 on one GPU: the SDXL flow-matching QLoRA step (train/sdxl/flow_match.py:109-174) on the
+    reference's aspect-ratio buckets (configs/sdxl/flow_match/config.yml:46-50: base 1024, step 128, min 384; the
+    five nearest to square, 896x1152 ... 1408x768, latents / 8), batch 4, drawn per step from one seeded shuffled
+    order: t ~ scale_shift_sigmoid, noising, the UNet's 11 SpatialTransformers (70 blocks, 700 LoRA r=16 targets over
+    NF4 bases, dequantised per call as bitsandbytes' MatMul4Bit does -- vpt.sdxl.BASE_MODES) inside a frozen skeleton
+    of the UNet's topology (its ResNet / conv path is outside SURVEY §8), velocity MSE, backward, RAdamScheduleFree on
+    the adapters (vpt/sdxl_flow.py)."""
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         raise SystemExit("--workload c5 is a 1-GPU configuration")
     torch.cuda.set_device(0)
     from vpt import ops
-    from vpt.sdxl_flow import SDXLFlowMatchQLoRA
+    from vpt.sdxl import DEFAULT_BASE_MODE
+    from vpt.sdxl_flow import SDXL_BUCKETS_5, SDXLFlowMatchQLoRA
     B = 4
     m = SDXLFlowMatchQLoRA(B=B, device="cuda", seed=0)
-    lat, ctx, pooled, sizes = m.make_inputs(seed=1)
-    for _ in range(args.warmup):
-        m.step(lat, ctx, pooled, sizes)
+    batches = [m.make_inputs(seed=1 + i, latent=(H // 8, W // 8)) for i, (W, H) in enumerate(SDXL_BUCKETS_5)]
+    nb = len(batches)
+    order = shared_order(nb, args.warmup + args.steps + nb, 1, 0, seed=11)
+    for i in range(args.warmup):
+        m.step(*batches[order[i]])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        m.step(lat, ctx, pooled, sizes)
+    for i in range(args.warmup, args.warmup + args.steps):
+        m.step(*batches[order[i]])
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     loss = m.loss.item()
-    # probe pass after the timed region: NF4 GEMM and attention launches timed with HIP events
+    # probe pass after the timed region (one step per bucket): GEMM and attention launches timed with HIP events
     probes = {k: ops.KernelProbe(k) for k in ("gemm_lora", "gemm_nf4", "attn_fwd", "attn_bwd", "gemm", "nf4_dequant")}
     ops.PROBES.update(probes)
     for p in probes.values():
         p.active = True
-    m.step(lat, ctx, pooled, sizes)
+    for i in range(nb):
+        m.step(*batches[i])
     torch.cuda.synchronize()
     for p in probes.values():
         p.active = False
@@ -349,24 +374,26 @@ def bench_c5(args):
     kern = {}
     for k, pr in probes.items():
         n, ms, fl = pr.summary()
+        n_step = n / nb
         if k == "nf4_dequant":  # HBM-bound: algorithmic bytes / time
-            kern[k] = dict(launches=n, mean_ms=round(ms, 4), total_ms=round(n * ms, 3),
+            kern[k] = dict(launches_per_step=n_step, mean_ms=round(ms, 4), ms_per_step=round(n_step * ms, 3),
                            gb_s=round(fl / (ms * 1e-3) / 1e9, 1) if ms else 0.0,
                            frac=round(fl / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 3) if ms else 0.0)
         else:
-            kern[k] = dict(launches=n, mean_ms=round(ms, 4), total_ms=round(n * ms, 3),
+            kern[k] = dict(launches_per_step=n_step, mean_ms=round(ms, 4), ms_per_step=round(n_step * ms, 3),
                            tflops=round(fl / (ms * 1e-3) / 1e12, 2) if ms else 0.0)
-    if args.breakdown:  # per-shape totals of the base+LoRA GEMMs over the probed step
+    if args.breakdown:  # per-shape totals of the base+LoRA GEMMs over the probed steps
         rows = {k: dict(launches=n, total_ms=round(t, 3), tflops=round(w / (t * 1e-3) / 1e12, 1))
                 for k, (n, t, w) in sorted(probes["gemm_lora"].by_key().items(), key=lambda kv: -kv[1][1])}
         json.dump(rows, open(args.breakdown, "w"), indent=1)
     # headline roofline: the MFMA op with the largest total time in the step
-    dom = max((k for k in kern if k != "nf4_dequant"), key=lambda k: kern[k]["total_ms"])
+    dom = max((k for k in kern if k != "nf4_dequant"), key=lambda k: kern[k]["ms_per_step"])
     n, ms, fl = probes[dom].summary()
     tf = fl / (ms * 1e-3) / 1e12 if ms else 0.0
-    step_tf = m.flops_per_step() / 1e12
+    traffic, tsrc = measured_traffic(dom, "c5")
+    step_tf = sum(m.flops_per_step((H // 8, W // 8)) for (W, H) in SDXL_BUCKETS_5) / nb / 1e12
     res = {
-        "metric": "train images/sec, SDXL QLoRA r=16 flow-matching step (1024^2, latents 4x128x128), 1 MI355X",
+        "metric": "train images/sec, SDXL QLoRA r=16 flow-matching step (1024^2 bucketed, 5 buckets), 1 MI355X",
         "value": round(B * args.steps / dt, 3), "unit": "img/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "bf16 (NF4 weights)", "data": "synthetic latents / text context / pooled output, random-init weights",
@@ -374,14 +401,16 @@ def bench_c5(args):
                                "v = UNet(z, 1000 t, ctx 231x2048, pooled, sizes), loss = mse(v, eps - x); the UNet's "
                                "11 SpatialTransformers (70 blocks, 700 LoRA targets) with the reference's "
                                "conditioning path, its ResNet / conv / resample path replaced by frozen "
-                               "pixel-(un)shuffle + Linear maps (outside SURVEY §8); VAE and text encoders not run",
+                               "pixel-(un)shuffle + Linear maps (outside SURVEY §8, calibrated to unit-RMS outputs); "
+                               "VAE and text encoders not run",
+                   "buckets_wh": SDXL_BUCKETS_5, "bucket_rule": "base 1024, step 128, min 384 (config.yml:46-50); "
+                   "the five nearest to square, one seeded shuffled order",
                    "global_batch": B, "lora_rank": 16, "lora_alpha": 1.0, "adapter_params": m.n_adapter_params(),
                    "loss": "flow-matching velocity MSE (loss_with_predicted_velocity)",
-                   "nf4_base": __import__("vpt.sdxl", fromlist=["x"]).DEFAULT_BASE_MODE,
-                   "optimizer": "RAdamScheduleFree (fused HIP)"},
+                   "nf4_base": DEFAULT_BASE_MODE, "optimizer": "RAdamScheduleFree (fused HIP)"},
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(tf / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                     "mean_launch_ms": round(ms, 4), "launches_per_step": n},
+                     "unit": "TFLOP/s", "frac": round(tf / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                     "traffic_source": tsrc, "mean_launch_ms": round(ms, 4), "launches_per_step": n / nb},
         "kernels": kern,
         "model_tflops_per_step": round(step_tf, 3), "model_tflops_per_s": round(step_tf * args.steps / dt, 2),
         "mfu": round(step_tf * args.steps / dt / PEAK_BF16_TFLOPS, 4), "final_loss": round(loss, 5),

@@ -352,7 +352,8 @@ int vpt_lora_wgrad_partial_batch(const VptLoraWgradJob* jobs, int njobs, void* s
 /* SpatialTransformer (src/models/sdxl/denoiser.py:283-365) around the transformer blocks:
  * GroupNorm(G, C, eps) on NCHW bf16 [B][C][HW] (f32 statistics mean / rstd [B*G] saved for the backward;
  * output NCHW bf16), its input gradient (affine weights frozen under QLoRA; dres: + a second NCHW gradient),
- * and dst[b][s][r] = src[b][r][s] (+ add) -- the NCHW <-> token-major permutes, the residual add fused. */
+ * and dst[b][s][r] = src[b][r][s] (+ add) -- the NCHW <-> token-major permutes, the residual add fused (R, S
+ * multiples of 8: any aspect-ratio bucket's stage HW). */
 int vpt_groupnorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int B, int C,
                       int G, long HW, float eps, void* stream);
 int vpt_groupnorm_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const void* w,

@@ -104,3 +104,136 @@ def test_two_ranks_real_engine_gradient_mean():
     # hook order = backward completion order: final layer first, then blocks last to first
     assert out[0][2] == ["final"] + [f"block{i}" for i in reversed(range(cfg.depth))]
     assert sum(hi - lo for lo, hi in out[0][3]) == tr.engine.layout.total
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# The exact path bench.py runs at N > 1: GradSync.arm with overlap=True (each bucket stepped on a side HIP stream the
+# moment its reduction lands, during the rest of the backward), the real RAdamScheduleFreeFlat.apply_range, and
+# clipping (src/models/for_training.py:98-109: clip_grad_norm_ -> device grad_sumsq / clip_coef kernels; clip_grad_value_
+# -> the clamp inside the optimizer kernel). Reference: src/trainer/common.py:219, 376-388.
+LR = 1e-2
+
+
+def _opt(tr):
+    from vpt.optim import RAdamScheduleFreeFlat
+    # silent_sgd_phase=False: the first steps update (SGD phase) instead of holding still, so 2 steps move z and y
+    opt = RAdamScheduleFreeFlat(tr.engine.params, tr.engine.grads, lr=LR, silent_sgd_phase=False)
+    opt.train()
+    return opt
+
+
+def _run_steps(tr, opt, sync, b, sl, dev, overlap: bool, steps: int = 2, capture=None):
+    for k in range(steps):
+        s = opt.begin_step()
+        fn = lambda lo, hi, sc, g, **kw: opt.apply_range(s, lo, hi, sc, g, **kw)  # noqa: E731
+        if overlap:
+            sync.arm(fn)
+        _step(tr, b, sl, dev, on_ready=sync.launch)
+        sync.launch_rest()
+        if overlap:
+            sync.finish()
+        else:
+            sync.finish(fn)
+        opt.end_step(s)
+        if capture is not None and k == 0:
+            torch.cuda.synchronize()
+            capture(sync)
+
+
+def _worker_exact(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from vpt.ddp import GradSync, grad_buckets
+    b = _batch(dev)
+    sl = slice(rank * 2, rank * 2 + 2)
+    # clip thresholds that bind: from this step's reduced mean gradient (identical on both ranks)
+    tr, cfg = _trainer(dev)
+    sync = GradSync(tr.engine.grads, grad_buckets(tr.engine.layout, cfg.depth), wire="bf16", overlap=False)
+    _step(tr, b, sl, dev, on_ready=sync.launch)
+    sync.launch_rest()
+    gmean = torch.zeros_like(tr.engine.grads)
+    sync.finish(lambda lo, hi, sc, g: gmean[lo:hi].copy_(g.float() * sc))
+    torch.cuda.synchronize()
+    max_norm = 0.5 * gmean.norm().item()
+    max_value = 0.25 * gmean.abs().max().item()
+    res = {"max_norm": max_norm, "max_value": max_value}
+    for mode in ("none", "norm", "value"):
+        kw = dict(clip_grad_norm=max_norm if mode == "norm" else None,
+                  clip_grad_value=max_value if mode == "value" else None)
+        out = {}
+        for path in ("overlap", "serial"):
+            tr, cfg = _trainer(dev)
+            opt = _opt(tr)
+            sync = GradSync(tr.engine.grads, grad_buckets(tr.engine.layout, cfg.depth), wire="bf16",
+                            overlap=path == "overlap", **kw)
+            cap = {}
+
+            def capture(sy, cap=cap):
+                if sy.clip_norm is not None:
+                    cap["coef"] = sy.coef.item()
+                    cap["norm"] = sy.norm.item()
+                    cap["gmean"] = (sy.comm.float() * sy.scale).cpu()
+            _run_steps(tr, opt, sync, b, sl, dev, overlap=path == "overlap", capture=capture)
+            torch.cuda.synchronize()
+            out[path] = dict(y=tr.engine.params.cpu(), z=opt.z.cpu(), side=sync.side is not None, **cap)
+        res[mode] = out
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_overlapped_optimizer_and_clipping_exact_path():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_exact, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    out.sort(key=lambda t: t[0])
+    r0, r1 = out[0][1], out[1][1]
+    dev = torch.device("cuda", 0)
+    from vpt.ddp import GradSync, grad_buckets
+    for mode in ("none", "norm", "value"):
+        a0 = r0[mode]
+        assert a0["overlap"]["side"] and not a0["serial"]["side"]
+        # (1) overlap on the side stream == the serial per-bucket path, bitwise (parameters and the f32 z state),
+        #     and both ranks hold identical parameters
+        for k in ("y", "z"):
+            assert torch.equal(a0["overlap"][k], a0["serial"][k]), (mode, k)
+            assert torch.equal(a0["overlap"][k], r1[mode]["overlap"][k]), (mode, k)
+        # (2) vs ONE rank stepping the whole B=4 batch (same init, same clipping thresholds): within the bf16-wire bar
+        #     on the optimizer's f32 z state (z moves by -lr * clipped g per SGD-phase step; y is bf16-quantised)
+        tr, cfg = _trainer(dev)
+        y_init = tr.engine.params.float().cpu()
+        opt = _opt(tr)
+        kw = dict(clip_grad_norm=r0["max_norm"] if mode == "norm" else None,
+                  clip_grad_value=r0["max_value"] if mode == "value" else None)
+        sync = GradSync(tr.engine.grads, grad_buckets(tr.engine.layout, cfg.depth), wire="bf16", overlap=False, **kw)
+        _run_steps(tr, opt, sync, _batch(dev), slice(0, 4), dev, overlap=False)
+        torch.cuda.synchronize()
+        dz_ref = opt.z.cpu() - y_init
+        dz = a0["overlap"]["z"] - y_init
+        assert dz_ref.norm() > 0
+        assert ((dz - dz_ref).norm() / dz_ref.norm()).item() < 8e-3, mode
+    # the value clamp binds (else "value" would equal "none")
+    assert not torch.equal(r0["value"]["overlap"]["z"], r0["none"]["overlap"]["z"])
+    # (3) the clip coefficient the HIP kernels formed == torch.nn.utils.clip_grad_norm_ on the reduced mean gradient
+    cap = r0["norm"]["overlap"]
+    g = cap["gmean"]
+    p = torch.nn.Parameter(torch.zeros_like(g))
+    p.grad = g.clone()
+    total = torch.nn.utils.clip_grad_norm_([p], r0["max_norm"]).item()
+    ref_coef = min(1.0, r0["max_norm"] / (total + 1e-6))
+    assert abs(cap["norm"] - total) <= 1e-5 * total, (cap["norm"], total)
+    assert abs(cap["coef"] - ref_coef) <= 1e-5 * ref_coef and cap["coef"] < 1.0, (cap["coef"], ref_coef)
+    assert torch.allclose(p.grad, g * ref_coef, rtol=1e-5, atol=0)
+    assert r0["norm"]["serial"]["coef"] == cap["coef"]

@@ -409,10 +409,12 @@ def test_sdxl_spatial_transformer_matches_reference_bf16():
     assert not bad and len(grads) == 2 * 10 * depth, bad
 
 
-@pytest.mark.parametrize("B,C,HW", [(2, 640, 4096), (3, 1280, 1024)])
+@pytest.mark.parametrize("B,C,HW", [(2, 640, 4096), (3, 1280, 1024), (2, 640, 56 * 72), (2, 1280, 28 * 36),
+                                    (1, 1280, 24 * 44)])
 def test_groupnorm_and_transpose(ops, B, C, HW):
     """GroupNorm(32, C, eps 1e-6) fwd / input-grad (frozen affine) vs torch fp32, and the NCHW<->token
-    transposes (bit-exact) with the residual add, at SDXL's two stage shapes."""
+    transposes (bit-exact) with the residual add, at SDXL's two stage shapes of the square 1024^2 bucket and of the
+    896x1152 / 768x1408 buckets (HW not a multiple of the 64 x 64 transpose tile)."""
     G = 32
     x = rnd(B, C, HW, seed=30)
     w = (1 + rnd(C, scale=0.1, seed=31).float()).bfloat16()

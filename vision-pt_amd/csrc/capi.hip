@@ -15,6 +15,8 @@ extern "C" void vpt_set_error(const char* msg) {
 
 extern "C" const char* vpt_last_error_string(void) { return g_err; }
 
-extern "C" int vpt_abi_version(void) { return 2; }  // 2: attention takes nk (cross-attention)
+// 2: attention takes nk (cross-attention). 3: vpt_radam_sf_step takes (clip_coef, clip_value) before the stream and
+// vpt_ema_update takes one_minus_decay before `first` -- a caller built against ABI 2 must not bind ABI 3.
+extern "C" int vpt_abi_version(void) { return 3; }
 
-extern "C" const char* vpt_build_info(void) { return "vpt_hip gfx950 (CDNA4) bf16-MFMA abi=2"; }
+extern "C" const char* vpt_build_info(void) { return "vpt_hip gfx950 (CDNA4) bf16-MFMA abi=3"; }

@@ -1996,20 +1996,13 @@ extern "C" int vpt_lora_proj_grouped(const void* X, long ldx, long x_goff, const
 
 // Rows per split slab at least: 2048 -- in the config-5 step the batched slab + reduce launches take 5.29 ms per
 // step at 2048, 5.43 at 1024, 6.09 at 256 (rocprof, profiles/r03/r03zt, r03zu): fewer, longer slab blocks and
-// fewer slabs to sum. VPT_LORA_WGRAD_ROWS overrides (A/B).
-static int lora_wgrad_min_rows() {
-  static const int r = [] {
-    const char* e = getenv("VPT_LORA_WGRAD_ROWS");
-    const int v = e ? atoi(e) : 2048;
-    return v >= 128 && v <= 16384 ? v : 2048;
-  }();
-  return r;
-}
+// fewer slabs to sum. A constant: the library holds no process-wide switches.
+constexpr int kLoraWgradMinRows = 2048;
 
 static int lora_wgrad_splits(int M, int N) {
   const int nb = N / 64;
   int splits = 1024 / (nb > 0 ? nb : 1);
-  const int mr = lora_wgrad_min_rows();
+  const int mr = kLoraWgradMinRows;
   const int maxs = (M + mr - 1) / mr;
   return splits < 1 ? 1 : (splits > maxs ? maxs : splits);
 }

@@ -797,24 +797,29 @@ __global__ __launch_bounds__(256) void groupnorm_bwd_kernel(const bf16_t* __rest
 }
 
 // dst[b][s][r] = src[b][r][s] (+ add[b][s][r]), bf16, 64 x 64 tiles through LDS: the NCHW <-> token-major
-// permutes of SpatialTransformer.forward (denoiser.py:339-345, 356-363), the residual add fused.
+// permutes of SpatialTransformer.forward (denoiser.py:339-345, 356-363), the residual add fused. R and S are
+// multiples of 8 (16-B chunks); edge tiles (aspect-ratio buckets: HW = 28 x 36 = 1008 tokens) guard by chunk.
 __global__ __launch_bounds__(256) void transpose_add_kernel(const bf16_t* __restrict__ src, const bf16_t* __restrict__ add,
                                                             bf16_t* __restrict__ dst, int R, int S) {
   __shared__ float t[64][65];
   const int b = blockIdx.z, r0 = blockIdx.y * 64, s0 = blockIdx.x * 64, tid = threadIdx.x;
+  const int nr = min(64, R - r0), ns = min(64, S - s0);
   const bf16_t* sb = src + (long)b * R * S;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {  // 64 rows x 8 chunks of 8
     const int idx = tid + 256 * k, rr = idx >> 3, ch = idx & 7;
     float v[8];
-    unpack8(*reinterpret_cast<const uint4*>(sb + (long)(r0 + rr) * S + s0 + ch * 8), v);
+    if (rr < nr && ch * 8 < ns) {
+      unpack8(*reinterpret_cast<const uint4*>(sb + (long)(r0 + rr) * S + s0 + ch * 8), v);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) t[rr][ch * 8 + e] = v[e];
+      for (int e = 0; e < 8; ++e) t[rr][ch * 8 + e] = v[e];
+    }
   }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int idx = tid + 256 * k, ss = idx >> 3, ch = idx & 7;
+    if (ss >= ns || ch * 8 >= nr) continue;
     const long o = (long)b * R * S + (long)(s0 + ss) * R + r0 + ch * 8;
     float v[8];
 #pragma unroll
@@ -993,8 +998,8 @@ extern "C" int vpt_groupnorm_bwd(const void* dy, const void* x, const float* mea
 
 extern "C" int vpt_transpose_add(const void* src, const void* add, void* dst, int B, int R, int S, void* stream) {
   VPT_CHECK_ARG(src && dst && src != dst, "vpt_transpose_add: null or aliased pointer");
-  VPT_CHECK_ARG(B > 0 && R % 64 == 0 && S % 64 == 0, "vpt_transpose_add: R, S multiples of 64");
-  hipLaunchKernelGGL(transpose_add_kernel, dim3(S / 64, R / 64, B), dim3(256), 0, (hipStream_t)stream,
+  VPT_CHECK_ARG(B > 0 && R > 0 && S > 0 && R % 8 == 0 && S % 8 == 0, "vpt_transpose_add: R, S multiples of 8");
+  hipLaunchKernelGGL(transpose_add_kernel, dim3((S + 63) / 64, (R + 63) / 64, B), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)src, (const bf16_t*)add, (bf16_t*)dst, R, S);
   VPT_LAUNCH_CHECK();
   return VPT_OK;

@@ -154,6 +154,9 @@ def _load(path: Path, diag: bool = False) -> C.CDLL:
 DIAG = os.environ.get("VPT_DIAG", "0") == "1"
 LIB_PATH = LIB_DIAG if DIAG else LIB
 lib = _load(LIB_PATH, DIAG)
+ABI_VERSION = 3  # the signatures in SIGNATURES / include/vpt_hip.h
+if lib.vpt_abi_version() != ABI_VERSION:
+    raise ImportError(f"{LIB_PATH}: ABI {lib.vpt_abi_version()} != {ABI_VERSION} expected by these bindings; rebuild it")
 
 
 def call(name: str, *args):

@@ -9,7 +9,6 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
-import os
 
 import torch
 
@@ -764,7 +763,7 @@ def groupnorm_bwd(dy, x, mean, rstd, w, B, C, G, HW, dres=None, dx=None):
 
 
 def transpose_add(src, B, R, S, add=None, out=None):
-    """out[b][s][r] = src[b][r][s] (+ add[b][s][r]) for bf16 src [B, R, S] (R, S multiples of 64)."""
+    """out[b][s][r] = src[b][r][s] (+ add[b][s][r]) for bf16 src [B, R, S] (R, S multiples of 8)."""
     out = torch.empty(B, S, R, dtype=BF16, device=src.device) if out is None else out
     call("vpt_transpose_add", src.data_ptr(), _p(add), out.data_ptr(), B, R, S, stream())
     return out
@@ -985,8 +984,10 @@ class _LoraBatch:
 
 
 _LORA_BATCH: _LoraBatch | None = None
-# A/B knob: 0 = each target's slab launch at its call (round-2 behaviour); default: deferred to the block's end
-_LORA_DEFER = os.environ.get("VPT_LORA_DEFER", "1") != "0"
+# False = each target's slab launch at its call (round-2 behaviour); default: deferred to the block's end.
+# Module attributes, not environment switches: tools/ A/B scripts assign them in-process.
+_LORA_DEFER = True
+_LORA_BATCHED = True
 
 
 @contextlib.contextmanager
@@ -994,7 +995,7 @@ def lora_wgrad_batch():
     """Within the block, lora_wgrad2 only writes its split-M slabs (each target into its own workspace) and the
     reduces run batched at exit (or every 32 jobs): same results, ~1/16 of the reduce launches."""
     global _LORA_BATCH
-    if os.environ.get("VPT_LORA_BATCH", "1") == "0":  # A/B knob (tools/gpu_c5b.sh): per-target reduces
+    if not _LORA_BATCHED:  # per-target reduces (A/B: tools/c5_knob_ab.py)
         yield
         return
     outer = _LORA_BATCH

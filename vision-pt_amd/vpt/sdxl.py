@@ -14,7 +14,6 @@ a30  SDXLTransformerBlock: TransformerBlock.forward (src/models/sdxl/denoiser.py
 
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -103,7 +102,7 @@ class NF4Weight:
 #              memory-lean variant, ~1.5x slower on the config-5 shapes).
 # All three give the same dequantised values; "dequant" and "resident" give bitwise identical outputs.
 BASE_MODES = ("dequant", "resident", "inline")
-DEFAULT_BASE_MODE = os.environ.get("VPT_NF4_BASE", "dequant")
+DEFAULT_BASE_MODE = "dequant"
 _SCRATCH: dict = {}  # (device, "call" | "block") -> bf16 dequant scratch, grown on demand
 
 
@@ -264,14 +263,20 @@ class LoRALinearNF4:
         return vs
 
 
-# A/B knob: 0 = LayerNorm (forward / backward) and the LoRA projections of its output as separate launches
-FUSED_LN_LORA = os.environ.get("VPT_LN_LORA", "1") != "0"
-FUSED_LN_BWD_LORA = os.environ.get("VPT_LN_BWD_LORA", "1") != "0"  # the backward half alone (A/B)
-# 1 = the attention q projections emit q * scale * log2(e) from their GEMM epilogue (one rounding);
-# 0 = a bf16 q, then a separate scaling pass (two roundings, one more launch per q)
-FOLD_Q_SCALE = os.environ.get("VPT_FOLD_Q_SCALE", "1") != "0"
-# 1 = the GeGLU backward also emits ff.net.0.proj's input-gradient LoRA operand (ops.geglu_bwd_lora)
-FUSED_GEGLU_LORA = os.environ.get("VPT_GEGLU_LORA", "1") != "0"
+# Module attributes (tools/c5_knob_ab.py assigns them in-process for A/B runs; no environment switches).
+# False = LayerNorm (forward / backward) and the LoRA projections of its output as separate launches
+FUSED_LN_LORA = True
+FUSED_LN_BWD_LORA = True  # the backward half alone
+# True = the attention q projections emit q * scale * log2(e) from their GEMM epilogue (one rounding);
+# False = a bf16 q, then a separate scaling pass (two roundings, one more launch per q)
+FOLD_Q_SCALE = True
+# True = the GeGLU backward also emits ff.net.0.proj's input-gradient LoRA operand (ops.geglu_bwd_lora)
+FUSED_GEGLU_LORA = True
+
+
+def _ctx_key(ctx: torch.Tensor) -> tuple:
+    """Identity of a context tensor for SDXLTransformerBlock.ctx_kv (storage address, shape, strides, version)."""
+    return (ctx.data_ptr(), tuple(ctx.shape), tuple(ctx.stride()), ctx._version)
 
 
 def _adjacent(ts) -> bool:
@@ -307,8 +312,9 @@ class SDXLTransformerBlock:
         self.norm = {k: (sd[f"{k}.weight"].to(device, BF16).contiguous(), sd[f"{k}.bias"].to(device, BF16).contiguous())
                      for k in ("norm1", "norm2", "norm3")}
         self._st = None
-        # (k, v) of the cross-attention, projected for the next forward by the caller (SDXLStacksQLoRA.
-        # precompute_ctx_kv: every block's over one fixed context in stacked GEMMs); None: projected here
+        # (k, v, ctx key) of the cross-attention, projected for the next forward by the caller (SDXLStacksQLoRA.
+        # precompute_ctx_kv: every block's over one fixed context in stacked GEMMs); used only by a forward over
+        # the context it was projected from (_ctx_key); None: projected here
         self.ctx_kv = None
 
     def _attn_fwd(self, q, k, v, B, n, nk):
@@ -424,6 +430,9 @@ class SDXLTransformerBlock:
         L = self.lin
         kv = self.ctx_kv
         self.ctx_kv = None
+        if kv is not None and kv[2] != _ctx_key(ctx):
+            kv = None  # projected for another context (or a stale precompute): project this one here
+        kv = kv[:2] if kv is not None else None
         # the block's bases, one launch (the cross-attention k / v ones only when not projected already)
         Wb = dequant_bases(L, TARGETS if kv is None else [t for t in TARGETS if t not in ("attn2.to_k", "attn2.to_v")],
                            self.device)

@@ -34,6 +34,17 @@ from .timestep import sample_timestep
 
 BF16, F32 = torch.bfloat16, torch.float32
 POOLED_DIM = 1280
+# The reference's SDXL buckets (configs/sdxl/flow_match/config.yml:46-50 -> src/dataset/aspect_ratio_bucket.py:20-60,
+# base 1024, step 128, min 384): the five nearest to square, (width, height) in pixels; latents are / 8.
+SDXL_BUCKETS_5 = [(1024, 1024), (896, 1152), (1152, 896), (768, 1408), (1408, 768)]
+
+
+def _check_latent(lat):
+    h, w = lat
+    if h % 4 or w % 4 or h < 8 or w < 8:
+        raise ValueError(f"latent {h}x{w}: both sides must be multiples of 4 (two 2x2 resamplings)")
+    if ((h // 4) * (w // 4)) % 8:
+        raise ValueError(f"latent {h}x{w}: level-B token count must be a multiple of 8 (transposes, GroupNorm)")
 HIDDEN = 320              # UNet hidden_dim: sinusoid width of t, time_embed_dim = 4 x 320
 ADDITIONAL_DIM = 256      # additional_cond_dim (the six size conditions)
 
@@ -55,21 +66,26 @@ class _Frozen:
 class SDXLFlowMatchQLoRA:
     """One BASELINE-config-5 training step. `stacks` must follow SDXL's topology: two down stacks at level A
     (latent / 2), two down stacks at level B (latent / 4), the mid stack, three up stacks at B, three up at A
-    (SDXL_1024_STACKS: 640 ch at 64 x 64, 1280 ch at 32 x 32)."""
+    (SDXL_1024_STACKS: 640 ch at 64 x 64, 1280 ch at 32 x 32 for the square bucket). The step runs ANY
+    aspect-ratio bucket: the latent h x w of each step's batch sets the stage shapes (h/2 x w/2, h/4 x w/4); the
+    stacks' configured sides only fix the default `latent` (the reference's buckets: configs/sdxl/flow_match/
+    config.yml:46-50, bucket_base_size 1024, step 128, min_size 384 -> latents multiples of 16)."""
 
-    def __init__(self, B: int = 4, latent: int = 128, stacks=SDXL_1024_STACKS, n_ctx: int = CONTEXT_TOKENS,
+    def __init__(self, B: int = 4, latent=128, stacks=SDXL_1024_STACKS, n_ctx: int = CONTEXT_TOKENS,
                  context_dim: int = CONTEXT_DIM, rank: int = 16, alpha: float = 1.0, device="cuda", seed: int = 0,
                  lr: float = 1e-3, timestep_sampling: str = "scale_shift_sigmoid", timestep_mean: float = -0.8,
                  timestep_std: float = 0.8, noise_scale: float = 1.0, clean_at_zero: bool = False,
-                 emb_dim: int = 4 * HIDDEN, pooled_dim: int = POOLED_DIM):
+                 emb_dim: int = 4 * HIDDEN, pooled_dim: int = POOLED_DIM, calibrate: bool = True):
         stacks = list(stacks)
         if len(stacks) != 11:
             raise ValueError("SDXL topology: 2 + 2 down, 1 mid, 3 + 3 up stacks")
         cA, sA, cB, sB = stacks[0][1], stacks[0][4], stacks[2][1], stacks[2][4]
-        if sA * 2 != latent or sB * 2 != sA or any(s[1] != cA or s[4] != sA for s in stacks[:2] + stacks[8:]) or \
+        lat = (latent, latent) if isinstance(latent, int) else tuple(latent)
+        if sB * 2 != sA or any(s[1] != cA or s[4] != sA for s in stacks[:2] + stacks[8:]) or \
                 any(s[1] != cB or s[4] != sB for s in stacks[2:8]):
-            raise ValueError(f"stack channels / sides do not follow the SDXL levels for latent {latent}")
-        self.B, self.L, self.cA, self.cB, self.sA, self.sB = B, latent, cA, cB, sA, sB
+            raise ValueError("stack channels / sides do not follow the SDXL levels")
+        _check_latent(lat)
+        self.B, self.latent, self.cA, self.cB = B, lat, cA, cB
         self.n_ctx, self.cdim, self.emb_dim, self.pooled_dim = n_ctx, context_dim, emb_dim, pooled_dim
         self.device = torch.device(device)
         self.core = SDXLStacksQLoRA(B=B, rank=rank, alpha=alpha, stacks=stacks, context_dim=context_dim, n_ctx=n_ctx,
@@ -90,10 +106,14 @@ class SDXLFlowMatchQLoRA:
         self.m_down = _Frozen(cB, 4 * cA, g, dev, bias=False)    # pixel_unshuffle(level A, 2) -> cB
         self.m_up = _Frozen(4 * cA, cB, g, dev, bias=False)      # cB -> 4 cA, pixel_shuffle(2) -> level A
         self.m_out = _Frozen(16, cA, g, dev)                     # cA -> 4 x 2 x 2, pixel_shuffle(2) -> latents
+        self._seed = seed
         self.gen = torch.Generator().manual_seed(seed + 1)       # timestep sampling (host, like the reference)
         self.step_count = 0
         self.loss = torch.zeros(1, dtype=F32, device=dev)
         self.opt = self.core.opt
+        self._probe = None
+        if calibrate:
+            self.calibrate()
 
     # ------------------------------------------------------------------ pieces
     def condition(self, t1000: torch.Tensor, pooled: torch.Tensor, sizes: torch.Tensor) -> torch.Tensor:
@@ -113,19 +133,52 @@ class SDXLFlowMatchQLoRA:
             lin.fwd(x_tok[b * n_tok:(b + 1) * n_tok], out=out[b * n_tok:(b + 1) * n_tok], bias=emb[b])
         return out
 
+    def _capture(self, name: str, x: torch.Tensor):
+        if self._probe is not None and name not in self._probe:
+            self._probe[name] = float(x.float().pow(2).mean().sqrt())
+
+    @torch.no_grad()
+    def calibrate(self, seed: int = 4242):
+        """Unit-RMS outputs for the skeleton maps that read un-normalised residual sums (Downsample, Upsample and
+        out-conv surrogates: m_down, m_up, m_out), one forward each on a calibration batch, in graph order. The
+        UNet's ResNets renormalise (GroupNorm) what its skips concatenate; the skeleton's additions do not, and
+        without this the residual stream grows through the 70 blocks and 5 skips until the velocity MSE sits in
+        the hundreds on unit-variance targets. Everything the stacks' GEMMs read stays normalised (GroupNorm /
+        LayerNorm outputs) either way; this only sets the magnitudes of the residual stream and of v."""
+        lat, ctx, pooled, sizes = self.make_inputs(seed=seed)
+        t = torch.full((self.B,), 0.5, device=self.device)
+        for name in ("m_down", "m_up", "m_out"):
+            self._probe = {}
+            self.step(lat, ctx, pooled, sizes, t=t, backward=False)
+            rms = self._probe[name]
+            lin = getattr(self, name)
+            k = 1.0 / max(rms, 1e-6)  # the map's N(0, 1/in) weights keep the RMS of their input
+            lin.w = (lin.w.float() * k).to(BF16)
+        self._probe = None
+        self.step_count = 0
+        self.gen = torch.Generator().manual_seed(self._seed + 1)
+
+    def _levels(self, Lh: int, Lw: int):
+        """Stage sides of a latent h x w: level A (h/2 x w/2) and level B (h/4 x w/4)."""
+        _check_latent((Lh, Lw))
+        return (Lh // 2, Lw // 2), (Lh // 4, Lw // 4)
+
     def forward(self, z: torch.Tensor, ctx: torch.Tensor, sg: torch.Tensor) -> torch.Tensor:
-        """The UNet on z [B, 4, L, L] bf16 -> v [B, 4, L, L] bf16 (activations kept for backward)."""
-        B, cA, cB, sA, sB = self.B, self.cA, self.cB, self.sA, self.sB
-        hA, hB = sA * sA, sB * sB
+        """The UNet on z [B, 4, h, w] bf16 -> v [B, 4, h, w] bf16 (activations kept for backward)."""
+        B, cA, cB = self.B, self.cA, self.cB
+        Lh, Lw = z.shape[2], z.shape[3]
+        (ah, aw), (bh, bw) = self._levels(Lh, Lw)
+        hA, hB = ah * aw, bh * bw
         S = [st for (_, _, _, st) in self.core.stacks]
         nc = self.n_ctx
         self.core.precompute_ctx_kv(ctx)  # every block's cross-attention k / v of the fixed context, stacked GEMMs
         eA, eB, eU = self.e_in.fwd(sg), self.e_down.fwd(sg), self.e_up.fwd(sg)
-        tok = ops.space_to_depth(z, B, 4, self.L, self.L, 2).view(B * hA, 16)
+        tok = ops.space_to_depth(z, B, 4, Lh, Lw, 2).view(B * hA, 16)
         x64 = ops.transpose_add(self._map_per_sample(self.m_in, tok, eA, hA).view(B, hA, cA), B, hA, cA)
         e0 = S[0].forward(x64, ctx, B, hA, nc)
         e1 = S[1].forward(e0, ctx, B, hA, nc)
-        tok = ops.space_to_depth(e1, B, cA, sA, sA, 2).view(B * hB, 4 * cA)
+        tok = ops.space_to_depth(e1, B, cA, ah, aw, 2).view(B * hB, 4 * cA)
+        self._capture("m_down", tok)
         x32 = ops.transpose_add(self._map_per_sample(self.m_down, tok, eB, hB).view(B, hB, cB), B, hB, cB)
         d0 = S[2].forward(x32, ctx, B, hB, nc)
         d1 = S[3].forward(d0, ctx, B, hB, nc)
@@ -134,25 +187,29 @@ class SDXLFlowMatchQLoRA:
         u1 = S[6].forward(ops.add_bf16(u0, d0), ctx, B, hB, nc)
         u2 = S[7].forward(ops.add_bf16(u1, x32), ctx, B, hB, nc)
         tok = ops.transpose_add(u2, B, cB, hB).view(B * hB, cB)
-        y64 = ops.space_to_depth(self._map_per_sample(self.m_up, tok, eU, hB), B, cA, sA, sA, 2, inverse=True)
+        self._capture("m_up", tok)
+        y64 = ops.space_to_depth(self._map_per_sample(self.m_up, tok, eU, hB), B, cA, ah, aw, 2, inverse=True)
         y64 = y64.view(B, cA, hA)
         v0 = S[8].forward(ops.add_bf16(y64, e1), ctx, B, hA, nc)
         v1 = S[9].forward(ops.add_bf16(v0, e0), ctx, B, hA, nc)
         v2 = S[10].forward(ops.add_bf16(v1, x64), ctx, B, hA, nc)
         tok = ops.transpose_add(v2, B, cA, hA).view(B * hA, cA)
-        return ops.space_to_depth(self.m_out.fwd(tok), B, 4, self.L, self.L, 2, inverse=True)
+        self._capture("m_out", tok)
+        return ops.space_to_depth(self.m_out.fwd(tok), B, 4, Lh, Lw, 2, inverse=True)
 
     def backward(self, dv: torch.Tensor):
-        """dL/dv [B, 4, L, L] -> every adapter gradient (the skeleton is frozen; no input gradient needed)."""
-        B, cA, cB, sA, sB = self.B, self.cA, self.cB, self.sA, self.sB
-        hA, hB = sA * sA, sB * sB
+        """dL/dv [B, 4, h, w] -> every adapter gradient (the skeleton is frozen; no input gradient needed)."""
+        B, cA, cB = self.B, self.cA, self.cB
+        Lh, Lw = dv.shape[2], dv.shape[3]
+        (ah, aw), (bh, bw) = self._levels(Lh, Lw)
+        hA, hB = ah * aw, bh * bw
         S = [st for (_, _, _, st) in self.core.stacks]
         add = ops.add_bf16
 
         def back(i, dy):
             return S[i].backward(dy, need_dctx=False)[0]
 
-        d = self.m_out.bwd(ops.space_to_depth(dv, B, 4, self.L, self.L, 2).view(B * hA, 16))
+        d = self.m_out.bwd(ops.space_to_depth(dv, B, 4, Lh, Lw, 2).view(B * hA, 16))
         dv2 = ops.transpose_add(d.view(B, hA, cA), B, hA, cA)
         dsum = back(10, dv2)                      # d(v1 + x64)
         dx64 = dsum
@@ -160,7 +217,7 @@ class SDXLFlowMatchQLoRA:
         de0 = dsum
         dsum = back(8, dsum)                      # d(y64 + e1)
         de1 = dsum
-        tok = ops.space_to_depth(dsum.view(B, cA, sA, sA), B, cA, sA, sA, 2).view(B * hB, 4 * cA)
+        tok = ops.space_to_depth(dsum.view(B, cA, ah, aw), B, cA, ah, aw, 2).view(B * hB, 4 * cA)
         du2 = ops.transpose_add(self.m_up.bwd(tok).view(B, hB, cB), B, hB, cB)
         dsum = back(7, du2)                       # d(u1 + x32)
         dx32 = dsum
@@ -171,14 +228,14 @@ class SDXLFlowMatchQLoRA:
         dd0 = add(back(3, dd1), dd0)
         dx32 = add(back(2, dd0), dx32)
         tok = ops.transpose_add(dx32, B, cB, hB).view(B * hB, cB)
-        de1 = add(ops.space_to_depth(self.m_down.bwd(tok), B, cA, sA, sA, 2, inverse=True).view(B, cA, hA), de1)
+        de1 = add(ops.space_to_depth(self.m_down.bwd(tok), B, cA, ah, aw, 2, inverse=True).view(B, cA, hA), de1)
         de0 = add(back(1, de1), de0)
         back(0, de0)                               # (+ dx64: the input map is frozen, z needs no gradient)
 
     # ------------------------------------------------------------------ the step
     def sample_t(self) -> torch.Tensor:
         """sample_timestep(latents.shape, ...) (flow_match.py:127-140), t in (0, 1) f32 [B] on the device."""
-        return sample_timestep((self.B, 4, self.L, self.L), "cpu", generator=self.gen, **self.sampling).to(self.device)
+        return sample_timestep((self.B, 4, *self.latent), "cpu", generator=self.gen, **self.sampling).to(self.device)
 
     def step(self, latents: torch.Tensor, ctx: torch.Tensor, pooled: torch.Tensor, sizes: torch.Tensor,
              t: torch.Tensor | None = None, eps: torch.Tensor | None = None, backward: bool = True,
@@ -208,22 +265,28 @@ class SDXLFlowMatchQLoRA:
         self._last = dict(t=t, z=z, eps=eps)
         return self.loss, v
 
-    def make_inputs(self, seed: int = 1):
-        """Synthetic batch of the step's shapes: VAE latents (scaled, ~unit variance) bf16 [B, 4, L, L], the
-        231 x 2048 text context, the pooled CLIP-G output, and the 1024^2 size conditions."""
+    def make_inputs(self, seed: int = 1, latent=None):
+        """Synthetic batch of one bucket: VAE latents (scaled, ~unit variance) bf16 [B, 4, h, w] (latent = (h, w),
+        default the model's), the 231 x 2048 text context, the pooled CLIP-G output, and the size conditions
+        (original_size = target_size = (8h, 8w), crop (0, 0); text_to_image.py:198-217 order (height, width))."""
         g = torch.Generator(device=self.device).manual_seed(seed)
-        B, L = self.B, self.L
-        lat = torch.randn(B, 4, L, L, device=self.device, generator=g).to(BF16)
+        B = self.B
+        Lh, Lw = self.latent if latent is None else ((latent, latent) if isinstance(latent, int) else latent)
+        _check_latent((Lh, Lw))
+        lat = torch.randn(B, 4, Lh, Lw, device=self.device, generator=g).to(BF16)
         ctx = torch.randn(B * self.n_ctx, self.cdim, device=self.device, generator=g).to(BF16)
         pooled = torch.randn(B, self.pooled_dim, device=self.device, generator=g).to(BF16)
-        px = L * 8
-        sizes = torch.tensor([[px, px, 0, 0, px, px]] * B, dtype=F32, device=self.device)
+        sizes = torch.tensor([[8 * Lh, 8 * Lw, 0, 0, 8 * Lh, 8 * Lw]] * B, dtype=F32, device=self.device)
         return lat, ctx, pooled, sizes
 
-    def flops_per_step(self) -> float:
-        """Algorithmic FLOPs: the stacks' (vpt.sdxl_train) plus the skeleton's GEMMs, forward + input grad."""
-        B, hA, hB, cA, cB = self.B, self.sA ** 2, self.sB ** 2, self.cA, self.cB
-        f = self.core.flops_per_step()
+    def flops_per_step(self, latent=None) -> float:
+        """Algorithmic FLOPs of one step at a latent h x w (default the model's): the stacks' (vpt.sdxl_train) plus
+        the skeleton's GEMMs, forward + input grad."""
+        Lh, Lw = self.latent if latent is None else latent
+        (ah, aw), (bh, bw) = self._levels(Lh, Lw)
+        B, hA, hB, cA, cB = self.B, ah * aw, bh * bw, self.cA, self.cB
+        f = self.core.flops_per_step(hws=[hA if s[1] == cA and i in (0, 1, 8, 9, 10) else hB
+                                          for i, s in enumerate(self.core.stacks)])
         f += 2 * (2 * B * hA * 16 * cA) * 2 + 2 * (2 * B * hB * 4 * cA * cB) * 2  # in / out, down / up maps
         return f
 

@@ -168,12 +168,18 @@ class SDXLStacksQLoRA:
         base+LoRA GEMM per width class (vpt_gemm_bf16_lora_stacked). Each block's forward then takes its k / v column
         blocks (SDXLTransformerBlock.ctx_kv) and its adapters' backward the saved (ctx, ds) column slices. Returns
         False (nothing done: the blocks project per target) for the "inline" base mode or non-skinny adapters."""
-        from .sdxl import base_weight
+        from .sdxl import _ctx_key, base_weight
+        for (_, _, _, st) in self.stacks:
+            for blk in st.blocks:
+                blk.ctx_kv = None  # nothing from an earlier precompute survives this one
         all_lins = [blk.lin[t] for (_, _, _, st) in self.stacks for blk in st.blocks for t in TARGETS]
         owner = {id(blk.lin[t]): (blk, t) for (_, _, _, st) in self.stacks for blk in st.blocks for t in TARGETS}
         lins = [all_lins[k] for k in self._kv_order]
         if any(l.base_mode == "inline" or not (l.fused and l.skinny) for l in lins):
             return False
+        if len({l.scale for l in lins}) != 1:
+            return False  # one GEMM forms every target's ds with one LoRA scale: only when they all share it
+        key = _ctx_key(ctx)
         r, cd, M = self.rank, self.cdim, ctx.shape[0]
         downs = self.params[self._kv_down0:self._kv_down0 + len(lins) * r * cd].view(len(lins) * r, cd)
         ds = torch.empty(M, len(lins) * r, dtype=BF16, device=self.device)
@@ -196,41 +202,47 @@ class SDXLStacksQLoRA:
             for i, l in enumerate(group):
                 l._saved = (ctx, ds[:, c0 + i * r:c0 + (i + 1) * r]) if save else None
                 blk, t = owner[id(l)]
-                kv = list(blk.ctx_kv or (None, None))
+                kv = list(blk.ctx_kv or (None, None, key))
                 kv[0 if t == "attn2.to_k" else 1] = out[:, i * w:(i + 1) * w]
                 blk.ctx_kv = tuple(kv)
             c0 += G * r
         return True
 
-    def make_inputs(self, seed: int = 1):
-        """Synthetic stage activations (NCHW bf16), text context [B*231, 2048] and output gradients g_s."""
+    def make_inputs(self, seed: int = 1, hws=None):
+        """Synthetic stage activations (NCHW bf16), text context [B*231, 2048] and output gradients g_s. hws: the
+        token count of each stack (an aspect-ratio bucket's stage h x w); default the configured square sides."""
         g = torch.Generator(device=self.device).manual_seed(seed)
-        xs = [torch.randn(self.B, C, HW, device=self.device, generator=g).to(BF16) for (_, C, HW, _) in self.stacks]
-        gs = [(torch.randn(self.B, C, HW, device=self.device, generator=g) * 1e-3).to(BF16)
-              for (_, C, HW, _) in self.stacks]
+        hws = [HW for (_, _, HW, _) in self.stacks] if hws is None else list(hws)
+        xs = [torch.randn(self.B, C, hw, device=self.device, generator=g).to(BF16)
+              for (_, C, _, _), hw in zip(self.stacks, hws)]
+        gs = [(torch.randn(self.B, C, hw, device=self.device, generator=g) * 1e-3).to(BF16)
+              for (_, C, _, _), hw in zip(self.stacks, hws)]
         ctx = torch.randn(self.B * self.n_ctx, self.cdim, device=self.device, generator=g).to(BF16)
         return xs, ctx, gs
 
     def step(self, xs, ctx, gs):
-        """One training step: forward of every stack, backward in reverse order, fused optimizer step.
-        Returns the context gradient (summed over stacks), [B*231, 2048] bf16."""
+        """One training step: forward of every stack, backward in reverse order, fused optimizer step. Each
+        stack's token count is its input's (xs[i] [B, C, HW]: any bucket). Returns the context gradient (summed
+        over stacks), [B*231, 2048] bf16."""
         self.grads.zero_()
         self.precompute_ctx_kv(ctx)
-        for x, (_, C, HW, st) in zip(xs, self.stacks):
-            st.forward(x, ctx, self.B, HW, self.n_ctx)
+        for x, (_, C, _, st) in zip(xs, self.stacks):
+            st.forward(x, ctx, self.B, x.shape[2], self.n_ctx)
         dctx = None
-        for gout, (_, C, HW, st) in zip(reversed(gs), reversed(self.stacks)):
+        for gout, (_, C, _, st) in zip(reversed(gs), reversed(self.stacks)):
             _dx, dc = st.backward(gout)
             dctx = dc if dctx is None else ops.add_bf16(dctx, dc)
         self.opt.step()
         return dctx
 
-    def flops_per_step(self) -> float:
+    def flops_per_step(self, hws=None) -> float:
         """Algorithmic FLOPs of one step: forward + backward of every GEMM (QLoRA: no base-weight gradient;
-        LoRA down/up forward, their weight and input gradients) and attention (backward = 2x forward)."""
+        LoRA down/up forward, their weight and input gradients) and attention (backward = 2x forward). hws: each
+        stack's token count (default the configured square sides)."""
         B, r, nc, cd = self.B, self.rank, self.n_ctx, self.cdim
         f = 0.0
-        for (_, C, HW, st) in self.stacks:
+        hws = [HW for (_, _, HW, _) in self.stacks] if hws is None else list(hws)
+        for (_, C, _, st), HW in zip(self.stacks, hws):
             M = B * HW
             dim = st.inner
             f += 2 * (2 * M * C * dim)            # proj_in / proj_out forward
