@@ -226,14 +226,16 @@ def test_two_ranks_overlapped_optimizer_and_clipping_exact_path():
         assert ((dz - dz_ref).norm() / dz_ref.norm()).item() < 8e-3, mode
     # the value clamp binds (else "value" would equal "none")
     assert not torch.equal(r0["value"]["overlap"]["z"], r0["none"]["overlap"]["z"])
-    # (3) the clip coefficient the HIP kernels formed == torch.nn.utils.clip_grad_norm_ on the reduced mean gradient
+    # (3) the clip coefficient the HIP kernels formed == torch.nn.utils.clip_grad_norm_ on the reduced mean gradient.
+    #     torch's reference runs on a float64 copy: its float32 CPU norm is itself ~1e-4 off the exact value at these
+    #     sizes (measured: 0.0118458 vs exact 0.0118468), while the device partial sums agree with float64 to ~1e-7.
     cap = r0["norm"]["overlap"]
-    g = cap["gmean"]
+    g = cap["gmean"].double()
     p = torch.nn.Parameter(torch.zeros_like(g))
     p.grad = g.clone()
     total = torch.nn.utils.clip_grad_norm_([p], r0["max_norm"]).item()
     ref_coef = min(1.0, r0["max_norm"] / (total + 1e-6))
-    assert abs(cap["norm"] - total) <= 1e-5 * total, (cap["norm"], total)
-    assert abs(cap["coef"] - ref_coef) <= 1e-5 * ref_coef and cap["coef"] < 1.0, (cap["coef"], ref_coef)
-    assert torch.allclose(p.grad, g * ref_coef, rtol=1e-5, atol=0)
+    assert abs(cap["norm"] - total) <= 1e-6 * total, (cap["norm"], total)
+    assert abs(cap["coef"] - ref_coef) <= 1e-6 * ref_coef and cap["coef"] < 1.0, (cap["coef"], ref_coef)
+    assert torch.allclose(p.grad, g * ref_coef, rtol=1e-12, atol=0)
     assert r0["norm"]["serial"]["coef"] == cap["coef"]
