@@ -4,6 +4,7 @@ with GradSync.launch as the engine's on_ready hook (buckets reduced in backward-
 the rest launched after the class-embedding scatter, then the per-bucket finish. The averaged gradient must
 equal a single-rank step on the whole batch (SURVEY §8(e) parity) and be identical on both ranks; every
 bucket's reduction is applied exactly once."""
+import io
 import os
 import socket
 
@@ -179,7 +180,9 @@ def _worker_exact(rank, world, port, q):
             torch.cuda.synchronize()
             out[path] = dict(y=tr.engine.params.cpu(), z=opt.z.cpu(), side=sync.side is not None, **cap)
         res[mode] = out
-    q.put((rank, res))
+    buf = io.BytesIO()  # by value: shared-memory tensor handles die with this process before the parent reads them
+    torch.save(res, buf)
+    q.put((rank, buf.getvalue()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -199,7 +202,7 @@ def test_two_ranks_overlapped_optimizer_and_clipping_exact_path():
         p.join(timeout=60)
         assert p.exitcode == 0
     out.sort(key=lambda t: t[0])
-    r0, r1 = out[0][1], out[1][1]
+    r0, r1 = (torch.load(io.BytesIO(b), weights_only=True) for _, b in out)
     dev = torch.device("cuda", 0)
     from vpt.ddp import GradSync, grad_buckets
     for mode in ("none", "norm", "value"):
