@@ -136,6 +136,22 @@ int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr, const void* k, 
                  long l_sh, const float* kbias, long kb_sb, void* dq, long dq_sb, long dq_sh, long dq_sr,
                  void* dk, long dk_sb, long dk_sh, long dk_sr, void* dv, long dv_sb, long dv_sh, long dv_sr,
                  int B, int H, int n, int nk, int n_dense, float scale, void* stream);
+/* The same backward with the per-head QK-RMSNorm + RoPE backward fused into its dQ / dK stores (JiT self-attention,
+ * src/models/jit/denoiser.py:307-316, 98-111; replaces vpt_attn_bwd + vpt_qknorm_rope_bwd for that path): q, k are
+ * the normed, roped (q pre-scaled) attention inputs as for vpt_attn_bwd; xq / xk the raw projections they came from
+ * (same strides x_*), wq / wk the q_norm / k_norm weights [64], cos_t / sin_t the RoPE tables [positions][32] (a
+ * row's position is its row: n == nk). dq / dk (strides dqk_*) receive d loss / d (raw q, k) in bf16, computed from
+ * the f32 attention gradients; dwq_part / dwk_part [vpt_attn_bwd_dw_rows(B, H, n)][64] receive per-workgroup partial
+ * q_norm / k_norm weight gradients (sum them with vpt_reduce_rows, fixed order). */
+int vpt_attn_bwd_dw_rows(int B, int H, int n);
+int vpt_attn_bwd_qknorm(const void* q, long q_sb, long q_sh, long q_sr, const void* k, long k_sb, long k_sh, long k_sr,
+                        const void* v, long v_sb, long v_sh, long v_sr, const void* o, long o_sb, long o_sh, long o_sr,
+                        const void* dO, long do_sb, long do_sh, long do_sr, const float* lse, float* delta, long l_sb,
+                        long l_sh, const float* kbias, long kb_sb, const void* xq, const void* xk, long x_sb,
+                        long x_sh, long x_sr, const void* wq, const void* wk, const float* cos_t, const float* sin_t,
+                        float eps, void* dq, void* dk, long dqk_sb, long dqk_sh, long dqk_sr, float* dwq_part,
+                        float* dwk_part, void* dv, long dv_sb, long dv_sh, long dv_sr, int B, int H, int n, int nk,
+                        int n_dense, float scale, void* stream);
 
 /* ---- RMSNorm over the hidden dim -----------------------------------------------------------
  * Replaces FP32RMSNorm.forward src/modules/norm.py:20-27 (norm1/norm2/norm_final,

@@ -345,6 +345,80 @@ def test_attention_fwd_bwd(ops, n, n_dense, masked):
     assert rel(unh(dv), vf.grad) < 2e-2
 
 
+@pytest.mark.parametrize("n,n_dense,masked", [(200, 150, True), (330, 330, False), (1034, 1024, True), (700, 520, True)])
+def test_attention_bwd_fused_qknorm_rope(ops, n, n_dense, masked):
+    """vpt_attn_bwd_qknorm (the QK-RMSNorm + RoPE backward fused into the attention backward's dQ / dK stores) vs an
+    fp32 autograd reference of rope(rms(x) w) -> SDPA (denoiser.py:307-316, 98-111, attention.py:98-129), and vs the
+    unfused pair (vpt_attn_bwd then vpt_qknorm_rope_bwd). Rows past n (pre-context blocks) are left untouched; masked
+    keys get exactly zero gradients."""
+    B, H, rows = 2, 3, ((n + 127) // 128) * 128
+    D = H * 64
+    qkv = rnd(B * rows, 3 * D, seed=50)
+    wq = (1 + rnd(64, scale=0.1, seed=51).float()).to(torch.bfloat16)
+    wk = (1 + rnd(64, scale=0.1, seed=52).float()).to(torch.bfloat16)
+    cos, sin = _rope_tables(rows, seed=53)
+    kb = torch.zeros(B, rows, device=DEV)
+    if masked:
+        kb[:, n_dense + (n - n_dense) // 2:] = float("-inf")
+        kb[1, n_dense:] = 0.0
+    M = B * rows
+    # forward: the production pieces (qknorm_rope_fwd with the q pre-scale, then attention)
+    qk = ops.qknorm_rope_fwd(qkv[:, :3 * D], wq, wk, cos, sin, rows, q_scale=ops.attn_q_scale(0.125))
+    o = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
+    lse = torch.zeros(B, H, rows, device=DEV)
+    q4, k4, v4 = ops._t4(qk, B, rows, H, 0), ops._t4(qk, B, rows, H, D), ops._t4(qkv, B, rows, H, 2 * D)
+    o4 = ops._t4(o, B, rows, H, 0)
+    ops.attn_fwd(q4, k4, v4, o4, lse, kb, B, H, rows, n, n_dense)
+    do = rnd(M, D, seed=54)
+    sentinel = 7.0
+    dqkv = torch.full((M, 3 * D), sentinel, dtype=torch.bfloat16, device=DEV)
+    nd = ops.attn_bwd_dw_rows(B, H, n)
+    part = torch.full((2, nd, 64), float("nan"), device=DEV)
+    delta = torch.zeros(B, H, rows, device=DEV)
+    ops.attn_bwd_qknorm(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, kb, ops._t4(qkv, B, rows, H, 0),
+                        ops._t4(qkv, B, rows, H, D), wq, wk, cos, sin, ops._t4(dqkv, B, rows, H, 0),
+                        ops._t4(dqkv, B, rows, H, D), part[0], part[1], ops._t4(dqkv, B, rows, H, 2 * D),
+                        B, H, rows, n, n_dense)
+    dw = torch.zeros(128, device=DEV)
+    ops.reduce_rows(part[0], dw[:64])
+    ops.reduce_rows(part[1], dw[64:])
+    # fp32 reference over the valid rows
+    x = qkv.float().view(B, rows, 3 * D)[:, :n].reshape(B * n, 3 * D).requires_grad_(True)
+    wqf, wkf = wq.float().requires_grad_(True), wk.float().requires_grad_(True)
+    fc = torch.complex(cos[:n], sin[:n])
+
+    def nr(t, w):
+        y = torch.nn.functional.rms_norm(t.view(B, n, H, 64), (64,), weight=w, eps=1e-6)
+        yc = torch.view_as_complex(y.reshape(B, n, H, 32, 2)) * fc[None, :, None, :]
+        return torch.view_as_real(yc).reshape(B, n, H, 64).permute(0, 2, 1, 3)
+    qn, kn = nr(x[:, :D], wqf), nr(x[:, D:2 * D], wkf)
+    vf = x[:, 2 * D:].view(B, n, H, 64).permute(0, 2, 1, 3)
+    ref = _attn_ref(qn, kn, vf, kb[:, :n], 0.125)
+    ref.backward(do.float().view(B, rows, H, 64)[:, :n].permute(0, 2, 1, 3))
+    got = dqkv.float().view(B, rows, 3 * D)
+    gx = x.grad.view(B, n, 3 * D)
+    assert rel(got[:, :n, :D], gx[..., :D]) < 2e-2
+    assert rel(got[:, :n, D:2 * D], gx[..., D:2 * D]) < 2e-2
+    assert rel(got[:, :n, 2 * D:], gx[..., 2 * D:]) < 2e-2
+    assert rel(dw[:64], wqf.grad) < 1e-2 and rel(dw[64:], wkf.grad) < 1e-2
+    assert (got[:, n:] == sentinel).all()  # rows past n untouched
+    if masked:
+        dead = (kb[0, :n] == float("-inf")).nonzero().flatten()
+        assert (got[0, dead, D:2 * D] == 0).all()
+    # the unfused pair: same result up to the bf16 rounding of dq / dk between the two kernels
+    dq2, dk2 = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV), torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
+    dqk = torch.zeros(M, 2 * D, dtype=torch.bfloat16, device=DEV)
+    dqkv2 = torch.zeros(M, 3 * D, dtype=torch.bfloat16, device=DEV)
+    ops.attn_bwd(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, kb, ops._t4(dqk, B, rows, H, 0),
+                 ops._t4(dqk, B, rows, H, D), ops._t4(dqkv2, B, rows, H, 2 * D), B, H, rows, n, n_dense)
+    del dq2, dk2
+    p2 = ops.qknorm_rope_bwd(dqk, qkv, wq, wk, cos, sin, rows, dqkv2)
+    g2 = dqkv2.float().view(B, rows, 3 * D)
+    assert rel(got[:, :n, :2 * D], g2[:, :n, :2 * D]) < 1e-2
+    assert torch.equal(got[:, :n, 2 * D:], g2[:, :n, 2 * D:])  # dV is the same kernel path
+    assert p2 is not None
+
+
 @pytest.mark.parametrize("n,nk,masked", [(300, 231, False), (1000, 77, True), (64, 500, True)])
 def test_cross_attention_fwd_bwd(ops, n, nk, masked):
     """SDXL cross-attention shape (src/models/sdxl/denoiser.py:101-171): n query rows attend to nk

@@ -43,6 +43,14 @@ struct AttnArgs {
   int kb0;    // start of the key-bias LDS array: n_dense rounded down to 64 (fwd, dq)
   float* dqacc; int nq_pad;  // fused backward: f32 dQ accumulator [B*H][nq_pad][64] (workspace)
   int H;
+  // Fused QK-RMSNorm + RoPE backward (vpt_attn_bwd_qknorm; qkn = 0: dq / dk are plain gradients of the attention
+  // inputs). dq / dk then receive d loss / d (raw q, k), the pre-norm projections read from xq / xk.
+  int qkn;
+  Tensor4 xq, xk;
+  const bf16_t* wq; const bf16_t* wk;   // q_norm / k_norm weights [64]
+  const float* rcos; const float* rsin; // RoPE tables [positions][32]
+  float eps;
+  float* dwq; float* dwk;               // per-workgroup partial weight gradients [workgroups][64]
 };
 
 constexpr float kNegInf = -__builtin_huge_valf();
@@ -242,6 +250,102 @@ __device__ __forceinline__ void store_T(const OTensor4& t, long base_off, const 
       if (zero) w = make_uint2(0u, 0u);
       *reinterpret_cast<uint2*>(dst + d) = w;
     }
+}
+
+// ---- fused QK-RMSNorm + RoPE backward of one q / k row (JiT Attention.q_norm / k_norm + apply_rope,
+// src/models/jit/denoiser.py:307-316, 98-111; the standalone form is qknorm_rope_bwd_kernel, csrc/norm.hip).
+// The row's gradient arrives as a transposed accumulator pair (row on the lane, register 16 db + 4 g4 + e of lane l
+// holding dim d = 32 db + 8 g4 + 4 h + e, h = l >> 5): g = mul * acc = d loss / d rope(rms(x) w), in f32 (never
+// rounded to bf16 on the way). Lanes l and l + 32 hold the two halves of the row, so the two 64-dim sums are one
+// permlane32 swap each. Writes dx = d loss / d x (bf16) and adds this row's dy * xhat to dwp (this lane's 32 dims).
+__device__ __forceinline__ int qkn_dim(int v, int h) { return 32 * (v >> 4) + 8 * ((v >> 2) & 3) + 4 * h + (v & 3); }
+
+__device__ __forceinline__ void qkn_load_w(const bf16_t* w, int lane, float (&wf)[32]) {
+  const int h = lane >> 5;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint2 u = *reinterpret_cast<const uint2*>(w + qkn_dim(4 * q, h));
+    wf[4 * q + 0] = __uint_as_float(u.x << 16); wf[4 * q + 1] = __uint_as_float(u.x & 0xffff0000u);
+    wf[4 * q + 2] = __uint_as_float(u.y << 16); wf[4 * q + 3] = __uint_as_float(u.y & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ void qkn_bwd_row(const AttnArgs& g, const Tensor4& xs, const OTensor4& out, int b, int hd,
+                                            const floatx16 (&acc)[2], float mul, const float (&wf)[32], int row, int n,
+                                            int lane, bool zero, float (&dwp)[32]) {
+  if (row >= n) return;  // both lanes of a row take the same branch (the swaps below pair l with l ^ 32)
+  const int h = lane >> 5;
+  const bf16_t* xr = xs.p + (long)b * xs.sb + (long)hd * xs.sh + (long)row * xs.sr;
+  bf16_t* orow = out.p + (long)b * out.sb + (long)hd * out.sh + (long)row * out.sr;
+  if (zero) {  // masked key: its gradient is exactly zero (and contributes nothing to the weight gradient)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) *reinterpret_cast<uint2*>(orow + qkn_dim(4 * q, h)) = make_uint2(0u, 0u);
+    return;
+  }
+  float x[32], cs[16], sn[16];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int d0 = qkn_dim(4 * q, h);
+    const uint2 u = *reinterpret_cast<const uint2*>(xr + d0);
+    x[4 * q + 0] = __uint_as_float(u.x << 16); x[4 * q + 1] = __uint_as_float(u.x & 0xffff0000u);
+    x[4 * q + 2] = __uint_as_float(u.y << 16); x[4 * q + 3] = __uint_as_float(u.y & 0xffff0000u);
+    const float2 c2 = *reinterpret_cast<const float2*>(g.rcos + (long)row * 32 + d0 / 2);
+    const float2 s2 = *reinterpret_cast<const float2*>(g.rsin + (long)row * 32 + d0 / 2);
+    cs[2 * q] = c2.x; cs[2 * q + 1] = c2.y; sn[2 * q] = s2.x; sn[2 * q + 1] = s2.y;
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int v = 0; v < 32; ++v) ss += x[v] * x[v];
+  const float r = rsqrtf(pair_sum(ss) * (1.f / 64.f) + g.eps);
+  float dy[32], xh[32], gg[32], dot = 0.f;
+#pragma unroll
+  for (int p = 0; p < 16; ++p) {  // RoPE backward: rotate the pair (2p, 2p + 1) back by the conjugate
+    const int db = p >> 3, i = (p >> 1) & 3, e = 2 * (p & 1);
+    const float a = acc[db][4 * i + e] * mul, c = acc[db][4 * i + e + 1] * mul;
+    dy[2 * p] = a * cs[p] + c * sn[p];
+    dy[2 * p + 1] = -a * sn[p] + c * cs[p];
+  }
+#pragma unroll
+  for (int v = 0; v < 32; ++v) {
+    xh[v] = x[v] * r;
+    gg[v] = dy[v] * wf[v];
+    dot += gg[v] * xh[v];
+    dwp[v] += dy[v] * xh[v];
+  }
+  dot = pair_sum(dot) * (1.f / 64.f);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    uint2 w;
+    w.x = pack_bf16x2(r * (gg[4 * q] - xh[4 * q] * dot), r * (gg[4 * q + 1] - xh[4 * q + 1] * dot));
+    w.y = pack_bf16x2(r * (gg[4 * q + 2] - xh[4 * q + 2] * dot), r * (gg[4 * q + 3] - xh[4 * q + 3] * dot));
+    *reinterpret_cast<uint2*>(orow + qkn_dim(4 * q, h)) = w;
+  }
+}
+
+// The block's 128 rows' dwp (4 waves x 32 rows, two lanes per row) summed in a fixed order into dw[64] (one
+// partial row per workgroup, reduced by vpt_reduce_rows). red: 32 KB of the staging LDS, red2: 1 KB.
+template <int NW>
+__device__ __forceinline__ void qkn_dw_partial(float* red, float* red2, const float (&dwp)[32], float* dw, int tid) {
+  const int lane = tid & 63, wid = tid >> 6, h = lane >> 5;
+  __syncthreads();  // every wave is done reading the staging tiles
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    *reinterpret_cast<floatx4*>(red + (wid * 32 + (lane & 31)) * 64 + qkn_dim(4 * q, h)) =
+        floatx4{dwp[4 * q], dwp[4 * q + 1], dwp[4 * q + 2], dwp[4 * q + 3]};
+  __syncthreads();
+  {
+    const int d = tid & 63, w = tid >> 6;
+    float acc = 0.f;
+    for (int r2 = 0; r2 < 32; ++r2) acc += red[(w * 32 + r2) * 64 + d];
+    red2[w * 64 + d] = acc;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) acc += red2[w * 64 + tid];
+    dw[tid] = acc;
+  }
 }
 
 // Key bias for keys [kb0, round_up(n, 64)) in LDS, filled once per block: 0 below n_dense,
@@ -559,13 +663,24 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
   }
   store_T(g.dv, (long)b * g.dv.sb + hd * g.dv.sh, dvT, 1.f, key, g.nk, lane, kmasked);
   // dK = scale * dS^T.Q = (scale / c) * dS^T.Q~ with Q~ = c*Q, c = scale*log2(e): the factor is ln 2
-  store_T(g.dk, (long)b * g.dk.sb + hd * g.dk.sh, dkT, 0.69314718055994531f, key, g.nk, lane, kmasked);
+  if (!g.qkn) {
+    store_T(g.dk, (long)b * g.dk.sb + hd * g.dk.sh, dkT, 0.69314718055994531f, key, g.nk, lane, kmasked);
+    return;
+  }
+  float wf[32], dwp[32];
+  qkn_load_w(g.wk, lane, wf);
+#pragma unroll
+  for (int v = 0; v < 32; ++v) dwp[v] = 0.f;
+  qkn_bwd_row(g, g.xk, g.dk, b, hd, dkT, 0.69314718055994531f, wf, key, g.nk, lane, kmasked, dwp);
+  qkn_dw_partial<NW>(reinterpret_cast<float*>(&lds[0][0][0]), &lstat[0][0][0], dwp,
+                     g.dwk + ((long)(b * g.H + hd) * ((g.nk + 32 * NW - 1) / (32 * NW)) + bx) * 64, tid);
 }
 
 // ------------------------------------------------------------------ backward dQ
 // Body of one dQ block (query block bx of head hd, batch b); lds = [buf][K / V] tiles, kbl = key bias of keys kb0..
 template <int ABL, int NW>
-__device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b, char (&lds)[2][2][8192], float* kbl) {
+__device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b, char (&lds)[2][2][8192], float* kbl,
+                                        float* red2) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
   const int q0 = bx * (32 * NW) + wid * 32;
   const int qrow = q0 + (lane & 31);
@@ -701,7 +816,17 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
     __syncthreads();
     if (ABL != 1) cur ^= 1;
   }
-  store_T(g.dq, (long)b * g.dq.sb + hd * g.dq.sh, dqT, g.scale, qrow, g.n, lane, false);
+  if (!g.qkn) {
+    store_T(g.dq, (long)b * g.dq.sb + hd * g.dq.sh, dqT, g.scale, qrow, g.n, lane, false);
+    return;
+  }
+  float wf[32], dwp[32];
+  qkn_load_w(g.wq, lane, wf);
+#pragma unroll
+  for (int v = 0; v < 32; ++v) dwp[v] = 0.f;
+  qkn_bwd_row(g, g.xq, g.dq, b, hd, dqT, g.scale, wf, qrow, g.n, lane, false, dwp);
+  qkn_dw_partial<NW>(reinterpret_cast<float*>(&lds[0][0][0]), red2,
+                     dwp, g.dwq + ((long)(b * g.H + hd) * ((g.n + 32 * NW - 1) / (32 * NW)) + bx) * 64, tid);
 }
 
 // The production backward as ONE launch over both block kinds: the dK/dV blocks first (the longer ones),
@@ -731,7 +856,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs g, int nkb, i
     r = kv ? bid / nkb : bid / nqb;
   }
   if (kv) dkdv_body<DKDV, 4>(g, bx, r % g.H, r / g.H, lds, lstat);
-  else dq_body<DQ, 4>(g, bx, r % g.H, r / g.H, lds, kbl);
+  else dq_body<DQ, 4>(g, bx, r % g.H, r / g.H, lds, kbl, &lstat[0][0][0]);
 }
 constexpr int kDqBody = 0;  // production dQ body (0 = compiler-scheduled, 8 = explicitly ordered)
 
@@ -786,6 +911,10 @@ extern "C" int vpt_attn_fwd(const void* q, long q_sb, long q_sh, long q_sr,
 }
 
 
+namespace {
+int attn_bwd_impl(AttnArgs& g, int B, int H, int n, int nk, hipStream_t s);
+}
+
 extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
                             const void* k, long k_sb, long k_sh, long k_sr,
                             const void* v, long v_sb, long v_sh, long v_sr,
@@ -816,7 +945,59 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
   g.kb0 = g.n_dense / 64 * 64;
   g.nq_pad = (n + 63) / 64 * 64;
   g.H = H;
-  hipStream_t s = (hipStream_t)stream;
+  return attn_bwd_impl(g, B, H, n, nk, (hipStream_t)stream);
+}
+
+// Rows of the per-workgroup weight-gradient partials vpt_attn_bwd_qknorm writes for n rows (q: n = query rows,
+// k: n = key rows): one 64-float row per 128-row block of every (batch, head).
+extern "C" int vpt_attn_bwd_dw_rows(int B, int H, int n) { return B * H * ((n + 127) / 128); }
+
+extern "C" int vpt_attn_bwd_qknorm(const void* q, long q_sb, long q_sh, long q_sr,
+                                   const void* k, long k_sb, long k_sh, long k_sr,
+                                   const void* v, long v_sb, long v_sh, long v_sr,
+                                   const void* o, long o_sb, long o_sh, long o_sr,
+                                   const void* dO, long do_sb, long do_sh, long do_sr,
+                                   const float* lse, float* delta, long l_sb, long l_sh,
+                                   const float* kbias, long kb_sb,
+                                   const void* xq, const void* xk, long x_sb, long x_sh, long x_sr,
+                                   const void* wq, const void* wk, const float* cos_t, const float* sin_t, float eps,
+                                   void* dq, void* dk, long dqk_sb, long dqk_sh, long dqk_sr, float* dwq_part,
+                                   float* dwk_part, void* dv, long dv_sb, long dv_sh, long dv_sr,
+                                   int B, int H, int n, int nk, int n_dense, float scale, void* stream) {
+  int rc = check_common(B, H, n, nk);
+  if (rc) return rc;
+  VPT_CHECK_ARG(q && k && v && o && dO && lse && delta && dq && dk && dv, "vpt_attn_bwd_qknorm: null pointer");
+  VPT_CHECK_ARG(xq && xk && wq && wk && cos_t && sin_t && dwq_part && dwk_part, "vpt_attn_bwd_qknorm: null pointer");
+  VPT_CHECK_ARG(n == nk, "vpt_attn_bwd_qknorm: self-attention only (the RoPE position of a key is its row)");
+  VPT_CHECK_ARG(x_sr % 4 == 0 && dqk_sr % 4 == 0 && x_sh % 4 == 0 && dqk_sh % 4 == 0 && x_sb % 4 == 0 &&
+                dqk_sb % 4 == 0, "vpt_attn_bwd_qknorm: 8-byte aligned row pieces");
+  AttnArgs g = {};
+  g.q = {(const bf16_t*)q, q_sb, q_sh, q_sr};
+  g.k = {(const bf16_t*)k, k_sb, k_sh, k_sr};
+  g.v = {(const bf16_t*)v, v_sb, v_sh, v_sr};
+  g.o = {(bf16_t*)o, o_sb, o_sh, o_sr};
+  g.dO = {(const bf16_t*)dO, do_sb, do_sh, do_sr};
+  g.dq = {(bf16_t*)dq, dqk_sb, dqk_sh, dqk_sr};
+  g.dk = {(bf16_t*)dk, dqk_sb, dqk_sh, dqk_sr};
+  g.dv = {(bf16_t*)dv, dv_sb, dv_sh, dv_sr};
+  g.lse = (float*)lse; g.delta_in = delta; g.delta_out = delta; g.l_sb = l_sb; g.l_sh = l_sh;
+  g.kbias = kbias; g.kb_sb = kb_sb;
+  g.n = n; g.nk = nk; g.n_dense = n_dense < nk ? n_dense : nk;
+  g.scale = scale; g.scale_log2 = scale * 1.4426950408889634f;
+  g.kb0 = g.n_dense / 64 * 64;
+  g.nq_pad = (n + 63) / 64 * 64;
+  g.H = H;
+  g.qkn = 1;
+  g.xq = {(const bf16_t*)xq, x_sb, x_sh, x_sr};
+  g.xk = {(const bf16_t*)xk, x_sb, x_sh, x_sr};
+  g.wq = (const bf16_t*)wq; g.wk = (const bf16_t*)wk;
+  g.rcos = cos_t; g.rsin = sin_t; g.eps = eps;
+  g.dwq = dwq_part; g.dwk = dwk_part;
+  return attn_bwd_impl(g, B, H, n, nk, (hipStream_t)stream);
+}
+
+namespace {
+int attn_bwd_impl(AttnArgs& g, int B, int H, int n, int nk, hipStream_t s) {
   const long rows = (long)B * H * n;
   g.dqacc = nullptr;
 #ifdef VPT_DIAG
@@ -863,6 +1044,7 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
+}  // namespace
 
 #ifdef VPT_DIAG
 #include "diag/attention_diag_api.inc"

@@ -289,8 +289,9 @@ class JiTEngine:
         # --- blocks in reverse
         dctx = pool.get("dctx", (max(B * n_ctx, 1), D), F32, zero=True)
         dqkv = pool.get("d_qkv", (M, 3 * D))
-        dqk = pool.get("d_qk", (M, 2 * D))
         delta = pool.get("delta", (B, Hh, rows), F32)
+        n_dw = ops.attn_bwd_dw_rows(B, Hh, rows)
+        qk_dw = pool.get("qk_dw_part", (2, n_dw, 64), F32)  # q_norm | k_norm weight-gradient partials
         pre_zeroed = False
         scale = 1.0 / math.sqrt(cfg.head_dim)
         ck = st.get("ckpt", False)
@@ -309,8 +310,7 @@ class JiTEngine:
             lse = pool.get(tag + "lse", (B, Hh, rows), F32)
             n_i = rows if (n_ctx and self._ctx_present(i)) else n_pre
             if n_i < rows and not pre_zeroed:
-                dqkv.zero_()
-                dqk.zero_()
+                dqkv.zero_()  # the context rows take no gradient in the blocks before context_start_block
                 pre_zeroed = True
             # MLP
             wgrad(dx, h, w["gw3"], w["gb3"])
@@ -324,13 +324,17 @@ class JiTEngine:
             # attention
             wgrad(dxm, o, w["gwo"], w["gbo"])
             do = ops.linear_dgrad(dxm, w["pwo"], out=pool.get("d_o", (M, D)))
-            ops.attn_bwd(ops._t4(qk, B, rows, Hh, 0), ops._t4(qk, B, rows, Hh, D), ops._t4(qkv, B, rows, Hh, 2 * D),
-                         ops._t4(o, B, rows, Hh, 0), ops._t4(do, B, rows, Hh, 0), lse, delta, st["kbias"],
-                         ops._t4(dqk, B, rows, Hh, 0), ops._t4(dqk, B, rows, Hh, D), ops._t4(dqkv, B, rows, Hh, 2 * D),
-                         B, Hh, rows, n_i, n_pre, scale)
-            qpart = ops.qknorm_rope_bwd(dqk, qkv, w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, rows, dqkv,
-                                        dw_part=pool.get("qk_part", (ops.qknorm_rope_blocks(M), 128), F32))
-            ops.reduce_rows(qpart[:ops.qknorm_rope_blocks(M)], w["gqk_norm"], acc)
+            # attention backward with the QK-RMSNorm + RoPE backward fused into its dQ / dK stores: dqkv receives the
+            # gradients of the raw q | k | v projections directly
+            ops.attn_bwd_qknorm(ops._t4(qk, B, rows, Hh, 0), ops._t4(qk, B, rows, Hh, D),
+                                ops._t4(qkv, B, rows, Hh, 2 * D), ops._t4(o, B, rows, Hh, 0), ops._t4(do, B, rows, Hh, 0),
+                                lse, delta, st["kbias"], ops._t4(qkv, B, rows, Hh, 0), ops._t4(qkv, B, rows, Hh, D),
+                                w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, ops._t4(dqkv, B, rows, Hh, 0),
+                                ops._t4(dqkv, B, rows, Hh, D), qk_dw[0], qk_dw[1], ops._t4(dqkv, B, rows, Hh, 2 * D),
+                                B, Hh, rows, n_i, n_pre, scale)
+            n_dw_i = ops.attn_bwd_dw_rows(B, Hh, n_i)
+            ops.reduce_rows(qk_dw[0][:n_dw_i], w["gqk_norm"][:64], acc)
+            ops.reduce_rows(qk_dw[1][:n_dw_i], w["gqk_norm"][64:], acc)
             wgrad(dqkv, xn1, w["gwqkv"], w["gbqkv"])
             dxn1 = ops.linear_dgrad(dqkv, w["pwqkv"], out=pool.get("d_b", (M, D)))
             dx_new, part = ops.rmsnorm_bwd(dxn1, x_in, rstd1, w["pn1"], dres=dxm, dx=pool.get("dx_a", (M, D)),

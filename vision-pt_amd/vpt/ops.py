@@ -488,6 +488,33 @@ def attn_bwd(q, k, v, o, do, lse, delta, kbias, dq, dk, dv, B, H, rows, n, n_den
     return pr.record(8.0 * B * H * n * nk * 64, run, nbytes=B * H * (2.0 * 64 * 4 * (n + nk) + 12.0 * n))
 
 
+def attn_bwd_dw_rows(B: int, H: int, n: int) -> int:
+    return int(lib.vpt_attn_bwd_dw_rows(B, H, n))
+
+
+def attn_bwd_qknorm(q, k, v, o, do, lse, delta, kbias, xq, xk, wq, wk, cos_t, sin_t, dq, dk, dwq_part, dwk_part, dv,
+                    B, H, rows, n, n_dense, scale=0.125, eps=1e-6):
+    """attn_bwd with the QK-RMSNorm + RoPE backward fused into the dQ / dK stores (include/vpt_hip.h
+    vpt_attn_bwd_qknorm): xq / xk (raw projections) and dq / dk share their (sb, sh, sr) strides; dq / dk receive the
+    raw-projection gradients; dwq_part / dwk_part [attn_bwd_dw_rows(B, H, n), 64] f32 the norm-weight partials."""
+    if xq[1:] != xk[1:] or dq[1:] != dk[1:]:
+        raise ValueError("attn_bwd_qknorm: q / k operands must share strides")
+    rows_needed = attn_bwd_dw_rows(B, H, n)
+    for t in (dwq_part, dwk_part):
+        if t.dtype != F32 or t.numel() < rows_needed * 64 or not t.is_contiguous():
+            raise ValueError(f"attn_bwd_qknorm: dw partials must be contiguous f32 [{rows_needed}, 64]")
+
+    def run():
+        call("vpt_attn_bwd_qknorm", *q, *k, *v, *o, *do, lse.data_ptr(), delta.data_ptr(), lse.stride(0), lse.stride(1),
+             _p(kbias), 0 if kbias is None else kbias.stride(0), xq[0], xk[0], *xq[1:], wq.data_ptr(), wk.data_ptr(),
+             cos_t.data_ptr(), sin_t.data_ptr(), float(eps), dq[0], dk[0], *dq[1:], dwq_part.data_ptr(),
+             dwk_part.data_ptr(), *dv, B, H, n, n, n_dense, scale, stream())
+    pr = PROBES.get("attn_bwd")
+    if pr is None:
+        return run()
+    return pr.record(8.0 * B * H * n * n * 64, run, nbytes=B * H * (2.0 * 64 * 4 * (2 * n) + 12.0 * n))
+
+
 # ----------------------------------------------------------------------------- misc
 def patchify(img, B, H, W, out, t=None, noise=None, noise_scale=1.0, seed=0, noising=True):
     _launch("patchify", B * 3 * H * W * (4 + (2 if noise is not None else 0)),  # fp16 pixel in, bf16 out
