@@ -115,6 +115,14 @@ long vpt_gemm_swiglu_bwd_workspace(int M, int F, int D);
 int vpt_gemm_swiglu_bwd(const void* dy, long lddy, const void* w3, long ldw3, const void* x12, long ldx12, void* dx12,
                         long lddx12, int M, int F, int D, void* workspace, void* stream);
 
+/* The JiT attention input projection with the per-head QK-RMSNorm + RoPE fused into its epilogue: qkv [M][3D] =
+ * x . W^T + b (W = to_q|to_k|to_v [3D][K], bf16 out) and qk [M][2D] = (rope(rms(q) wq) * q_scale | rope(rms(k) wk)),
+ * bitwise what vpt_qknorm_rope_fwd computes from that qkv. Replaces Attention.to_q/to_k/to_v + q_norm/k_norm +
+ * apply_rope, src/models/jit/denoiser.py:318-323, 307-316, 369-373, 98-111. */
+int vpt_linear_qknorm_rope(const void* x, long ldx, const void* w, long ldw, const void* bias, void* qkv, long ldqkv,
+                           void* qk, long ldqk, int M, int D, int K, const void* wq, const void* wk, const float* cos_t,
+                           const float* sin_t, int rows_per_seq, float eps, float q_scale, void* stream);
+
 /* ---- flash attention, head_dim 64 ---------------------------------------------------------
  * Tensors addressed p[b*sb + h*sh + row*sr + d]; n query rows, nk key rows (nk = n for
  * self-attention; SDXL cross-attention nk = context length). Keys < n_dense always valid; keys in

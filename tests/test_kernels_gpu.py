@@ -281,6 +281,33 @@ def test_qknorm_rope_fwd_bwd(ops):
     assert rel(dw[64:], wkf.grad) < 1e-3
 
 
+@pytest.mark.parametrize("M,rps", [(530, 265), (8 * 4170, 4170), (4 * 1034 + 6, 1034)])
+def test_linear_qknorm_rope_fused_epilogue(ops, M, rps):
+    """vpt_linear_qknorm_rope (q|k|v projection with the per-head QK-RMSNorm + RoPE in the ring GEMM's epilogue) ==
+    linear then qknorm_rope_fwd, bitwise (qkv and qk), at a small M, the C3 1024^2 B=8 shape (ring items with q, k and
+    v heads, partial last row tile) and a ragged one; and within bf16 of the fp32 reference."""
+    D, K = 768, 768
+    x = rnd(M, K, seed=61)
+    w = rnd(3 * D, K, scale=0.05, seed=62)
+    b = rnd(3 * D, scale=0.1, seed=63)
+    wq = (1 + rnd(64, scale=0.1, seed=64).float()).to(torch.bfloat16)
+    wk = (1 + rnd(64, scale=0.1, seed=65).float()).to(torch.bfloat16)
+    cos, sin = _rope_tables(rps, seed=66)
+    qs = ops.attn_q_scale(0.125)
+    qkv = torch.empty(M, 3 * D, dtype=torch.bfloat16, device=DEV)
+    qk = torch.empty(M, 2 * D, dtype=torch.bfloat16, device=DEV)
+    ops.linear_qknorm_rope(x, w, b, qkv, qk, wq, wk, cos, sin, rps, q_scale=qs)
+    ref_qkv = ops.linear(x, w, b)
+    ref_qk = ops.qknorm_rope_fwd(ref_qkv, wq, wk, cos, sin, rps, q_scale=qs)
+    torch.cuda.synchronize()
+    assert torch.equal(qkv, ref_qkv)
+    assert torch.equal(qk, ref_qk)
+    if M < 4096:
+        f = _ref_qknorm_rope(qkv.float(), wq.float(), wk.float(), cos, sin, rps)
+        f[:, :D] *= qs
+        assert rel(qk, f) < 8e-3
+
+
 # ------------------------------------------------------------------------------------ attention
 def prescale_q(ops, t, D, scale=0.125):
     """Copy of t whose first D columns (q) carry the attention kernels' pre-scale (include/vpt_hip.h)."""

@@ -71,6 +71,14 @@ struct GemmArgs {
   // alpha_cols > 0: alpha scales output columns [0, alpha_cols) only, the rest take 1 (the attention q block of a
   // fused q|k|v GEMM pre-scaled in its epilogue); a multiple of the ring tile width (256) or the T128 path is used
   int alpha_cols;
+  // fused per-head QK-RMSNorm + RoPE forward (ring kernel, EPI_QKN; vpt_linear_qknorm_rope): qk_d > 0 marks output
+  // columns [0, qk_d) as q and [qk_d, 2 qk_d) as k projections; each 64-column head of them is also normed (weights
+  // qk_wq / qk_wk [64], eps qk_eps), roped (tables rcos / rsin [rps][32], position = row % rps), q times qk_scale,
+  // and stored to C2 [M][ldc2] at the same column -- exactly qknorm_rope_fwd_kernel's arithmetic (csrc/norm.hip).
+  int qk_d, rps;
+  const bf16_t* qk_wq; const bf16_t* qk_wk;
+  const float* rcos; const float* rsin;
+  float qk_scale, qk_eps;
 };
 
 // ---- LDS images -----------------------------------------------------------------------------
@@ -631,12 +639,12 @@ __device__ __forceinline__ EpiAddr epi_addr(const GemmArgs& g, const RingItem& i
 // Epilogue modes (a template parameter of the ring kernel, so that each mode gets its own register
 // allocation): 0 = no loads (bf16 / f32 out, bias, SiLU), 1 = residual, 2 = fused SwiGLU backward (x12),
 // 3 = f32 accumulate into C.
-enum { EPI_PLAIN = 0, EPI_RESID = 1, EPI_SWB = 2, EPI_ACC = 3 };
+enum { EPI_PLAIN = 0, EPI_RESID = 1, EPI_SWB = 2, EPI_ACC = 3, EPI_QKN = 4 };
 __host__ __device__ constexpr int epi_frags(int epi) {  // fragments per preload group (0: no loads)
   return epi == EPI_RESID ? 4 : (epi == EPI_SWB || epi == EPI_ACC) ? 2 : 0;
 }
 __host__ __device__ inline int epi_mode(const GemmArgs& g) {
-  return g.sw == 2 ? EPI_SWB : g.out_mode == OUT_F32_ACC ? EPI_ACC : g.resid ? EPI_RESID : EPI_PLAIN;
+  return g.sw == 2 ? EPI_SWB : g.out_mode == OUT_F32_ACC ? EPI_ACC : g.resid ? EPI_RESID : g.qk_d > 0 ? EPI_QKN : EPI_PLAIN;
 }
 struct EpiPre {
   u32x4 v[8];
@@ -765,6 +773,93 @@ __device__ __forceinline__ void epilogue_ring(const GemmArgs& g, const floatx4 (
             u32x4{__float_as_uint(o[4]), __float_as_uint(o[5]), __float_as_uint(o[6]), __float_as_uint(o[7])}, e.rs,
             (int)e.voff, soff + 16);
       }
+    }
+  }
+}
+
+// Fused QK-RMSNorm + RoPE forward epilogue (EPI_QKN, bf16 output, no residual): as epilogue_ring's bf16 path, plus,
+// for a wave whose 64-column slice is a q or k head, the head's rope(rms(x) w) (q: times qk_scale) of the bf16-rounded
+// output row to C2. A lane holds 8 consecutive columns of one row and the row's 64 columns sit in the 8 lanes
+// lane >> 3 == row: the sum of squares is 8 in-lane adds and xor-shuffles 1, 2, 4, the RoPE pairs are in-lane -- the
+// operation order of qknorm_rope_fwd_kernel, so qk is bitwise what that kernel computes from the stored qkv. The RoPE
+// table rows (L2-resident) are loaded one fragment ahead; this epilogue runs BEFORE the next item's tiles are DMA'd
+// (its loads are waited for by the compiler, and vmcnt retires in order), so the item seam waits count no stores.
+__device__ __forceinline__ void epilogue_ring_qkn(const GemmArgs& g, const floatx4 (&acc)[8][4], char* stg, int lane,
+                                                  const EpiAddr& e, const float (&bias8)[8], const RingItem& it, int wm,
+                                                  int wn) {
+  const int cw = lane & 7;
+  const int hcol = it.n0 + wn * 64;                    // first column of this wave's head slice
+  const bool isq = hcol < g.qk_d, isk = !isq && hcol < 2 * g.qk_d;
+  const bool qk = isq || isk;                          // wave-uniform
+  const int rows_here = min(256, g.M - it.m0);
+  const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc(
+      (char*)g.C2 + ((long)it.m0 * g.ldc2 + (qk ? hcol : 0)) * 2, (short)0, rows_here * (int)g.ldc2 * 2, 0x00020000);
+  const int lrow = wm * 128 + (lane >> 3);
+  const uint32_t voff2 = (uint32_t)((lrow * (int)g.ldc2 + cw * 8) * 2);
+  const int rstride2 = (int)g.ldc2 * 2;
+  float wf[8];
+  {
+    uint4 wr = make_uint4(0, 0, 0, 0);
+    if (qk) wr = *reinterpret_cast<const uint4*>((isq ? g.qk_wq : g.qk_wk) + cw * 8);
+    unpack8(wr, wf);
+  }
+  const float osc = isq ? g.qk_scale : 1.f;
+  // RoPE table pieces (4 cos + 4 sin of the lane's column pairs) of fragment i, halves p = 0, 1
+  auto table = [&](int i, floatx4 (&c)[2], floatx4 (&sn)[2]) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const long pos = (long)(it.m0 + lrow + i * 16 + p * 8) % g.rps;
+      c[p] = *reinterpret_cast<const floatx4*>(g.rcos + pos * 32 + cw * 4);
+      sn[p] = *reinterpret_cast<const floatx4*>(g.rsin + pos * 32 + cw * 4);
+    }
+  };
+  floatx4 cc[2], sc[2];
+  if (qk) table(0, cc, sc);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    floatx4 cn[2], sn[2];
+    if (qk && i < 7) table(i + 1, cn, sn);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        *reinterpret_cast<float*>(stg + stg_off((lane >> 4) * 4 + r, j * 16 + (lane & 15))) = acc[i][j][r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own-wave LDS writes retired
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int lr = p * 8 + (lane >> 3);
+      const floatx4 x0 = *reinterpret_cast<const floatx4*>(stg + stg_off(lr, cw * 8));
+      const floatx4 x1 = *reinterpret_cast<const floatx4*>(stg + stg_off(lr, cw * 8 + 4));
+      float o[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = bf2f(f2bf(o[q] * e.alpha + bias8[q]));  // the stored bf16 qkv values
+      const int soff = (i * 16 + p * 8) * e.rstride;
+      const uint4 w = pack8(o);
+      store_b128_padded(u32x4{w.x, w.y, w.z, w.w}, e.rs, (int)e.voff, soff);
+      if (qk) {
+        float ss = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) ss += o[q] * o[q];
+        ss += __shfl_xor(ss, 1, 64);
+        ss += __shfl_xor(ss, 2, 64);
+        ss += __shfl_xor(ss, 4, 64);
+        const float rr = rsqrtf(ss * (1.f / 64.f) + g.qk_eps);
+        float y[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float a = bf2f(f2bf((o[2 * q] * rr) * wf[2 * q]));
+          const float b = bf2f(f2bf((o[2 * q + 1] * rr) * wf[2 * q + 1]));
+          y[2 * q] = (a * cc[p][q] - b * sc[p][q]) * osc;
+          y[2 * q + 1] = (a * sc[p][q] + b * cc[p][q]) * osc;
+        }
+        const uint4 w2 = pack8(y);
+        store_b128_padded(u32x4{w2.x, w2.y, w2.z, w2.w}, r2, (int)voff2, (i * 16 + p * 8) * rstride2);
+      }
+    }
+    if (i < 7) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) { cc[p] = cn[p]; sc[p] = sn[p]; }
     }
   }
 }
@@ -1007,7 +1102,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
       }
     }
     RingItem nx;
-    if (next < items) {
+    if (next < items && EPI != EPI_QKN) {
       nx = ring_item<AK, BK_, SW>(g, next, items, tiles, tiles_n, wid, lane);
       ring_issue<AK, BK_, SW>(g, nx, 0, lds0, wid, lane);
       if (nx.nk > 1) ring_issue<AK, BK_, SW>(g, nx, 1, lds0, wid, lane);
@@ -1024,6 +1119,8 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
       if (s == 1.2345e37f) reinterpret_cast<float*>(g.C)[threadIdx.x] = s;
     } else if (SW) {
       epilogue_ring_swf(g, acc, stg, lane, it, wm, wn, bias8, bias8b);
+    } else if (EPI == EPI_QKN) {
+      epilogue_ring_qkn(g, acc, stg, lane, ea, bias8, it, wm, wn);
     } else if (GF == 2) {
       epilogue_ring<EPI, 0, 2>(g, acc, stg, lane, ea, bias8, pre);
       epi_preload<EPI, 2>(g, ea, pre);
@@ -1042,11 +1139,18 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
     if (TL) tl_stamp(g, kth, 3, wid, lane);
     ++kth;
     if (next >= items) break;
+    if (EPI == EPI_QKN) {  // the next item's first tiles after this epilogue (its table loads are compiler-waited)
+      nx = ring_item<AK, BK_, SW>(g, next, items, tiles, tiles_n, wid, lane);
+      ring_issue<AK, BK_, SW>(g, nx, 0, lds0, wid, lane);
+      if (nx.nk > 1) ring_issue<AK, BK_, SW>(g, nx, 1, lds0, wid, lane);
+      if (nx.nk > 2) ring_issue<AK, BK_, SW>(g, nx, 2, lds0, wid, lane);
+    }
     // The next item's first LDS-DMA into stage 3 (tile 3, issued at its K step 0) follows its barrier
     // X_0, which every wave reaches only after its staging reads (raw_barrier: lgkmcnt(0) first).
     item = next;
     it = nx;
-    pend = ABL == 3 || ABL == 5 ? 0 : S;  // the epilogue's S stores are younger than the next item's pre-issued tiles 0-2
+    // the epilogue's S stores are younger than the next item's pre-issued tiles 0-2 (EPI_QKN: older)
+    pend = ABL == 3 || ABL == 5 || EPI == EPI_QKN ? 0 : S;
   }
 }
 
@@ -1101,7 +1205,13 @@ int launch_ring(const GemmArgs& g, int splits, hipStream_t s) {
   else if (epi == EPI_ACC)
     hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, SW, SW ? 0 : EPI_ACC>), dim3(grid), dim3(512),
                        LDS, s, gl);
-  else
+  else if (epi == EPI_QKN) {
+    if constexpr (AK && BK_ && SW == 0 && ABL == 0 && !STAMP && !TL && !DMAC)
+      hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, 0, EPI_QKN>), dim3(grid), dim3(512), LDS, s,
+                         gl);
+    else
+      VPT_CHECK_ARG(false, "gemm ring: the QK-norm epilogue is a forward (k-major x k-major) mode");
+  } else
     hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, SW, EPI_PLAIN>), dim3(grid), dim3(512), LDS, s,
                        gl);
   VPT_LAUNCH_CHECK();
@@ -1308,6 +1418,36 @@ extern "C" int vpt_gemm_bf16_tiled(const void* A, long lda, int a_kmajor, const 
   VPT_CHECK_ARG(ring_grid >= 0 && ring_grid <= 65536, "vpt_gemm_bf16_tiled: ring_grid 0..65536");
   return gemm_impl(A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, M, N, K, bias, resid, ldr, out_mode, act, splits,
                    workspace, alpha, geometry, ring_grid, stream);
+}
+
+// The JiT attention input projection with its per-head QK-RMSNorm + RoPE in the epilogue: qkv[M][3D] = x . W^T + b
+// (bf16, as vpt_gemm_bf16) and qk[M][2D] = (rope(rms(q) wq) * q_scale | rope(rms(k) wk)) -- bitwise what
+// vpt_qknorm_rope_fwd computes from that qkv (src/models/jit/denoiser.py:307-316, 318-323, 369-373, 98-111). Always
+// the 256x256 ring (its epilogue owns whole 64-column heads).
+extern "C" int vpt_linear_qknorm_rope(const void* x, long ldx, const void* w, long ldw, const void* bias, void* qkv,
+                                      long ldqkv, void* qk, long ldqk, int M, int D, int K, const void* wq,
+                                      const void* wk, const float* cos_t, const float* sin_t, int rows_per_seq,
+                                      float eps, float q_scale, void* stream) {
+  VPT_CHECK_ARG(x && w && qkv && qk && wq && wk && cos_t && sin_t, "vpt_linear_qknorm_rope: null pointer");
+  VPT_CHECK_ARG(M > 0 && K > 0 && D > 0 && D % 64 == 0 && K % 8 == 0 && rows_per_seq > 0,
+                "vpt_linear_qknorm_rope: heads of 64, K % 8 == 0");
+  VPT_CHECK_ARG(ldx % 8 == 0 && ldw % 8 == 0 && ldqkv % 8 == 0 && ldqk % 8 == 0 && ldqkv >= 3L * D && ldqk >= 2L * D,
+                "vpt_linear_qknorm_rope: 16-B leading dims, qkv >= 3D and qk >= 2D columns");
+  GemmArgs g = {};
+  g.A = (const bf16_t*)x; g.lda = ldx;
+  g.B = (const bf16_t*)w; g.ldb = ldw;
+  g.bias = (const bf16_t*)bias;
+  g.M = M; g.N = 3 * D; g.K = K;
+  g.act = ACT_NONE;
+  g.alpha = 1.f;
+  g.k_split = K; g.splits = 1;
+  g.C = qkv; g.ldc = ldqkv; g.out_mode = OUT_BF16;
+  g.C2 = (bf16_t*)qk; g.ldc2 = ldqk;
+  g.qk_d = D; g.rps = rows_per_seq;
+  g.qk_wq = (const bf16_t*)wq; g.qk_wk = (const bf16_t*)wk;
+  g.rcos = cos_t; g.rsin = sin_t;
+  g.qk_scale = q_scale; g.qk_eps = eps;
+  return launch_ring<true, true, true>(g, 1, (hipStream_t)stream);
 }
 
 namespace {

@@ -215,10 +215,10 @@ class JiTEngine:
         M = x.shape[0]
         n_i = rows if (n_ctx and self._ctx_present(i)) else n_pre
         xn1, rstd1 = ops.rmsnorm_fwd(x, w["pn1"], pool.get(tag + "xn1", (M, D)), pool.get(tag + "rstd1", (M,), F32))
-        qkv = ops.linear(xn1, w["pwqkv"], w["pbqkv"], out=pool.get(tag + "qkv", (M, 3 * D)))
-        qk = ops.qknorm_rope_fwd(qkv, w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, rows,
-                                 out=pool.get(tag + "qk", (M, 2 * D)),
-                                 q_scale=ops.attn_q_scale(1.0 / math.sqrt(cfg.head_dim)))
+        # q|k|v projection with the per-head QK-RMSNorm + RoPE (q pre-scaled for the attention kernels) in its epilogue
+        qkv, qk = ops.linear_qknorm_rope(xn1, w["pwqkv"], w["pbqkv"], pool.get(tag + "qkv", (M, 3 * D)),
+                                         pool.get(tag + "qk", (M, 2 * D)), w["pqk_norm"][:64], w["pqk_norm"][64:],
+                                         cos_t, sin_t, rows, q_scale=ops.attn_q_scale(1.0 / math.sqrt(cfg.head_dim)))
         o = pool.get(tag + "o", (M, D))
         lse = pool.get(tag + "lse", (B, Hh, rows), F32)
         ops.attn_fwd(ops._t4(qk, B, rows, Hh, 0), ops._t4(qk, B, rows, Hh, D), ops._t4(qkv, B, rows, Hh, 2 * D),

@@ -272,6 +272,30 @@ def linear(x, w, bias=None, resid=None, out=None, act=ACT_NONE, **tile):
     return gemm(x, True, w, True, M, N, K, out, bias=bias, resid=resid, act=act, **tile)
 
 
+def linear_qknorm_rope(x, w, bias, qkv, qk, wq, wk, cos_t, sin_t, rows_per_seq, q_scale=1.0, eps=1e-6):
+    """qkv = x @ w.T + bias (bf16, [M, 3D]) and qk = (rope(rms(q)) * q_scale | rope(rms(k))) [M, 2D] in ONE ring GEMM
+    (vpt_linear_qknorm_rope: the norm + RoPE in the epilogue) -- what linear + qknorm_rope_fwd compute, bitwise."""
+    M, K = x.shape
+    N = w.shape[0]
+    D = N // 3
+    for t, n in ((x, "x"), (w, "w"), (qkv, "qkv"), (qk, "qk"), (wq, "wq"), (wk, "wk")):
+        _chk(t, BF16, n)
+    if bias is not None:
+        _chk(bias, BF16, "bias")
+
+    def run():
+        call("vpt_linear_qknorm_rope", x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), _p(bias), qkv.data_ptr(),
+             qkv.stride(0), qk.data_ptr(), qk.stride(0), M, D, K, wq.data_ptr(), wk.data_ptr(), cos_t.data_ptr(),
+             sin_t.data_ptr(), rows_per_seq, float(eps), float(q_scale), stream())
+    pr = PROBES.get("gemm")
+    if pr is None:
+        run()
+    else:
+        pr.record(2.0 * M * N * K, run, key=f"fwd+qkn M{M} N{N} K{K} s1",
+                  nbytes=2.0 * (M + N) * K + M * N * 2 + M * 2 * D * 2)
+    return qkv, qk
+
+
 def linear_dgrad(dy, w, out=None, resid=None, **tile):
     """dx = dy @ w (+resid) (dy [M,N], w [N,K]) — nn.Linear input gradient (resid: a second bf16 gradient
     of the same input, summed with the reference's bf16 rounding)."""
