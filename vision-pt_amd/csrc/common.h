@@ -67,6 +67,33 @@ __device__ __forceinline__ void swiglu_bwd1(float gd, float a, float b, float& d
   d1 = ds * (sg * (1.f + a * (1.f - sg)));
 }
 
+// Per-head QK-RMSNorm + RoPE forward math on one lane's 8 consecutive head dims (4 RoPE pairs), shared by
+// qknorm_rope_fwd_kernel (norm.hip) and the QKV GEMM's fused epilogue (gemm.hip), contraction off so both compile to
+// the same operations (tested bitwise equal). qkn_sumsq8: the lane's part of the sum of squares (the callers add the
+// other 7 lanes' parts by xor-shuffles 1, 2, 4); qkn_rope8: y = rope(bf16(x r w)) * osc with r = rsqrt(ss / 64 + eps).
+__device__ __forceinline__ float qkn_sumsq8(const float (&f)[8]) {
+#pragma clang fp contract(off)
+  float ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ss += f[e] * f[e];
+  return ss;
+}
+__device__ __forceinline__ float qkn_rstd(float ss, float eps) {
+#pragma clang fp contract(off)
+  return rsqrtf(ss * (1.f / 64.f) + eps);
+}
+__device__ __forceinline__ void qkn_rope8(const float (&f)[8], float r, const float (&w)[8], const float (&c)[4],
+                                          const float (&sn)[4], float osc, float (&y)[8]) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a = bf2f(f2bf((f[2 * i] * r) * w[2 * i]));
+    const float b = bf2f(f2bf((f[2 * i + 1] * r) * w[2 * i + 1]));
+    y[2 * i] = (a * c[i] - b * sn[i]) * osc;
+    y[2 * i + 1] = (a * sn[i] + b * c[i]) * osc;
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -838,21 +838,15 @@ __device__ __forceinline__ void epilogue_ring_qkn(const GemmArgs& g, const float
       const uint4 w = pack8(o);
       store_b128_padded(u32x4{w.x, w.y, w.z, w.w}, e.rs, (int)e.voff, soff);
       if (qk) {
-        float ss = 0.f;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) ss += o[q] * o[q];
+        float ss = qkn_sumsq8(o);
         ss += __shfl_xor(ss, 1, 64);
         ss += __shfl_xor(ss, 2, 64);
         ss += __shfl_xor(ss, 4, 64);
-        const float rr = rsqrtf(ss * (1.f / 64.f) + g.qk_eps);
+        const float rr = qkn_rstd(ss, g.qk_eps);
+        const float c4[4] = {cc[p][0], cc[p][1], cc[p][2], cc[p][3]};
+        const float s4[4] = {sc[p][0], sc[p][1], sc[p][2], sc[p][3]};
         float y[8];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float a = bf2f(f2bf((o[2 * q] * rr) * wf[2 * q]));
-          const float b = bf2f(f2bf((o[2 * q + 1] * rr) * wf[2 * q + 1]));
-          y[2 * q] = (a * cc[p][q] - b * sc[p][q]) * osc;
-          y[2 * q + 1] = (a * sc[p][q] + b * cc[p][q]) * osc;
-        }
+        qkn_rope8(o, rr, wf, c4, s4, osc, y);
         const uint4 w2 = pack8(y);
         store_b128_padded(u32x4{w2.x, w2.y, w2.z, w2.w}, r2, (int)voff2, (i * 16 + p * 8) * rstride2);
       }

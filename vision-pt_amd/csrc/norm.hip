@@ -173,23 +173,15 @@ __global__ __launch_bounds__(256) void qknorm_rope_fwd_kernel(const bf16_t* __re
     const long pos = row % rows_per_seq;
     float f[8];
     unpack8(*reinterpret_cast<const uint4*>(qkv + row * ldin + which * D + head * 64 + part * 8), f);
-    float ss = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) ss += f[e] * f[e];
+    float ss = qkn_sumsq8(f);
     ss += __shfl_xor(ss, 1, 64);
     ss += __shfl_xor(ss, 2, 64);
     ss += __shfl_xor(ss, 4, 64);
-    const float r = rsqrtf(ss * (1.f / 64.f) + eps);
+    const float r = qkn_rstd(ss, eps);
     float c[4], s[4];
     rope_load(cs, sn, pos, part, c, s);
     float o[8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float a = bf2f(f2bf((f[2 * i] * r) * wf[2 * i]));
-      const float b = bf2f(f2bf((f[2 * i + 1] * r) * wf[2 * i + 1]));
-      o[2 * i] = (a * c[i] - b * s[i]) * osc;
-      o[2 * i + 1] = (a * s[i] + b * c[i]) * osc;
-    }
+    qkn_rope8(f, r, wf, c, s, osc, o);
     *reinterpret_cast<uint4*>(out + row * ldout + which * D + head * 64 + part * 8) = pack8(o);
   }
 }
