@@ -138,6 +138,13 @@ int vpt_attn_fwd(const void* q, long q_sb, long q_sh, long q_sr, const void* k, 
                  const void* v, long v_sb, long v_sh, long v_sr, void* o, long o_sb, long o_sh, long o_sr,
                  float* lse, long l_sb, long l_sh, const float* kbias, long kb_sb, int B, int H, int n,
                  int nk, int n_dense, float scale, void* stream);
+/* vpt_attn_fwd for QK-RMSNormed inputs (JiT: q, k = rope(rms(x) w), q pre-scaled; wq / wk the q_norm / k_norm
+ * weights [64]): the same outputs computed with a fixed softmax reference point -- the scores' Cauchy-Schwarz bound
+ * from the norm weights -- instead of a running row maximum, while that bound stays below 60 (log2 units). */
+int vpt_attn_fwd_qknorm(const void* q, long q_sb, long q_sh, long q_sr, const void* k, long k_sb, long k_sh,
+                        long k_sr, const void* v, long v_sb, long v_sh, long v_sr, void* o, long o_sb, long o_sh,
+                        long o_sr, float* lse, long l_sb, long l_sh, const float* kbias, long kb_sb, const void* wq,
+                        const void* wk, int B, int H, int n, int nk, int n_dense, float scale, void* stream);
 int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr, const void* k, long k_sb, long k_sh, long k_sr,
                  const void* v, long v_sb, long v_sh, long v_sr, const void* o, long o_sb, long o_sh, long o_sr,
                  const void* dO, long do_sb, long do_sh, long do_sr, const float* lse, float* delta, long l_sb,
@@ -149,8 +156,9 @@ int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr, const void* k, 
  * the normed, roped (q pre-scaled) attention inputs as for vpt_attn_bwd; xq / xk the raw projections they came from
  * (same strides x_*), wq / wk the q_norm / k_norm weights [64], cos_t / sin_t the RoPE tables [positions][32] (a
  * row's position is its row: n == nk). dq / dk (strides dqk_*) receive d loss / d (raw q, k) in bf16, computed from
- * the f32 attention gradients; dwq_part / dwk_part [vpt_attn_bwd_dw_rows(B, H, n)][64] receive per-workgroup partial
- * q_norm / k_norm weight gradients (sum them with vpt_reduce_rows, fixed order). */
+ * the f32 attention gradients; dwq_part / dwk_part receive per-workgroup partial q_norm / k_norm weight gradients,
+ * vpt_attn_bwd_dw_rows(B, H, n) rows of 64 floats at row stride dw_ld (dwk_part = dwq_part + 64 with dw_ld = 128
+ * interleaves them, so ONE vpt_reduce_rows over [rows][128] sums both in a fixed order). */
 int vpt_attn_bwd_dw_rows(int B, int H, int n);
 int vpt_attn_bwd_qknorm(const void* q, long q_sb, long q_sh, long q_sr, const void* k, long k_sb, long k_sh, long k_sr,
                         const void* v, long v_sb, long v_sh, long v_sr, const void* o, long o_sb, long o_sh, long o_sr,
@@ -158,7 +166,7 @@ int vpt_attn_bwd_qknorm(const void* q, long q_sb, long q_sh, long q_sr, const vo
                         long l_sh, const float* kbias, long kb_sb, const void* xq, const void* xk, long x_sb,
                         long x_sh, long x_sr, const void* wq, const void* wk, const float* cos_t, const float* sin_t,
                         float eps, void* dq, void* dk, long dqk_sb, long dqk_sh, long dqk_sr, float* dwq_part,
-                        float* dwk_part, void* dv, long dv_sb, long dv_sh, long dv_sr, int B, int H, int n, int nk,
+                        float* dwk_part, long dw_ld, void* dv, long dv_sb, long dv_sh, long dv_sr, int B, int H, int n, int nk,
                         int n_dense, float scale, void* stream);
 
 /* ---- RMSNorm over the hidden dim -----------------------------------------------------------

@@ -400,15 +400,14 @@ def test_attention_bwd_fused_qknorm_rope(ops, n, n_dense, masked):
     sentinel = 7.0
     dqkv = torch.full((M, 3 * D), sentinel, dtype=torch.bfloat16, device=DEV)
     nd = ops.attn_bwd_dw_rows(B, H, n)
-    part = torch.full((2, nd, 64), float("nan"), device=DEV)
+    part = torch.full((nd, 128), float("nan"), device=DEV)
     delta = torch.zeros(B, H, rows, device=DEV)
     ops.attn_bwd_qknorm(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, kb, ops._t4(qkv, B, rows, H, 0),
                         ops._t4(qkv, B, rows, H, D), wq, wk, cos, sin, ops._t4(dqkv, B, rows, H, 0),
-                        ops._t4(dqkv, B, rows, H, D), part[0], part[1], ops._t4(dqkv, B, rows, H, 2 * D),
+                        ops._t4(dqkv, B, rows, H, D), part, ops._t4(dqkv, B, rows, H, 2 * D),
                         B, H, rows, n, n_dense)
     dw = torch.zeros(128, device=DEV)
-    ops.reduce_rows(part[0], dw[:64])
-    ops.reduce_rows(part[1], dw[64:])
+    ops.reduce_rows(part, dw)
     # fp32 reference over the valid rows
     x = qkv.float().view(B, rows, 3 * D)[:, :n].reshape(B * n, 3 * D).requires_grad_(True)
     wqf, wkf = wq.float().requires_grad_(True), wk.float().requires_grad_(True)
@@ -444,6 +443,47 @@ def test_attention_bwd_fused_qknorm_rope(ops, n, n_dense, masked):
     assert rel(got[:, :n, :2 * D], g2[:, :n, :2 * D]) < 1e-2
     assert torch.equal(got[:, :n, 2 * D:], g2[:, :n, 2 * D:])  # dV is the same kernel path
     assert p2 is not None
+
+
+@pytest.mark.parametrize("n,n_dense,wscale", [(1034, 1024, 1.0), (700, 520, 1.0), (4170, 4106, 1.5), (700, 520, 3.0)])
+def test_attention_fwd_fixed_reference(ops, n, n_dense, wscale):
+    """vpt_attn_fwd_qknorm (softmax with the QK-norm score bound as a fixed reference point instead of the running row
+    maximum) vs vpt_attn_fwd (online maximum) on QK-RMSNormed, roped inputs: the same attention up to f32 / bf16
+    rounding, and the -LSE both hand the backward. wscale 3 puts the bound above 60 (log2 units): the online path,
+    bitwise equal to vpt_attn_fwd."""
+    B, H, rows = 2, 3, ((n + 127) // 128) * 128
+    D = H * 64
+    qkv = rnd(B * rows, 3 * D, seed=70)
+    wq = (wscale * (1 + rnd(64, scale=0.2, seed=71).float())).to(torch.bfloat16)
+    wk = (wscale * (1 + rnd(64, scale=0.2, seed=72).float())).to(torch.bfloat16)
+    cos, sin = _rope_tables(rows, seed=73)
+    qk = ops.qknorm_rope_fwd(qkv, wq, wk, cos, sin, rows, q_scale=ops.attn_q_scale(0.125))
+    kb = torch.zeros(B, rows, device=DEV)
+    kb[:, n_dense + (n - n_dense) // 2:] = float("-inf")
+    kb[1, n_dense:] = 0.0
+    q4, k4, v4 = ops._t4(qk, B, rows, H, 0), ops._t4(qk, B, rows, H, D), ops._t4(qkv, B, rows, H, 2 * D)
+    o1 = torch.zeros(B * rows, D, dtype=torch.bfloat16, device=DEV)
+    o2 = torch.zeros_like(o1)
+    l1 = torch.zeros(B, H, rows, device=DEV)
+    l2 = torch.zeros_like(l1)
+    ops.attn_fwd(q4, k4, v4, ops._t4(o1, B, rows, H), l1, kb, B, H, rows, n, n_dense)
+    ops.attn_fwd_qknorm(q4, k4, v4, ops._t4(o2, B, rows, H), l2, kb, wq, wk, B, H, rows, n, n_dense)
+    torch.cuda.synchronize()
+    bound = 0.125 * 1.4426950408889634 * 64 * wq.float().abs().max().item() * wk.float().abs().max().item() * 1.0625
+    v1 = o1.view(B, rows, D)[:, :n].float()
+    v2 = o2.view(B, rows, D)[:, :n].float()
+    if bound >= 60:
+        assert torch.equal(v1, v2) and torch.equal(l1[..., :n], l2[..., :n])
+        return
+    assert rel(v2, v1) < 4e-3
+    assert (l2[..., :n] - l1[..., :n]).abs().max().item() < 1e-4 * max(1.0, l1[..., :n].abs().max().item())
+    # and against fp32 attention of the same (bf16) q~, k, v
+    def heads(t, c0, ld):
+        return t.float().view(B, rows, ld)[:, :n, c0:c0 + D].reshape(B, n, H, 64).permute(0, 2, 1, 3)
+    qf = heads(qk, 0, 2 * D) / ops.attn_q_scale(0.125) * 1.0
+    kf, vf = heads(qk, D, 2 * D), heads(qkv, 2 * D, 3 * D)
+    ref = _attn_ref(qf, kf, vf, kb[:, :n], 0.125).permute(0, 2, 1, 3).reshape(B, n, D)
+    assert rel(v2, ref) < 1e-2
 
 
 @pytest.mark.parametrize("n,nk,masked", [(300, 231, False), (1000, 77, True), (64, 500, True)])

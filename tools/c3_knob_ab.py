@@ -1,0 +1,80 @@
+"""In-process A/B of the JiT engine's module-level switches (vpt.engine: FUSED_QKNORM_FWD, FUSED_QKNORM_BWD,
+FIXREF_ATTN_FWD): one JiT-B/16 trainer at C3 (B=8, the 5 buckets round-robin, fused optimizer), then rounds of K timed
+steps alternating the knob(s) on / off, so allocation, clocks and box are shared; medians of ms per step.
+
+  python tools/c3_knob_ab.py FIXREF_ATTN_FWD [--rounds 6] [--steps 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "vision-pt_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from vpt import engine  # noqa: E402
+from vpt.config import JiT_B_16_Config, JiTTrainingConfig  # noqa: E402
+from vpt.jit_train import JiTTrainer  # noqa: E402
+from vpt.optim import RAdamScheduleFreeFlat  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("knobs", help="comma-separated vpt.engine globals switched together")
+    ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--steps", type=int, default=5)
+    args = ap.parse_args()
+    knobs = args.knobs.split(",")
+    for k in knobs:
+        if not isinstance(getattr(engine, k), bool):
+            raise SystemExit(f"{k}: not a boolean knob of vpt.engine")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    tr = JiTTrainer(JiT_B_16_Config(), bench.N_CLASSES, JiTTrainingConfig(loss_target="image"), device=dev, seed=1)
+    tr.engine.init_weights(seed=0)
+    opt = RAdamScheduleFreeFlat(tr.engine.params, tr.engine.grads, lr=1e-4)
+    opt.train()
+    batches = bench.make_batches(8, dev, seed=100)
+    it = [0]
+
+    def step():
+        b = batches[it[0] % len(batches)]
+        it[0] += 1
+        tr.step(b["images"], b["ids"], b["mask"], b["original_size"], b["target_size"], b["crop_coords"])
+        opt.step()
+
+    def setk(v):
+        for k in knobs:
+            setattr(engine, k, v)
+
+    for v in (True, False):
+        setk(v)
+        for _ in range(len(batches)):
+            step()
+    torch.cuda.synchronize()
+    res = {"1": [], "0": []}
+    for r in range(args.rounds):
+        for v in ((True, False) if r % 2 == 0 else (False, True)):
+            setk(v)
+            step()  # one untimed step after the switch
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            res["1" if v else "0"].append((time.perf_counter() - t0) / args.steps * 1e3)
+        print(f"round {r}: on {res['1'][-1]:.3f} ms  off {res['0'][-1]:.3f} ms", flush=True)
+    med = {k: sorted(v)[len(v) // 2] for k, v in res.items()}
+    print(json.dumps({"knobs": knobs, "ms_per_step": {k: [round(x, 3) for x in v] for k, v in res.items()},
+                      "median_ms": {k: round(v, 3) for k, v in med.items()},
+                      "img_s_median": {k: round(8e3 / v, 3) for k, v in med.items()},
+                      "gain": round(med["0"] / med["1"] - 1, 4)}))
+
+
+if __name__ == "__main__":
+    main()

@@ -50,7 +50,8 @@ struct AttnArgs {
   const bf16_t* wq; const bf16_t* wk;   // q_norm / k_norm weights [64]
   const float* rcos; const float* rsin; // RoPE tables [positions][32]
   float eps;
-  float* dwq; float* dwk;               // per-workgroup partial weight gradients [workgroups][64]
+  float* dwq; float* dwk;               // per-workgroup partial weight gradients, rows of 64 at stride dw_ld
+  long dw_ld;
 };
 
 constexpr float kNegInf = -__builtin_huge_valf();
@@ -361,10 +362,18 @@ __device__ __forceinline__ void fill_key_bias(float* kbl, const AttnArgs& g, int
 // NW waves per block, 32 query rows per wave: one K/V tile staged per block serves 32*NW queries.
 // Occupancy: 134 VGPRs -> 3 waves per SIMD with 4-wave blocks (forcing <= 128 VGPRs for 4 waves
 // spills inside the tile loop and measured slower: 749 vs 823 TFLOP/s).
-template <int NW>
-__global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnArgs g) {
-  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];
-  extern __shared__ __attribute__((aligned(16))) float kbl[];  // key bias of keys kb0.. (fill_key_bias)
+//
+// FIX (fixed reference point, vpt_attn_fwd_qknorm): when q and k are QK-RMSNormed (JiT, denoiser.py:307-316), every
+// score is bounded by Cauchy-Schwarz: |q~.k| <= ||q~|| ||k|| <= (c 8 max|w_q|) (8 max|w_k|) = bound (log2 units, q~ the
+// pre-scaled query, ||rms(x)|| <= 8 for 64 dims, RoPE a rotation; with margin for the bf16 roundings). Then
+// p = exp2(s - bound) <= 1 needs no running row maximum: the per-tile fmax reduction, its lane-pair exchange and the
+// rescale test -- a third of the loop's VALU at head_dim 64, where the softmax and not the MFMA bounds the loop --
+// are gone. The caller's kernel takes this path only while bound < kFixMax (p >= 2^-2 bound stays a normal float:
+// no underflow of the largest p); otherwise the online-max path below.
+constexpr float kFixMax = 60.f;
+
+template <int NW, bool FIX>
+__device__ __forceinline__ void fwd_body(const AttnArgs& g, float bound, char (&lds)[2][2][8192], float* kbl) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
   const int b = blockIdx.z, hd = blockIdx.y;
   const int q0 = blockIdx.x * (32 * NW) + wid * 32;
@@ -378,8 +387,8 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnArgs g) {
   floatx16 oacc[2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) { oacc[0][i] = 0.f; oacc[1][i] = 0.f; }
-  float m_c = 0.f, lsum = 0.f;  // running reference point (log2 units), row sum
-  floatx16 nm = splat16(0.f);   // -m_c: the S^T chain's initial accumulator, so it ends at S - m_c
+  float m_c = FIX ? bound : 0.f, lsum = 0.f;  // reference point (log2 units), row sum
+  floatx16 nm = splat16(-m_c);  // -m_c: the S^T chain's initial accumulator, so it ends at S - m_c
 
   const int nt = (g.nk + 63) / 64;
   const void* Ku = uniform_ptr(K);
@@ -419,29 +428,31 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnArgs g) {
           for (int e = 0; e < 4; ++e) sacc[kb][4 * g4 + e] += bias[e];
         }
     }
-    float mx = kNegInf;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[kb][i]);
-    mx = pair_max(mx);
-    // Lazy rescale: the reference point m_c moves only on the first tile and when a tile's max
-    // exceeds it by more than tau (p <= 2^tau otherwise); wave-uniform branch, rarely taken after t=0.
-    const bool up = t == 0 || mx > g.tau;
-    if (__builtin_amdgcn_ballot_w64(up)) {
-      const float sh = up && mx != kNegInf ? mx : 0.f;  // shift of the reference point
-      if (t > 0) {
-        const float alpha = __builtin_amdgcn_exp2f(-sh);
-        lsum *= alpha;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
-      }
+    if (!FIX) {
+      float mx = kNegInf;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sacc[kb][i] -= sh;
-      m_c += sh;
-      nm = splat16(-m_c);
+        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[kb][i]);
+      mx = pair_max(mx);
+      // Lazy rescale: the reference point m_c moves only on the first tile and when a tile's max
+      // exceeds it by more than tau (p <= 2^tau otherwise); wave-uniform branch, rarely taken after t=0.
+      const bool up = t == 0 || mx > g.tau;
+      if (__builtin_amdgcn_ballot_w64(up)) {
+        const float sh = up && mx != kNegInf ? mx : 0.f;  // shift of the reference point
+        if (t > 0) {
+          const float alpha = __builtin_amdgcn_exp2f(-sh);
+          lsum *= alpha;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
+        }
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) sacc[kb][i] -= sh;
+        m_c += sh;
+        nm = splat16(-m_c);
+      }
     }
     float ps = 0.f;
 #pragma unroll
@@ -470,6 +481,23 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnArgs g) {
   const int qrow = q0 + (lane & 31);
   store_T(g.o, (long)b * g.o.sb + hd * g.o.sh, oacc, inv, qrow, g.n, lane, false);
   if (lane < 32 && qrow < g.n) g.lse[b * g.l_sb + hd * g.l_sh + qrow] = -(m_c + __log2f(l));  // -LSE, log2
+}
+
+template <int NW, bool QKN = false>
+__global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnArgs g) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];
+  extern __shared__ __attribute__((aligned(16))) float kbl[];  // key bias of keys kb0.. (fill_key_bias)
+  if (QKN) {
+    // score bound from the QK-norm weights (every wave computes the same value: wave-uniform branch)
+    const int lane = threadIdx.x & 63;
+    const float aq = fabsf(bf2f(g.wq[lane])), ak = fabsf(bf2f(g.wk[lane]));
+    const float bound = g.scale_log2 * 64.f * wave_max(aq) * wave_max(ak) * 1.0625f;
+    if (bound < kFixMax) {
+      fwd_body<NW, true>(g, bound, lds, kbl);
+      return;
+    }
+  }
+  fwd_body<NW, false>(g, 0.f, lds, kbl);
 }
 
 // ------------------------------------------------------------------ backward preprocess
@@ -673,7 +701,7 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
   for (int v = 0; v < 32; ++v) dwp[v] = 0.f;
   qkn_bwd_row(g, g.xk, g.dk, b, hd, dkT, 0.69314718055994531f, wf, key, g.nk, lane, kmasked, dwp);
   qkn_dw_partial<NW>(reinterpret_cast<float*>(&lds[0][0][0]), &lstat[0][0][0], dwp,
-                     g.dwk + ((long)(b * g.H + hd) * ((g.nk + 32 * NW - 1) / (32 * NW)) + bx) * 64, tid);
+                     g.dwk + ((long)(b * g.H + hd) * ((g.nk + 32 * NW - 1) / (32 * NW)) + bx) * g.dw_ld, tid);
 }
 
 // ------------------------------------------------------------------ backward dQ
@@ -826,7 +854,7 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
   for (int v = 0; v < 32; ++v) dwp[v] = 0.f;
   qkn_bwd_row(g, g.xq, g.dq, b, hd, dqT, g.scale, wf, qrow, g.n, lane, false, dwp);
   qkn_dw_partial<NW>(reinterpret_cast<float*>(&lds[0][0][0]), red2,
-                     dwp, g.dwq + ((long)(b * g.H + hd) * ((g.n + 32 * NW - 1) / (32 * NW)) + bx) * 64, tid);
+                     dwp, g.dwq + ((long)(b * g.H + hd) * ((g.n + 32 * NW - 1) / (32 * NW)) + bx) * g.dw_ld, tid);
 }
 
 // The production backward as ONE launch over both block kinds: the dK/dV blocks first (the longer ones),
@@ -901,11 +929,43 @@ extern "C" int vpt_attn_fwd(const void* q, long q_sb, long q_sh, long q_sr,
   g.tau = g_tau;
   g.kb0 = g.n_dense / 64 * 64;
   if (g_waves != 8)
-    hipLaunchKernelGGL(attn_fwd_kernel<4>, dim3((n + 127) / 128, H, B), dim3(256), key_bias_lds_bytes(g),
+    hipLaunchKernelGGL((attn_fwd_kernel<4>), dim3((n + 127) / 128, H, B), dim3(256), key_bias_lds_bytes(g),
                        (hipStream_t)stream, g);
   else
     hipLaunchKernelGGL(attn_fwd_kernel<8>, dim3((n + 255) / 256, H, B), dim3(512), key_bias_lds_bytes(g),
                        (hipStream_t)stream, g);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+// vpt_attn_fwd for QK-RMSNormed q / k (JiT self-attention: q, k = rope(rms(x) w), q pre-scaled): the same results,
+// computed with a fixed softmax reference point (the Cauchy-Schwarz bound of the scores from the q_norm / k_norm
+// weights wq, wk [64]) while that bound is below kFixMax -- no running row maximum in the loop; larger weights take
+// the online-maximum path.
+extern "C" int vpt_attn_fwd_qknorm(const void* q, long q_sb, long q_sh, long q_sr,
+                                   const void* k, long k_sb, long k_sh, long k_sr,
+                                   const void* v, long v_sb, long v_sh, long v_sr,
+                                   void* o, long o_sb, long o_sh, long o_sr,
+                                   float* lse, long l_sb, long l_sh,
+                                   const float* kbias, long kb_sb, const void* wq, const void* wk,
+                                   int B, int H, int n, int nk, int n_dense, float scale, void* stream) {
+  int rc = check_common(B, H, n, nk);
+  if (rc) return rc;
+  VPT_CHECK_ARG(q && k && v && o && lse && wq && wk, "vpt_attn_fwd_qknorm: null pointer");
+  AttnArgs g = {};
+  g.q = {(const bf16_t*)q, q_sb, q_sh, q_sr};
+  g.k = {(const bf16_t*)k, k_sb, k_sh, k_sr};
+  g.v = {(const bf16_t*)v, v_sb, v_sh, v_sr};
+  g.o = {(bf16_t*)o, o_sb, o_sh, o_sr};
+  g.lse = lse; g.l_sb = l_sb; g.l_sh = l_sh;
+  g.kbias = kbias; g.kb_sb = kb_sb;
+  g.n = n; g.nk = nk; g.n_dense = n_dense < nk ? n_dense : nk;
+  g.scale = scale; g.scale_log2 = scale * 1.4426950408889634f;
+  g.tau = g_tau;
+  g.kb0 = g.n_dense / 64 * 64;
+  g.wq = (const bf16_t*)wq; g.wk = (const bf16_t*)wk;
+  hipLaunchKernelGGL((attn_fwd_kernel<4, true>), dim3((n + 127) / 128, H, B), dim3(256), key_bias_lds_bytes(g),
+                     (hipStream_t)stream, g);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
@@ -962,7 +1022,7 @@ extern "C" int vpt_attn_bwd_qknorm(const void* q, long q_sb, long q_sh, long q_s
                                    const void* xq, const void* xk, long x_sb, long x_sh, long x_sr,
                                    const void* wq, const void* wk, const float* cos_t, const float* sin_t, float eps,
                                    void* dq, void* dk, long dqk_sb, long dqk_sh, long dqk_sr, float* dwq_part,
-                                   float* dwk_part, void* dv, long dv_sb, long dv_sh, long dv_sr,
+                                   float* dwk_part, long dw_ld, void* dv, long dv_sb, long dv_sh, long dv_sr,
                                    int B, int H, int n, int nk, int n_dense, float scale, void* stream) {
   int rc = check_common(B, H, n, nk);
   if (rc) return rc;
@@ -992,7 +1052,8 @@ extern "C" int vpt_attn_bwd_qknorm(const void* q, long q_sb, long q_sh, long q_s
   g.xk = {(const bf16_t*)xk, x_sb, x_sh, x_sr};
   g.wq = (const bf16_t*)wq; g.wk = (const bf16_t*)wk;
   g.rcos = cos_t; g.rsin = sin_t; g.eps = eps;
-  g.dwq = dwq_part; g.dwk = dwk_part;
+  VPT_CHECK_ARG(dw_ld >= 64, "vpt_attn_bwd_qknorm: dw_ld >= 64");
+  g.dwq = dwq_part; g.dwk = dwk_part; g.dw_ld = dw_ld;
   return attn_bwd_impl(g, B, H, n, nk, (hipStream_t)stream);
 }
 

@@ -253,18 +253,21 @@ __global__ __launch_bounds__(256) void qknorm_rope_bwd_kernel(const bf16_t* __re
 
 // Sum rows of a [R][C] f32 matrix: out[c] (=|+=) sum_r in[r][c]. Block = 64 columns (16 lanes x
 // float4, 256 B per row segment) x 16 row groups; fixed summation order (deterministic).
-__global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ in, int R, int C,
-                                                          float* __restrict__ out, int accumulate) {
-  __shared__ floatx4 red[16][16];
+// One block per 64 columns; RG row groups of 16 threads each stride over the rows (fixed assignment and order:
+// deterministic). RG = 64 (1024 threads) for tall partial sets (thousands of rows: more loads in flight per column).
+template <int RG>
+__global__ __launch_bounds__(16 * RG) void reduce_rows_kernel(const float* __restrict__ in, int R, int C,
+                                                              float* __restrict__ out, int accumulate) {
+  __shared__ floatx4 red[RG][16];
   const int cl = threadIdx.x & 15, rg = threadIdx.x >> 4;
   const int c = blockIdx.x * 64 + cl * 4;
   floatx4 s = {0.f, 0.f, 0.f, 0.f};
   if (c < C) {
     if (C % 4 == 0) {
 #pragma unroll 8
-      for (int r = rg; r < R; r += 16) s += *reinterpret_cast<const floatx4*>(in + (long)r * C + c);
+      for (int r = rg; r < R; r += RG) s += *reinterpret_cast<const floatx4*>(in + (long)r * C + c);
     } else {
-      for (int r = rg; r < R; r += 16)
+      for (int r = rg; r < R; r += RG)
         for (int e = 0; e < 4; ++e)
           if (c + e < C) s[e] += in[(long)r * C + c + e];
     }
@@ -273,7 +276,7 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
   __syncthreads();
   if (rg == 0 && c < C) {
     floatx4 t = red[0][cl];
-    for (int g = 1; g < 16; ++g) t += red[g][cl];
+    for (int g = 1; g < RG; ++g) t += red[g][cl];
     for (int e = 0; e < 4 && c + e < C; ++e) out[c + e] = accumulate ? out[c + e] + t[e] : t[e];
   }
 }
@@ -339,8 +342,12 @@ extern "C" int vpt_qknorm_rope_bwd(const void* dqk, long lddqk, const void* qkv,
 
 extern "C" int vpt_reduce_rows(const float* in, int R, int C, float* out, int accumulate, void* stream) {
   VPT_CHECK_ARG(in && out && R > 0 && C > 0, "vpt_reduce_rows: bad args");
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3((C + 63) / 64), dim3(256), 0, (hipStream_t)stream, in, R, C, out,
-                     accumulate);
+  if (R >= 1024)
+    hipLaunchKernelGGL(reduce_rows_kernel<64>, dim3((C + 63) / 64), dim3(1024), 0, (hipStream_t)stream, in, R, C, out,
+                       accumulate);
+  else
+    hipLaunchKernelGGL(reduce_rows_kernel<16>, dim3((C + 63) / 64), dim3(256), 0, (hipStream_t)stream, in, R, C, out,
+                       accumulate);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

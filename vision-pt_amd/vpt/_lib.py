@@ -35,8 +35,9 @@ SIGNATURES: dict[str, list] = {
     "vpt_attn_bwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, P, L, L, P, L,
                      P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, I, F, P],
     "vpt_attn_bwd_qknorm": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, P, L, L, P, L,
-                            P, P, L, L, L, P, P, P, P, F, P, P, L, L, L, P, P, P, L, L, L, I, I, I, I, I, F, P],
+                            P, P, L, L, L, P, P, P, P, F, P, P, L, L, L, P, P, L, P, L, L, L, I, I, I, I, I, F, P],
     "vpt_attn_bwd_dw_rows": [I, I, I],
+    "vpt_attn_fwd_qknorm": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, P, L, P, P, I, I, I, I, I, F, P],
     "vpt_linear_qknorm_rope": [P, L, P, L, P, P, L, P, L, I, I, I, P, P, P, P, I, F, F, P],
     "vpt_attn_q_scale": [F],
     "vpt_rmsnorm_fwd": [P, L, P, P, L, P, I, I, F, P],

@@ -31,6 +31,15 @@ from .rope import RopeCache
 BF16, F32 = torch.bfloat16, torch.float32
 NEG_INF = float("-inf")
 
+# Module attributes (no environment switches; tools/c3_knob_ab.py assigns them in-process for same-box A/B runs),
+# defaults = the measured faster form:
+# QK-RMSNorm + RoPE forward inside the q|k|v GEMM's epilogue (vpt_linear_qknorm_rope) vs its own pass after it
+FUSED_QKNORM_FWD = True
+# QK-RMSNorm + RoPE backward inside the attention backward's dQ / dK stores (vpt_attn_bwd_qknorm) vs its own pass
+FUSED_QKNORM_BWD = True
+# attention forward with the QK-norm score bound as a fixed softmax reference point (vpt_attn_fwd_qknorm)
+FIXREF_ATTN_FWD = True
+
 
 class _Pool:
     """Named, growable device buffers (views into cached storages)."""
@@ -215,14 +224,23 @@ class JiTEngine:
         M = x.shape[0]
         n_i = rows if (n_ctx and self._ctx_present(i)) else n_pre
         xn1, rstd1 = ops.rmsnorm_fwd(x, w["pn1"], pool.get(tag + "xn1", (M, D)), pool.get(tag + "rstd1", (M,), F32))
-        # q|k|v projection with the per-head QK-RMSNorm + RoPE (q pre-scaled for the attention kernels) in its epilogue
-        qkv, qk = ops.linear_qknorm_rope(xn1, w["pwqkv"], w["pbqkv"], pool.get(tag + "qkv", (M, 3 * D)),
-                                         pool.get(tag + "qk", (M, 2 * D)), w["pqk_norm"][:64], w["pqk_norm"][64:],
-                                         cos_t, sin_t, rows, q_scale=ops.attn_q_scale(1.0 / math.sqrt(cfg.head_dim)))
+        qs = ops.attn_q_scale(1.0 / math.sqrt(cfg.head_dim))  # q leaves pre-scaled for the attention kernels
+        qkv_buf, qk_buf = pool.get(tag + "qkv", (M, 3 * D)), pool.get(tag + "qk", (M, 2 * D))
+        wq, wk = w["pqk_norm"][:64], w["pqk_norm"][64:]
+        if FUSED_QKNORM_FWD:  # q|k|v projection with the per-head QK-RMSNorm + RoPE in its epilogue
+            qkv, qk = ops.linear_qknorm_rope(xn1, w["pwqkv"], w["pbqkv"], qkv_buf, qk_buf, wq, wk, cos_t, sin_t, rows,
+                                             q_scale=qs)
+        else:
+            qkv = ops.linear(xn1, w["pwqkv"], w["pbqkv"], out=qkv_buf)
+            qk = ops.qknorm_rope_fwd(qkv, wq, wk, cos_t, sin_t, rows, out=qk_buf, q_scale=qs)
         o = pool.get(tag + "o", (M, D))
         lse = pool.get(tag + "lse", (B, Hh, rows), F32)
-        ops.attn_fwd(ops._t4(qk, B, rows, Hh, 0), ops._t4(qk, B, rows, Hh, D), ops._t4(qkv, B, rows, Hh, 2 * D),
-                     ops._t4(o, B, rows, Hh, 0), lse, kbias, B, Hh, rows, n_i, n_pre, 1.0 / math.sqrt(cfg.head_dim))
+        a4 = (ops._t4(qk, B, rows, Hh, 0), ops._t4(qk, B, rows, Hh, D), ops._t4(qkv, B, rows, Hh, 2 * D),
+              ops._t4(o, B, rows, Hh, 0))
+        if FIXREF_ATTN_FWD:
+            ops.attn_fwd_qknorm(*a4, lse, kbias, wq, wk, B, Hh, rows, n_i, n_pre, 1.0 / math.sqrt(cfg.head_dim))
+        else:
+            ops.attn_fwd(*a4, lse, kbias, B, Hh, rows, n_i, n_pre, 1.0 / math.sqrt(cfg.head_dim))
         xm = ops.linear(o, w["pwo"], w["pbo"], resid=x, out=pool.get(tag + "xm", (M, D)))
         xn2, rstd2 = ops.rmsnorm_fwd(xm, w["pn2"], pool.get(tag + "xn2", (M, D)), pool.get(tag + "rstd2", (M,), F32))
         x12, h = ops.linear_swiglu(xn2, w["pw12"], w["pb12"], pool.get(tag + "x12", (M, 2 * F)),
@@ -291,7 +309,7 @@ class JiTEngine:
         dqkv = pool.get("d_qkv", (M, 3 * D))
         delta = pool.get("delta", (B, Hh, rows), F32)
         n_dw = ops.attn_bwd_dw_rows(B, Hh, rows)
-        qk_dw = pool.get("qk_dw_part", (2, n_dw, 64), F32)  # q_norm | k_norm weight-gradient partials
+        qk_dw = pool.get("qk_dw_part", (n_dw, 128), F32)  # q_norm | k_norm weight-gradient partials
         pre_zeroed = False
         scale = 1.0 / math.sqrt(cfg.head_dim)
         ck = st.get("ckpt", False)
@@ -324,17 +342,25 @@ class JiTEngine:
             # attention
             wgrad(dxm, o, w["gwo"], w["gbo"])
             do = ops.linear_dgrad(dxm, w["pwo"], out=pool.get("d_o", (M, D)))
-            # attention backward with the QK-RMSNorm + RoPE backward fused into its dQ / dK stores: dqkv receives the
-            # gradients of the raw q | k | v projections directly
-            ops.attn_bwd_qknorm(ops._t4(qk, B, rows, Hh, 0), ops._t4(qk, B, rows, Hh, D),
-                                ops._t4(qkv, B, rows, Hh, 2 * D), ops._t4(o, B, rows, Hh, 0), ops._t4(do, B, rows, Hh, 0),
-                                lse, delta, st["kbias"], ops._t4(qkv, B, rows, Hh, 0), ops._t4(qkv, B, rows, Hh, D),
-                                w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, ops._t4(dqkv, B, rows, Hh, 0),
-                                ops._t4(dqkv, B, rows, Hh, D), qk_dw[0], qk_dw[1], ops._t4(dqkv, B, rows, Hh, 2 * D),
-                                B, Hh, rows, n_i, n_pre, scale)
-            n_dw_i = ops.attn_bwd_dw_rows(B, Hh, n_i)
-            ops.reduce_rows(qk_dw[0][:n_dw_i], w["gqk_norm"][:64], acc)
-            ops.reduce_rows(qk_dw[1][:n_dw_i], w["gqk_norm"][64:], acc)
+            a5 = (ops._t4(qk, B, rows, Hh, 0), ops._t4(qk, B, rows, Hh, D), ops._t4(qkv, B, rows, Hh, 2 * D),
+                  ops._t4(o, B, rows, Hh, 0), ops._t4(do, B, rows, Hh, 0), lse, delta, st["kbias"])
+            if FUSED_QKNORM_BWD:
+                # attention backward with the QK-RMSNorm + RoPE backward fused into its dQ / dK stores: dqkv receives
+                # the gradients of the raw q | k | v projections directly
+                ops.attn_bwd_qknorm(*a5, ops._t4(qkv, B, rows, Hh, 0), ops._t4(qkv, B, rows, Hh, D),
+                                    w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, ops._t4(dqkv, B, rows, Hh, 0),
+                                    ops._t4(dqkv, B, rows, Hh, D), qk_dw, ops._t4(dqkv, B, rows, Hh, 2 * D),
+                                    B, Hh, rows, n_i, n_pre, scale)
+                ops.reduce_rows(qk_dw[:ops.attn_bwd_dw_rows(B, Hh, n_i)], w["gqk_norm"], acc)
+            else:
+                dqk = pool.get("d_qk", (M, 2 * D))
+                if n_i < rows:
+                    dqk.view(B, rows, 2 * D)[:, n_i:].zero_()
+                ops.attn_bwd(*a5, ops._t4(dqk, B, rows, Hh, 0), ops._t4(dqk, B, rows, Hh, D),
+                             ops._t4(dqkv, B, rows, Hh, 2 * D), B, Hh, rows, n_i, n_pre, scale)
+                qpart = ops.qknorm_rope_bwd(dqk, qkv, w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, rows, dqkv,
+                                            dw_part=pool.get("qk_part", (ops.qknorm_rope_blocks(M), 128), F32))
+                ops.reduce_rows(qpart[:ops.qknorm_rope_blocks(M)], w["gqk_norm"], acc)
             wgrad(dqkv, xn1, w["gwqkv"], w["gbqkv"])
             dxn1 = ops.linear_dgrad(dqkv, w["pwqkv"], out=pool.get("d_b", (M, D)))
             dx_new, part = ops.rmsnorm_bwd(dxn1, x_in, rstd1, w["pn1"], dres=dxm, dx=pool.get("dx_a", (M, D)),

@@ -498,6 +498,19 @@ def attn_fwd(q, k, v, o, lse, kbias, B, H, rows, n, n_dense, scale=0.125, nk=Non
     return pr.record(4.0 * B * H * n * nk * 64, run, nbytes=B * H * (2.0 * 64 * 2 * (n + nk) + 4.0 * n))
 
 
+def attn_fwd_qknorm(q, k, v, o, lse, kbias, wq, wk, B, H, rows, n, n_dense, scale=0.125):
+    """attn_fwd for QK-RMSNormed self-attention inputs (include/vpt_hip.h vpt_attn_fwd_qknorm): a fixed softmax
+    reference point from the norm weights wq / wk [64] instead of the running row maximum."""
+    def run():
+        call("vpt_attn_fwd_qknorm", *q, *k, *v, *o, lse.data_ptr(), lse.stride(0), lse.stride(1),
+             _p(kbias), 0 if kbias is None else kbias.stride(0), wq.data_ptr(), wk.data_ptr(), B, H, n, n, n_dense,
+             scale, stream())
+    pr = PROBES.get("attn_fwd")
+    if pr is None:
+        return run()
+    return pr.record(4.0 * B * H * n * n * 64, run, nbytes=B * H * (2.0 * 64 * 2 * (2 * n) + 4.0 * n))
+
+
 def attn_bwd(q, k, v, o, do, lse, delta, kbias, dq, dk, dv, B, H, rows, n, n_dense, scale=0.125, nk=None):
     nk = n if nk is None else nk
 
@@ -516,23 +529,24 @@ def attn_bwd_dw_rows(B: int, H: int, n: int) -> int:
     return int(lib.vpt_attn_bwd_dw_rows(B, H, n))
 
 
-def attn_bwd_qknorm(q, k, v, o, do, lse, delta, kbias, xq, xk, wq, wk, cos_t, sin_t, dq, dk, dwq_part, dwk_part, dv,
+def attn_bwd_qknorm(q, k, v, o, do, lse, delta, kbias, xq, xk, wq, wk, cos_t, sin_t, dq, dk, dw_part, dv,
                     B, H, rows, n, n_dense, scale=0.125, eps=1e-6):
     """attn_bwd with the QK-RMSNorm + RoPE backward fused into the dQ / dK stores (include/vpt_hip.h
     vpt_attn_bwd_qknorm): xq / xk (raw projections) and dq / dk share their (sb, sh, sr) strides; dq / dk receive the
-    raw-projection gradients; dwq_part / dwk_part [attn_bwd_dw_rows(B, H, n), 64] f32 the norm-weight partials."""
+    raw-projection gradients; dw_part [>= attn_bwd_dw_rows(B, H, n), 128] f32 the q_norm | k_norm weight partials
+    (one reduce_rows into the 128 weight gradients)."""
     if xq[1:] != xk[1:] or dq[1:] != dk[1:]:
         raise ValueError("attn_bwd_qknorm: q / k operands must share strides")
     rows_needed = attn_bwd_dw_rows(B, H, n)
-    for t in (dwq_part, dwk_part):
-        if t.dtype != F32 or t.numel() < rows_needed * 64 or not t.is_contiguous():
-            raise ValueError(f"attn_bwd_qknorm: dw partials must be contiguous f32 [{rows_needed}, 64]")
+    if dw_part.dtype != F32 or dw_part.dim() != 2 or dw_part.shape[0] < rows_needed or dw_part.shape[1] != 128 \
+            or not dw_part.is_contiguous():
+        raise ValueError(f"attn_bwd_qknorm: dw_part must be contiguous f32 [>= {rows_needed}, 128]")
 
     def run():
         call("vpt_attn_bwd_qknorm", *q, *k, *v, *o, *do, lse.data_ptr(), delta.data_ptr(), lse.stride(0), lse.stride(1),
              _p(kbias), 0 if kbias is None else kbias.stride(0), xq[0], xk[0], *xq[1:], wq.data_ptr(), wk.data_ptr(),
-             cos_t.data_ptr(), sin_t.data_ptr(), float(eps), dq[0], dk[0], *dq[1:], dwq_part.data_ptr(),
-             dwk_part.data_ptr(), *dv, B, H, n, n, n_dense, scale, stream())
+             cos_t.data_ptr(), sin_t.data_ptr(), float(eps), dq[0], dk[0], *dq[1:], dw_part.data_ptr(),
+             dw_part.data_ptr() + 64 * 4, 128, *dv, B, H, n, n, n_dense, scale, stream())
     pr = PROBES.get("attn_bwd")
     if pr is None:
         return run()
