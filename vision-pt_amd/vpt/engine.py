@@ -33,11 +33,14 @@ NEG_INF = float("-inf")
 
 # Module attributes (no environment switches; tools/c3_knob_ab.py assigns them in-process for same-box A/B runs),
 # defaults = the measured faster form:
-# QK-RMSNorm + RoPE forward inside the q|k|v GEMM's epilogue (vpt_linear_qknorm_rope) vs its own pass after it
+# QK-RMSNorm + RoPE forward inside the q|k|v GEMM's epilogue (vpt_linear_qknorm_rope) vs its own pass after it:
+# +0.29 % per C3 step (r04e, same-box in-process A/B)
 FUSED_QKNORM_FWD = True
-# QK-RMSNorm + RoPE backward inside the attention backward's dQ / dK stores (vpt_attn_bwd_qknorm) vs its own pass
-FUSED_QKNORM_BWD = True
-# attention forward with the QK-norm score bound as a fixed softmax reference point (vpt_attn_fwd_qknorm)
+# QK-RMSNorm + RoPE backward inside the attention backward's dQ / dK stores (vpt_attn_bwd_qknorm) vs its own pass:
+# measured 0.76 % SLOWER per C3 step (r04e: the per-workgroup tail -- raw-row loads, RoPE tables, the LDS reduction of
+# the weight-gradient partials -- costs more than the standalone memory-bound pass), so off
+FUSED_QKNORM_BWD = False
+# attention forward with the QK-norm score bound as a fixed softmax reference point (vpt_attn_fwd_qknorm): +0.2 %
 FIXREF_ATTN_FWD = True
 
 
