@@ -30,7 +30,14 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     args = ap.parse_args()
     knobs = args.knobs.split(",")
+    # diagnostic-library switches (run with VPT_DIAG=1): name -> setter(on)
+    from vpt import _lib
+    diag = {"ATTN_BWD_STAGES3": lambda on: _lib.lib.vpt_attn_set_bwd_stages(3 if on else 2)}
     for k in knobs:
+        if k in diag:
+            if not _lib.DIAG:
+                raise SystemExit(f"{k}: needs the diagnostic library (VPT_DIAG=1)")
+            continue
         if not isinstance(getattr(engine, k), bool):
             raise SystemExit(f"{k}: not a boolean knob of vpt.engine")
     dev = torch.device("cuda", 0)
@@ -50,7 +57,10 @@ def main():
 
     def setk(v):
         for k in knobs:
-            setattr(engine, k, v)
+            if k in diag:
+                diag[k](v)
+            else:
+                setattr(engine, k, v)
 
     for v in (True, False):
         setk(v)

@@ -61,6 +61,7 @@ constexpr float kTau = 8.f;  // forward lazy-rescale threshold, log2 units
 int g_variant = 0;  // backward kernel variant (vpt_attn_set_variant; 1, 2 = timing-only ablations)
 int g_waves = 4;    // waves per block (vpt_attn_set_variant 3 -> 8-wave blocks, A/B only)
 float g_tau = kTau; // forward lazy-rescale threshold (vpt_attn_set_rescale_threshold)
+int g_bwd_nst = 2;  // backward LDS ring stages (vpt_attn_set_bwd_stages, A/B)
 int g_rows64 = 0;   // backward variants (vpt_attn_set_rows64 bit mask, A/B): 1 = 64-key dK/dV, 2 = 64-query dQ
                     // at 2 waves / SIMD, 4 = 64-query dQ at 1 wave / SIMD; 0 = the 32-row pair
 #else
@@ -528,9 +529,10 @@ __global__ void attn_bwd_pre_kernel(AttnArgs g, int H, long rows_total) {
 // ABL (timing-only ablations, wrong results): 1 = no next-tile staging (global -> regs -> LDS) in
 // the loop, 2 = transposed fragment reads replaced by row reads.
 // Body of one dK/dV block (key block bx of head hd, batch b); lds = [buf][Q / dO] tiles, lstat = [buf][lse / delta].
-template <int ABL, int NW>
-__device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int b, char (&lds)[2][2][8192],
-                                          float (&lstat)[2][2][64]) {
+// NST: LDS stages of the Q / dO ring (2: tile t+1 in flight during tile t; 3: tiles t+1 and t+2, counted vmcnt).
+template <int ABL, int NW, int NST = 2>
+__device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int b, char (&lds)[NST][2][8192],
+                                          float (&lstat)[NST][2][64]) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
   const int k0 = bx * (32 * NW) + wid * 32;
   const bf16_t* Q = g.q.p + b * g.q.sb + hd * g.q.sh;
@@ -568,8 +570,15 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
   };
   // After the DMA into `buf` landed for every wave: a partial last query tile gets its padding rows of
   // Q and dO zeroed, so the clamped duplicates contribute nothing to dK (dS.Q) or dV (P^T.dO).
-  auto settle = [&](int buf, int r0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // younger: a later tile's pieces were issued after this tile's (3-stage ring): wait only for this one's -- each
+  // wave issues 4 pieces per tile (Q, dO) plus the stats piece on waves 0 and 1, and vmcnt retires in order.
+  auto settle = [&](int buf, int r0, bool younger) {
+    if (NST == 3 && younger) {
+      if (wid < 2) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
     if (g.n - r0 < 64) {
       zero_rows<NW>(lds[buf][0], g.n - r0, tid);
@@ -578,12 +587,15 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
     }
   };
   stage(0, 0);
-  settle(0, 0);
+  if (NST == 3 && ABL != 1 && nt > 1) stage(1, 64);
+  settle(0, 0, NST == 3 && ABL != 1 && nt > 1);
 
-  int cur = 0;
   for (int t = 0; t < nt; ++t) {
+    const int cur = NST == 2 ? (t & 1) : t % NST;
     const bool more = ABL != 1 && t + 1 < nt;
-    if (more) stage(cur ^ 1, (t + 1) * 64);
+    if (NST == 2 && more) stage(cur ^ 1, (t + 1) * 64);
+    if (NST == 3 && ABL != 1 && t + 2 < nt) stage((t + 2) % 3, (t + 2) * 64);
+    const int nxt = NST == 2 ? (cur ^ 1) : (t + 1) % NST;
     const char* lq = lds[cur][0];
     const char* ld = lds[cur][1];
     if (ABL == 8) {
@@ -638,8 +650,7 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
           }
           __builtin_amdgcn_s_setprio(0);
         }
-      if (more) settle(cur ^ 1, (t + 1) * 64);
-      cur ^= 1;
+      if (more) settle(nxt, (t + 1) * 64, NST == 3 && t + 2 < nt);
       continue;
     }
     floatx16 P[2], dS[2];
@@ -686,8 +697,7 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
           }
         }
       }
-    if (more) settle(cur ^ 1, (t + 1) * 64);
-    if (ABL != 1) cur ^= 1;
+    if (more) settle(nxt, (t + 1) * 64, NST == 3 && t + 2 < nt);
   }
   store_T(g.dv, (long)b * g.dv.sb + hd * g.dv.sh, dvT, 1.f, key, g.nk, lane, kmasked);
   // dK = scale * dS^T.Q = (scale / c) * dS^T.Q~ with Q~ = c*Q, c = scale*log2(e): the factor is ln 2
@@ -706,8 +716,8 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
 
 // ------------------------------------------------------------------ backward dQ
 // Body of one dQ block (query block bx of head hd, batch b); lds = [buf][K / V] tiles, kbl = key bias of keys kb0..
-template <int ABL, int NW>
-__device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b, char (&lds)[2][2][8192], float* kbl,
+template <int ABL, int NW, int NST = 2>
+__device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b, char (&lds)[NST][2][8192], float* kbl,
                                         float* red2) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
   const int q0 = bx * (32 * NW) + wid * 32;
@@ -733,19 +743,31 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
   fill_key_bias<NW>(kbl, g, b, tid);
   const uint32_t lb = lds_addr(&lds[0][0][0]);  // [buf][K / V] tiles of 8 KB
   const RowPlan<NW> pk = row_plan<NW>(g.k.sr, wid, lane), pv = row_plan<NW>(g.v.sr, wid, lane);
+  // the lse / delta / q / dO register loads above retire here, visibly to hipcc's wait placement (as in dkdv_body)
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
   dma_rows_at<NW>(lb, Ku, g.k.sr, 0, g.nk, pk, wid, lane);
   dma_rows_at<NW>(lb + 8192, Vu, g.v.sr, 0, g.nk, pv, wid, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (NST == 3 && ABL != 1 && nt > 1) {  // tile 1 in flight while tile 0 is waited for (4 pieces per wave)
+    dma_rows_at<NW>(lb + 16384, Ku, g.k.sr, 64, g.nk, pk, wid, lane);
+    dma_rows_at<NW>(lb + 16384 + 8192, Vu, g.v.sr, 64, g.nk, pv, wid, lane);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
 
-  int cur = 0;
   for (int t = 0; t < nt; ++t) {
     const int kv0 = t * 64;
+    const int cur = NST == 2 ? (t & 1) : t % NST;
     const bool more = ABL != 1 && t + 1 < nt;
-    if (more) {
-      dma_rows_at<NW>(lb + (cur ^ 1) * 16384, Ku, g.k.sr, kv0 + 64, g.nk, pk, wid, lane);
-      dma_rows_at<NW>(lb + (cur ^ 1) * 16384 + 8192, Vu, g.v.sr, kv0 + 64, g.nk, pv, wid, lane);
+    const int ahead = NST == 2 ? 1 : 2;  // the tile this iteration DMAs
+    if (ABL != 1 && t + ahead < nt) {
+      const int nb = (t + ahead) % NST;
+      dma_rows_at<NW>(lb + nb * 16384, Ku, g.k.sr, kv0 + 64 * ahead, g.nk, pk, wid, lane);
+      dma_rows_at<NW>(lb + nb * 16384 + 8192, Vu, g.v.sr, kv0 + 64 * ahead, g.nk, pv, wid, lane);
     }
+    // at the end of this tile: wait for tile t + 1 with tile t + 2 (if any) still in flight (3-stage ring)
+    const bool younger = NST == 3 && ABL != 1 && t + 2 < nt;
     const char* lk = lds[cur][0];
     const char* lv = lds[cur][1];
     const bool dense = kv0 + 64 <= g.n_dense;
@@ -805,9 +827,9 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
           __builtin_amdgcn_s_setprio(0);
         }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (younger) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      cur ^= 1;
       continue;
     }
     floatx16 dS[2];
@@ -840,9 +862,10 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
           dqT[db] = mfma32(ABL == 2 ? frag_rows(lk, 32 * db, 2 * kb + s2, lane) : frag_tr(lk, db, 2 * kb + s2, lane), pd,
                            dqT[db]);
       }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (younger) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (ABL != 1) cur ^= 1;
+    (void)more;
   }
   if (!g.qkn) {
     store_T(g.dq, (long)b * g.dq.sb + hd * g.dq.sh, dqT, g.scale, qrow, g.n, lane, false);
@@ -863,10 +886,10 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
 // so the pair runs in ~(work of both) / slots instead of two rounded-up launches.
 // DKDV: the dK/dV body (8 = explicitly ordered, 0 = compiler-scheduled). ORDER 1 (diagnostic A/B): per (batch,
 // head) its nkb dK/dV blocks then its nqb dQ blocks, heads in sequence (a head's Q / dO / K / V shared in time).
-template <int DQ, int DKDV = 8, int ORDER = 0>
+template <int DQ, int DKDV = 8, int ORDER = 0, int NST = 2>
 __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs g, int nkb, int nqb, int B) {
-  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];
-  __shared__ __attribute__((aligned(16))) float lstat[2][2][64];
+  __shared__ __attribute__((aligned(16))) char lds[NST][2][8192];
+  __shared__ __attribute__((aligned(16))) float lstat[NST][2][64];
   extern __shared__ __attribute__((aligned(16))) float kbl[];
   int bid = blockIdx.x;
   bool kv;
@@ -883,8 +906,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs g, int nkb, i
     bx = kv ? bid % nkb : bid % nqb;
     r = kv ? bid / nkb : bid / nqb;
   }
-  if (kv) dkdv_body<DKDV, 4>(g, bx, r % g.H, r / g.H, lds, lstat);
-  else dq_body<DQ, 4>(g, bx, r % g.H, r / g.H, lds, kbl, &lstat[0][0][0]);
+  if (kv) dkdv_body<DKDV, 4, NST>(g, bx, r % g.H, r / g.H, lds, lstat);
+  else dq_body<DQ, 4, NST>(g, bx, r % g.H, r / g.H, lds, kbl, &lstat[0][0][0]);
 }
 constexpr int kDqBody = 0;  // production dQ body (0 = compiler-scheduled, 8 = explicitly ordered)
 
@@ -1096,6 +1119,14 @@ int attn_bwd_impl(AttnArgs& g, int B, int H, int n, int nk, hipStream_t s) {
   if (g_rows64 & 16) {  // A/B: the other dQ body in the one-launch kernel
     hipLaunchKernelGGL((attn_bwd_kernel<8 - kDqBody>), dim3((nkb + nqb) * H * B), dim3(256), key_bias_lds_bytes(g), s, g,
                        nkb, nqb, B);
+    VPT_LAUNCH_CHECK();
+    return VPT_OK;
+  }
+#endif
+#ifdef VPT_DIAG
+  if (g_bwd_nst == 3) {
+    hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, 8, 0, 3>), dim3((nkb + nqb) * H * B), dim3(256), key_bias_lds_bytes(g),
+                       s, g, nkb, nqb, B);
     VPT_LAUNCH_CHECK();
     return VPT_OK;
   }

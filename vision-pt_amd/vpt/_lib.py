@@ -125,6 +125,7 @@ DIAG_SIGNATURES: dict[str, list] = {
     "vpt_attn_fused_workspace_bytes": [I, I, I],
     "vpt_attn_set_fused_workspace": [P],
     "vpt_attn_set_rows64": [I],
+    "vpt_attn_set_bwd_stages": [I],
     "vpt_gemm_set_nf4_ablation": [I],
 }
 _RESTYPES = {
