@@ -639,9 +639,12 @@ __device__ __forceinline__ EpiAddr epi_addr(const GemmArgs& g, const RingItem& i
 // Epilogue modes (a template parameter of the ring kernel, so that each mode gets its own register
 // allocation): 0 = no loads (bf16 / f32 out, bias, SiLU), 1 = residual, 2 = fused SwiGLU backward (x12),
 // 3 = f32 accumulate into C.
-enum { EPI_PLAIN = 0, EPI_RESID = 1, EPI_SWB = 2, EPI_ACC = 3, EPI_QKN = 4 };
+// EPI_SWB1: the SwiGLU-backward epilogue with its x12 operands loaded one group at a time (the form before the
+// one-group-ahead preload; diagnostic build only, A/B)
+enum { EPI_PLAIN = 0, EPI_RESID = 1, EPI_SWB = 2, EPI_ACC = 3, EPI_QKN = 4, EPI_SWB1 = 5 };
+__host__ __device__ constexpr bool epi_swb(int e) { return e == EPI_SWB || e == EPI_SWB1; }
 __host__ __device__ constexpr int epi_frags(int epi) {  // fragments per preload group (0: no loads)
-  return epi == EPI_RESID ? 4 : (epi == EPI_SWB || epi == EPI_ACC) ? 2 : 0;
+  return epi == EPI_RESID ? 4 : (epi_swb(epi) || epi == EPI_ACC) ? 2 : 0;
 }
 __host__ __device__ inline int epi_mode(const GemmArgs& g) {
   return g.sw == 2 ? EPI_SWB : g.out_mode == OUT_F32_ACC ? EPI_ACC : g.resid ? EPI_RESID : g.qk_d > 0 ? EPI_QKN : EPI_PLAIN;
@@ -651,7 +654,7 @@ struct EpiPre {
 };
 template <int EPI, int I0>
 __device__ __forceinline__ void epi_preload(const GemmArgs& g, const EpiAddr& e, EpiPre& pre) {
-  if (EPI == EPI_SWB) {
+  if (epi_swb(EPI)) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -735,7 +738,7 @@ __device__ __forceinline__ void epilogue_ring(const GemmArgs& g, const floatx4 (
         for (int q = 0; q < 8; ++q) o[q] = o[q] / (1.f + __expf(-o[q]));
       }
       const int soff = (i * 16 + p * 8) * e.rstride;
-      if (EPI == EPI_SWB) {
+      if (epi_swb(EPI)) {
         // fused SwiGLU backward (the reference's SwiGLU autograd, denoiser.py:480-506, as swiglu_bwd_kernel):
         // o = dh; x1, x2 from x12; dx1 -> column c, dx2 -> column F + c of dx12 (F = N)
         const u32x4 a4 = pre.v[4 * il + 2 * p], b4 = pre.v[4 * il + 2 * p + 1];
@@ -1086,11 +1089,17 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
     const int next = item + gridDim.x;
     constexpr int GF = SW ? 0 : epi_frags(EPI);
     EpiAddr ea;
-    EpiPre pre;
+    EpiPre pre, pre2;
     if (!SW) {
       ea = epi_addr(g, it, wm, wn, lane);
       if (ABL == 4) ea.rs = __builtin_amdgcn_make_buffer_rsrc(g.C, (short)0, 0, 0x00020000);  // stores dropped
-      if (GF) {
+      if (EPI == EPI_SWB) {
+        // two groups in flight (the K loop's fragment registers are free now): group 0 waited for here, group 1
+        // lands under group 0's epilogue, and each later group is loaded one group ahead of its use
+        epi_preload<EPI, 0>(g, ea, pre);
+        epi_preload<EPI, 2>(g, ea, pre2);
+        __builtin_amdgcn_s_waitcnt(0x0f78);  // vmcnt(8): the first group landed; the second may be in flight
+      } else if (GF) {
         epi_preload<EPI, 0>(g, ea, pre);
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the first group landed (nothing else in flight)
       }
@@ -1115,6 +1124,13 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
       epilogue_ring_swf(g, acc, stg, lane, it, wm, wn, bias8, bias8b);
     } else if (EPI == EPI_QKN) {
       epilogue_ring_qkn(g, acc, stg, lane, ea, bias8, it, wm, wn);
+    } else if (EPI == EPI_SWB) {
+      epilogue_ring<EPI, 0, 2>(g, acc, stg, lane, ea, bias8, pre);
+      epi_preload<EPI, 4>(g, ea, pre);
+      epilogue_ring<EPI, 2, 4>(g, acc, stg, lane, ea, bias8, pre2);
+      epi_preload<EPI, 6>(g, ea, pre2);
+      epilogue_ring<EPI, 4, 6>(g, acc, stg, lane, ea, bias8, pre);
+      epilogue_ring<EPI, 6, 8>(g, acc, stg, lane, ea, bias8, pre2);
     } else if (GF == 2) {
       epilogue_ring<EPI, 0, 2>(g, acc, stg, lane, ea, bias8, pre);
       epi_preload<EPI, 2>(g, ea, pre);
@@ -1164,6 +1180,7 @@ int launch(const GemmArgs& g, int splits, hipStream_t s) {
 // production.
 #ifdef VPT_DIAG
 int g_stagger_override = 0;  // vpt_gemm_set_stagger
+int g_swb_one_group = 0;     // vpt_gemm_set_swb_one_group (A/B: the SwiGLU-backward epilogue's older preload form)
 #endif
 inline int ring_stagger() {
 #ifdef VPT_DIAG
@@ -1193,6 +1210,11 @@ int launch_ring(const GemmArgs& g, int splits, hipStream_t s) {
   } else if (epi == EPI_RESID)
     hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, SW, SW ? 0 : EPI_RESID>), dim3(grid), dim3(512),
                        LDS, s, gl);
+#ifdef VPT_DIAG
+  else if (epi == EPI_SWB && g_swb_one_group)
+    hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, SW, SW ? 0 : EPI_SWB1>), dim3(grid), dim3(512),
+                       LDS, s, gl);
+#endif
   else if (epi == EPI_SWB)
     hipLaunchKernelGGL((gemm_ring_kernel<AK, BK_, PP, ABL, DMAC, STAMP, TL, SW, SW ? 0 : EPI_SWB>), dim3(grid), dim3(512),
                        LDS, s, gl);
@@ -1541,6 +1563,11 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
 
 #ifdef VPT_DIAG
 // ---- diagnostic build only (libvpt_hip_diag.so, include/vpt_hip_diag.h): process-wide switches ----
+extern "C" int vpt_gemm_set_swb_one_group(int on) {
+  g_swb_one_group = on;
+  return VPT_OK;
+}
+
 extern "C" int vpt_gemm_set_geometry(int geo) {
   VPT_CHECK_ARG(geo == 0 || geo == 128 || geo == 256 || (geo >= 2561 && geo <= 2573) || geo == 1601 || geo == 1602,
                 "vpt_gemm_set_geometry: 0, 128, 256 or 2561-2573");
