@@ -221,7 +221,8 @@ int vpt_flow_loss(const void* pred, const void* img, const void* noise, const fl
  *   src/modules/timestep/embedding.py:10-62.
  * assemble/disassemble/ctx_rows: token concatenation and per-block context append/strip,
  *   src/models/jit/denoiser.py:982-993,1078-1113 (+ their backward).
- * copy_rows: patch-token slice tokens[:, :N_p] (denoiser.py:1115).
+ * copy_rows: patch-token slice tokens[:, :N_p] (denoiser.py:1115). reverse 0: seq -> dense; 1: dense -> seq;
+ *   2: dense -> seq and every other row of each sequence zeroed (the slice's backward into a fresh buffer).
  * embed_gather/scatter_add: nn.Embedding(padding_idx) of ClassEncoder, class_encoder.py:107-144. */
 int vpt_timestep_embed(const float* vals, int R, void* out, void* stream);
 int vpt_assemble_tokens(const void* patches, const void* size_emb, const void* time_emb, const void* tpe,

@@ -30,6 +30,40 @@ def rnd(*shape, scale=1.0, dtype=torch.bfloat16, seed=0):
     return (torch.randn(*shape, generator=g) * scale).to(dtype).to(DEV)
 
 
+# ------------------------------------------------------------------------------------ row sums / row copies
+@pytest.mark.parametrize("R,C", [(1, 8), (7, 130), (255, 768), (256, 768), (512, 768), (1024, 128), (3168, 128),
+                                 (300, 66)])
+def test_reduce_rows(ops, R, C):
+    """out (=|+=) the column sums of an f32 [R, C] partial set: within f32 summation error of a float64 sum,
+    and bitwise reproducible (fixed summation order)."""
+    part = rnd(R, C, dtype=torch.float32, seed=R + C)
+    out = torch.empty(C, device=DEV)
+    ops.reduce_rows(part, out)
+    ref = part.double().sum(0)
+    assert (out.double() - ref).abs().max().item() < 1e-5 * (part.abs().sum(0).max().item() + 1)
+    again = torch.empty(C, device=DEV)
+    ops.reduce_rows(part, again)
+    assert torch.equal(out, again)
+    base = rnd(C, dtype=torch.float32, seed=5)
+    acc = base.clone()
+    ops.reduce_rows(part, acc, accumulate=True)
+    assert (acc.double() - (base.double() + ref)).abs().max().item() < 1e-5 * (part.abs().sum(0).max().item() + 2)
+
+
+@pytest.mark.parametrize("B,rows,row0,cnt,D", [(2, 300, 0, 256, 64), (3, 97, 5, 80, 136), (1, 16, 0, 16, 8)])
+def test_copy_rows_scatter_zero_rest(ops, B, rows, row0, cnt, D):
+    """copy_rows reverse with zero_rest: the slice's rows from dense, every other row zero (no prior fill)."""
+    dense = rnd(B * cnt, D, seed=11)
+    seq = torch.full((B * rows, D), float("nan"), dtype=torch.bfloat16, device=DEV)
+    ops.copy_rows(seq, rows, row0, cnt, dense, B, reverse=True, zero_rest=True)
+    ref = torch.zeros(B, rows, D, dtype=torch.bfloat16, device=DEV)
+    ref[:, row0:row0 + cnt] = dense.view(B, cnt, D)
+    assert torch.equal(seq.view(B, rows, D), ref)
+    back = torch.empty_like(dense)
+    ops.copy_rows(seq, rows, row0, cnt, back, B)
+    assert torch.equal(back, dense)
+
+
 # ------------------------------------------------------------------------------------ GEMM
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 136, 200), (1000, 768, 768), (64, 2304, 768)])
 def test_gemm_forward(ops, M, N, K):

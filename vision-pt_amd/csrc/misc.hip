@@ -577,12 +577,17 @@ __global__ void copy_rows_kernel(bf16_t* __restrict__ seq, long ld_seq, int rows
                                  bf16_t* __restrict__ dense, long ld_dense, int B, int D, int reverse) {
   const int nch = D >> 3;
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (long)B * cnt * nch) return;
+  const int span = reverse == 2 ? rows : cnt;  // mode 2 walks every sequence row: the others are zeroed
+  if (gid >= (long)B * span * nch) return;
   const int ch = gid % nch;
   const long r = gid / nch;
-  const int b = r / cnt, j = r % cnt;
-  bf16_t* s = seq + ((long)b * rows + row0 + j) * ld_seq + ch * 8;
-  bf16_t* d = dense + r * ld_dense + ch * 8;
+  const int b = r / span, jr = r % span, j = reverse == 2 ? jr - row0 : jr;
+  bf16_t* s = seq + ((long)b * rows + (reverse == 2 ? jr : row0 + j)) * ld_seq + ch * 8;
+  if (reverse == 2 && (j < 0 || j >= cnt)) {
+    *reinterpret_cast<uint4*>(s) = make_uint4(0, 0, 0, 0);
+    return;
+  }
+  bf16_t* d = dense + ((long)b * cnt + j) * ld_dense + ch * 8;
   if (reverse) *reinterpret_cast<uint4*>(s) = *reinterpret_cast<const uint4*>(d);
   else *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
 }
@@ -615,8 +620,10 @@ inline dim3 grid1(long n, int threads = 256) { return dim3((unsigned)((n + threa
 
 extern "C" int vpt_copy_rows(void* seq, long ld_seq, int rows, int row0, int cnt, void* dense, long ld_dense, int B,
                              int D, int reverse, void* stream) {
-  VPT_CHECK_ARG(seq && dense && D % 8 == 0 && row0 + cnt <= rows, "vpt_copy_rows: bad args");
-  hipLaunchKernelGGL(copy_rows_kernel, grid1((long)B * cnt * (D / 8)), dim3(256), 0, (hipStream_t)stream,
+  VPT_CHECK_ARG(seq && dense && D % 8 == 0 && row0 >= 0 && row0 + cnt <= rows && reverse >= 0 && reverse <= 2,
+                "vpt_copy_rows: bad args");
+  hipLaunchKernelGGL(copy_rows_kernel, grid1((long)B * (reverse == 2 ? rows : cnt) * (D / 8)), dim3(256), 0,
+                     (hipStream_t)stream,
                      (bf16_t*)seq, ld_seq, rows, row0, cnt, (bf16_t*)dense, ld_dense, B, D, reverse);
   VPT_LAUNCH_CHECK();
   return VPT_OK;

@@ -251,20 +251,20 @@ __global__ __launch_bounds__(256) void qknorm_rope_bwd_kernel(const bf16_t* __re
   }
 }
 
-// Sum rows of a [R][C] f32 matrix: out[c] (=|+=) sum_r in[r][c]. Block = 64 columns (16 lanes x
-// float4, 256 B per row segment) x 16 row groups; fixed summation order (deterministic).
-// One block per 64 columns; RG row groups of 16 threads each stride over the rows (fixed assignment and order:
-// deterministic). RG = 64 (1024 threads) for tall partial sets (thousands of rows: more loads in flight per column).
+// Sum rows of a [R][C] f32 matrix: out[c] (=|+=) sum_r in[r][c]. Block = 16 columns (4 lanes x float4, 64 B per row
+// segment) x RG row groups; each row group strides over the rows in a fixed order, then a fixed pairwise tree over the
+// row groups (deterministic, no atomics). The partial sets are short and wide (512 x 768 for an RMSNorm weight, 256 x N
+// for a bias): 16-column blocks give C/16 workgroups and RG = 256 leaves each lane 2-4 rows, all loads in flight at once.
 template <int RG>
-__global__ __launch_bounds__(16 * RG) void reduce_rows_kernel(const float* __restrict__ in, int R, int C,
-                                                              float* __restrict__ out, int accumulate) {
-  __shared__ floatx4 red[RG][16];
-  const int cl = threadIdx.x & 15, rg = threadIdx.x >> 4;
-  const int c = blockIdx.x * 64 + cl * 4;
+__global__ __launch_bounds__(4 * RG) void reduce_rows_kernel(const float* __restrict__ in, int R, int C,
+                                                             float* __restrict__ out, int accumulate) {
+  __shared__ floatx4 red[RG][4];
+  const int cl = threadIdx.x & 3, rg = threadIdx.x >> 2;
+  const int c = blockIdx.x * 16 + cl * 4;
   floatx4 s = {0.f, 0.f, 0.f, 0.f};
   if (c < C) {
     if (C % 4 == 0) {
-#pragma unroll 8
+#pragma unroll 4
       for (int r = rg; r < R; r += RG) s += *reinterpret_cast<const floatx4*>(in + (long)r * C + c);
     } else {
       for (int r = rg; r < R; r += RG)
@@ -274,9 +274,13 @@ __global__ __launch_bounds__(16 * RG) void reduce_rows_kernel(const float* __res
   }
   red[rg][cl] = s;
   __syncthreads();
+#pragma unroll
+  for (int st = RG / 2; st >= 1; st >>= 1) {
+    if (rg < st) red[rg][cl] += red[rg + st][cl];
+    __syncthreads();
+  }
   if (rg == 0 && c < C) {
-    floatx4 t = red[0][cl];
-    for (int g = 1; g < RG; ++g) t += red[g][cl];
+    const floatx4 t = red[0][cl];
     for (int e = 0; e < 4 && c + e < C; ++e) out[c + e] = accumulate ? out[c + e] + t[e] : t[e];
   }
 }
@@ -342,11 +346,11 @@ extern "C" int vpt_qknorm_rope_bwd(const void* dqk, long lddqk, const void* qkv,
 
 extern "C" int vpt_reduce_rows(const float* in, int R, int C, float* out, int accumulate, void* stream) {
   VPT_CHECK_ARG(in && out && R > 0 && C > 0, "vpt_reduce_rows: bad args");
-  if (R >= 1024)
-    hipLaunchKernelGGL(reduce_rows_kernel<64>, dim3((C + 63) / 64), dim3(1024), 0, (hipStream_t)stream, in, R, C, out,
+  if (R >= 256)
+    hipLaunchKernelGGL(reduce_rows_kernel<256>, dim3((C + 15) / 16), dim3(1024), 0, (hipStream_t)stream, in, R, C, out,
                        accumulate);
   else
-    hipLaunchKernelGGL(reduce_rows_kernel<16>, dim3((C + 63) / 64), dim3(256), 0, (hipStream_t)stream, in, R, C, out,
+    hipLaunchKernelGGL(reduce_rows_kernel<64>, dim3((C + 15) / 16), dim3(256), 0, (hipStream_t)stream, in, R, C, out,
                        accumulate);
   VPT_LAUNCH_CHECK();
   return VPT_OK;

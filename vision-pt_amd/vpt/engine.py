@@ -274,7 +274,10 @@ class JiTEngine:
         M2 = B * np_
         cos_t, sin_t = st["cos"], st["sin"]
         if zero_grads:
-            self.grads.zero_()
+            # every gradient slice below is written with overwrite semantics when acc is False; only the slices this
+            # backward does not write (the class-embedding table the trainer scatter-adds into, the context embedder
+            # of a context-free batch) are zeroed, instead of a fill over the whole flat buffer
+            self._zero_unwritten_grads(n_ctx)
         acc = not zero_grads
         ws = pool.get("wgrad_ws", (self._ws_elems(max(M, M2)),), F32)
         f, g = self.fin, self.g
@@ -305,8 +308,8 @@ class JiTEngine:
         ops.reduce_rows(part[:ops.rmsnorm_bwd_blocks(M2)], f["gn"], acc)
         if on_ready is not None:
             on_ready("final")  # every final_layer.* gradient is enqueued
-        dx = pool.get("dx_a", (M, D), zero=True)
-        ops.copy_rows(dx, rows, 0, np_, dxf, B, reverse=True)
+        dx = pool.get("dx_a", (M, D))
+        ops.copy_rows(dx, rows, 0, np_, dxf, B, reverse=True, zero_rest=True)  # token / context rows: zero
         # --- blocks in reverse
         dctx = pool.get("dctx", (max(B * n_ctx, 1), D), F32, zero=True)
         dqkv = pool.get("d_qkv", (M, 3 * D))
@@ -331,7 +334,9 @@ class JiTEngine:
             lse = pool.get(tag + "lse", (B, Hh, rows), F32)
             n_i = rows if (n_ctx and self._ctx_present(i)) else n_pre
             if n_i < rows and not pre_zeroed:
-                dqkv.zero_()  # the context rows take no gradient in the blocks before context_start_block
+                # the context rows take no gradient in the blocks before context_start_block (q | k rows come from
+                # dqk, zeroed below; v rows are never written there)
+                dqkv.view(B, rows, 3 * D)[:, n_i:].zero_()
                 pre_zeroed = True
             # MLP
             wgrad(dx, h, w["gw3"], w["gb3"])
@@ -401,6 +406,14 @@ class JiTEngine:
             dctx_raw = ops.linear_dgrad(dctx_b, self.p["context_embedder.weight"],
                                         out=pool.get("d_ctx_raw", (B * n_ctx, cfg.context_dim)))
         return dctx_raw
+
+    def _zero_unwritten_grads(self, n_ctx: int):
+        names = ["class_encoder.embedding.weight"]
+        if not n_ctx:
+            names += ["context_embedder.weight", "context_embedder.bias"]
+        for n in names:
+            if n in self.g:
+                self.g[n].zero_()
 
     def _tpe_grad_target(self, acc: bool):
         if acc:

@@ -646,11 +646,14 @@ def embed_scatter_add(drows, ids, pad_id, dtable):
          stream())
 
 
-def copy_rows(seq, rows, row0, cnt, dense, B, reverse=False):
-    """dense[B*cnt, D] <-> seq[B*rows, D] rows [row0, row0+cnt) of every sequence."""
+def copy_rows(seq, rows, row0, cnt, dense, B, reverse=False, zero_rest=False):
+    """dense[B*cnt, D] <-> seq[B*rows, D] rows [row0, row0+cnt) of every sequence; zero_rest (with reverse) also
+    zeroes every other row of seq (one pass instead of a fill before the scatter)."""
     D = dense.shape[1]
+    if zero_rest and not reverse:
+        raise ValueError("copy_rows: zero_rest needs reverse=True")
     call("vpt_copy_rows", seq.data_ptr(), seq.stride(0), rows, row0, cnt, dense.data_ptr(), dense.stride(0), B, D,
-         int(reverse), stream())
+         2 if zero_rest else int(reverse), stream())
     return dense
 
 
