@@ -391,6 +391,10 @@ def bench_c5(args):
     n, ms, fl = probes[dom].summary()
     tf = fl / (ms * 1e-3) / 1e12 if ms else 0.0
     traffic, tsrc = measured_traffic(dom, "c5")
+    if traffic is None:
+        # the FETCH_SIZE pass of this command completes, but its WRITE_SIZE pass stalls under rocprofv3 right after
+        # HSA init, reproducibly (profiles/r04/r04k_c5_write_size_stall.log), so no read+write figure exists
+        tsrc = "unmeasured: rocprofv3 --pmc WRITE_SIZE stalls on the C5 command (profiles/r04/r04k_c5_write_size_stall.log)"
     step_tf = sum(m.flops_per_step((H // 8, W // 8)) for (W, H) in SDXL_BUCKETS_5) / nb / 1e12
     res = {
         "metric": "train images/sec, SDXL QLoRA r=16 flow-matching step (1024^2 bucketed, 5 buckets), 1 MI355X",

@@ -1,7 +1,7 @@
 """Per-launch HBM traffic of the bench's probed ops from two rocprofv3 counter passes
 (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950: MI355X_MICROARCH.md §rocprofv3 PMC slots).
 
-  python tools/pmc_traffic.py FETCH_DIR WRITE_DIR KTRACE_DIR OUT.json
+  python tools/pmc_traffic.py FETCH_DIR WRITE_DIR KTRACE_DIR OUT.json [MFMA_DIR] [--tag TAG]
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch. gfx950 correction (MI355X_MICROARCH.md §HBM):
 FETCH_SIZE reports exactly half of the bytes of a wide coalesced streaming read (16 B per lane,
@@ -67,8 +67,14 @@ def _counters(dirname, names):
 
 
 def main():
-    fdir, wdir, kdir, out = sys.argv[1:5]
-    mdir = sys.argv[5] if len(sys.argv) > 5 else None
+    args = sys.argv[1:]
+    tag = None
+    if "--tag" in args:
+        i = args.index("--tag")
+        tag = args[i + 1]
+        del args[i:i + 2]
+    fdir, wdir, kdir, out = args[:4]
+    mdir = args[4] if len(args) > 4 else None
     fetch, nf = _counter(fdir, "FETCH_SIZE")
     write, nw = _counter(wdir, "WRITE_SIZE")
     stats = glob.glob(f"{kdir}/**/*kernel_stats.csv", recursive=True)[0]
@@ -95,6 +101,8 @@ def main():
             "rocprof_mean_ms_per_launch": round(dur[op] / calls[op] / 1e6, 4) if calls[op] else None,
             "rocprof_launches": calls[op],
         }
+    if tag:
+        res["_tag"] = tag
     res["_method"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of the same "
                       "command; read bytes = 2 x FETCH_SIZE x 1024 (gfx950 half-count of 16-B/lane reads), "
                       "write bytes = WRITE_SIZE x 1024; per launch of the op")
