@@ -1,7 +1,9 @@
-"""The attention backward with a 3-stage LDS ring (diagnostic switch vpt_attn_set_bwd_stages) against the production
-2-stage ring at the C3 shape: bitwise equality of dq / dk / dv, then interleaved HIP-event timing (medians).
+"""A diagnostic variant of the attention backward against the production kernel at the C3 shape: bitwise equality of
+dq / dk / dv, then interleaved HIP-event timing (medians).
+  --knob stages --value 3: 3-stage LDS rings (vpt_attn_set_bwd_stages)
+  --knob pipe --value M:   software-pipelined block bodies, bit mask M (vpt_attn_set_bwd_pipe)
 
-  VPT_DIAG=1 python tools/attn_stage_check.py [--rounds 6]
+  VPT_DIAG=1 python tools/attn_bwd_variant_check.py --knob pipe --value 1 [--rounds 6]
 """
 import os
 os.environ.setdefault("VPT_DIAG", "1")
@@ -20,7 +22,12 @@ from vpt import _lib, ops  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--knob", choices=("stages", "pipe"), default="stages")
+    ap.add_argument("--value", type=int, default=3)
     args = ap.parse_args()
+    setter = _lib.lib.vpt_attn_set_bwd_stages if args.knob == "stages" else _lib.lib.vpt_attn_set_bwd_pipe
+    base = 2 if args.knob == "stages" else 0
+    A, Bv = base, args.value
     dev = torch.device("cuda", 0)
     B, H, n, nd = 8, 12, 4170, 4106
     D = 64 * H
@@ -42,22 +49,22 @@ def main():
     ops.attn_fwd(q4, k4, v4, o4, lse, kb, B, H, n, n, nd)
     outs = {}
 
-    def bwd(stages):
-        _lib.lib.vpt_attn_set_bwd_stages(stages)
+    def bwd(val):
+        setter(val)
         dqk = torch.zeros(M, 2 * D, dtype=torch.bfloat16, device=dev)
         dv = torch.zeros(M, D, dtype=torch.bfloat16, device=dev)
         delta = torch.empty(B, H, n, device=dev)
         ops.attn_bwd(q4, k4, v4, o4, do4, lse, delta, kb, ops._t4(dqk, B, n, H, 0), ops._t4(dqk, B, n, H, D),
                      ops._t4(dv, B, n, H, 0), B, H, n, n, nd)
         return dqk, dv
-    for st in (2, 3):
+    for st in (A, Bv):
         outs[st] = bwd(st)
     torch.cuda.synchronize()
-    eq = all(torch.equal(a, b) for a, b in zip(outs[2], outs[3]))
-    times = {2: [], 3: []}
+    eq = all(torch.equal(a, b) for a, b in zip(outs[A], outs[Bv]))
+    times = {A: [], Bv: []}
     for r in range(args.rounds):
-        for st in ((2, 3) if r % 2 == 0 else (3, 2)):
-            _lib.lib.vpt_attn_set_bwd_stages(st)
+        for st in ((A, Bv) if r % 2 == 0 else (Bv, A)):
+            setter(st)
             dqk = torch.zeros(M, 2 * D, dtype=torch.bfloat16, device=dev)
             dv = torch.zeros(M, D, dtype=torch.bfloat16, device=dev)
             delta = torch.empty(B, H, n, device=dev)
@@ -70,7 +77,8 @@ def main():
             torch.cuda.synchronize()
             times[st].append(s.elapsed_time(e) / 3)
     med = {k: sorted(v)[len(v) // 2] for k, v in times.items()}
-    print(json.dumps({"bitwise_equal": eq, "ms": {k: [round(x, 4) for x in v] for k, v in times.items()},
+    setter(base)
+    print(json.dumps({"knob": args.knob, "bitwise_equal": eq, "ms": {k: [round(x, 4) for x in v] for k, v in times.items()},
                       "median_ms": med}))
 
 
