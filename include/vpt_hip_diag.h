@@ -42,7 +42,6 @@ int vpt_attn_set_fused_workspace(void* ws);
 /* Backward kernel pair: 1 = 64 rows per wave (production default), 0 = the 32-row pair (A/B). */
 int vpt_attn_set_rows64(int on);
 int vpt_attn_set_bwd_stages(int n);
-int vpt_attn_set_bwd_pipe(int mask);
 int vpt_gemm_set_swb_one_group(int on);
 /* NF4 GEMM timing ablations (WRONG results): 0 off, 1 = no dequant, 2 = no NF4 code loads / dequant. */
 int vpt_gemm_set_nf4_ablation(int a);

@@ -1,9 +1,8 @@
 """A diagnostic variant of the attention backward against the production kernel at the C3 shape: bitwise equality of
 dq / dk / dv, then interleaved HIP-event timing (medians).
   --knob stages --value 3: 3-stage LDS rings (vpt_attn_set_bwd_stages)
-  --knob pipe --value M:   software-pipelined block bodies, bit mask M (vpt_attn_set_bwd_pipe)
 
-  VPT_DIAG=1 python tools/attn_bwd_variant_check.py --knob pipe --value 1 [--rounds 6]
+  VPT_DIAG=1 python tools/attn_bwd_variant_check.py --knob stages --value 3 [--rounds 6]
 """
 import os
 os.environ.setdefault("VPT_DIAG", "1")
@@ -22,11 +21,11 @@ from vpt import _lib, ops  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=6)
-    ap.add_argument("--knob", choices=("stages", "pipe"), default="stages")
+    ap.add_argument("--knob", choices=("stages",), default="stages")
     ap.add_argument("--value", type=int, default=3)
     args = ap.parse_args()
-    setter = _lib.lib.vpt_attn_set_bwd_stages if args.knob == "stages" else _lib.lib.vpt_attn_set_bwd_pipe
-    base = 2 if args.knob == "stages" else 0
+    setter = _lib.lib.vpt_attn_set_bwd_stages
+    base = 2
     A, Bv = base, args.value
     dev = torch.device("cuda", 0)
     B, H, n, nd = 8, 12, 4170, 4106

@@ -33,10 +33,7 @@ def main():
     # diagnostic-library switches (run with VPT_DIAG=1): name -> setter(on)
     from vpt import _lib
     diag = {"ATTN_BWD_STAGES3": lambda on: _lib.lib.vpt_attn_set_bwd_stages(3 if on else 2),
-            "SWB_AHEAD": lambda on: _lib.lib.vpt_gemm_set_swb_one_group(0 if on else 1),
-            "BWD_PIPE_DKDV": lambda on: _lib.lib.vpt_attn_set_bwd_pipe(1 if on else 0),
-            "BWD_PIPE_DQ": lambda on: _lib.lib.vpt_attn_set_bwd_pipe(2 if on else 0),
-            "BWD_PIPE_BOTH": lambda on: _lib.lib.vpt_attn_set_bwd_pipe(3 if on else 0)}
+            "SWB_AHEAD": lambda on: _lib.lib.vpt_gemm_set_swb_one_group(0 if on else 1)}
     for k in knobs:
         if k in diag:
             if not _lib.DIAG:

@@ -23,8 +23,6 @@
 // multiply in the backward.
 #include "common.h"
 
-#include <type_traits>
-
 namespace {
 
 struct Tensor4 {       // element strides: batch, head, row; the 64 head dims are contiguous
@@ -64,7 +62,6 @@ int g_variant = 0;  // backward kernel variant (vpt_attn_set_variant; 1, 2 = tim
 int g_waves = 4;    // waves per block (vpt_attn_set_variant 3 -> 8-wave blocks, A/B only)
 float g_tau = kTau; // forward lazy-rescale threshold (vpt_attn_set_rescale_threshold)
 int g_bwd_nst = 2;  // backward LDS ring stages (vpt_attn_set_bwd_stages, A/B)
-int g_bwd_pipe = 0; // backward bodies (vpt_attn_set_bwd_pipe bit mask, A/B): software-pipelined 1 = dK/dV, 2 = dQ body
 int g_rows64 = 0;   // backward variants (vpt_attn_set_rows64 bit mask, A/B): 1 = 64-key dK/dV, 2 = 64-query dQ
                     // at 2 waves / SIMD, 4 = 64-query dQ at 1 wave / SIMD; 0 = the 32-row pair
 #else
@@ -214,13 +211,6 @@ __device__ __forceinline__ bf16x8 pack_acc(const floatx16& a, int s) {
 __device__ __forceinline__ floatx16 mfma32(bf16x8 a, bf16x8 b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
-// Keep a value computed at this point of the stream: an empty volatile asm that "modifies" it, so neither the
-// IR nor the DAG scheduler sinks its producer past the next sched_barrier (pure VALU and LDS loads would move).
-__device__ __forceinline__ void pin(bf16x8& f) { asm volatile("" : "+v"(f)); }
-__device__ __forceinline__ void pin(floatx16& f) { asm volatile("" : "+v"(f)); }
-// sched_group_barrier masks (LLVM AMDGPU): MFMA, VALU incl. transcendentals, DS read
-constexpr int kSgMfma = 0x8, kSgValu = 0x2 | 0x400, kSgDsRead = 0x100;  // VALU | TRANS (v_exp is TRANS)
-#define VPT_SG(mask, n) __builtin_amdgcn_sched_group_barrier(mask, n, 0)
 __device__ __forceinline__ floatx16 splat16(float v) {
   floatx16 r;
 #pragma unroll
@@ -663,115 +653,6 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
       if (more) settle(nxt, (t + 1) * 64, NST == 3 && t + 2 < nt);
       continue;
     }
-    if (ABL == 9) {
-      // Software-pipelined body: every MFMA group carries the other query half's VALU / LDS work in its gaps
-      // (guide: <= 5 single-issue fillers per 32x32x16 gap) instead of running the exp / dS / pack of both halves
-      // as one VALU burst between the chains and the dV / dK products:
-      //   R1  S0 / dP0 chains      || row fragments + row constants of half 1
-      //   R2  S1 / dP1 chains      || exp, dS, bf16 pack of half 0
-      //   R3  dV / dK of half 0    || exp, dS, bf16 pack of half 1 (+ its transposed reads, one product ahead)
-      //   R4  dV / dK of half 1    || transposed reads
-      // Same operations in the same order per accumulator as the other bodies: bitwise equal results.
-      floatx16 s0 = rows16(lstat[cur][0], 0, h), d0 = rows16(lstat[cur][1], 0, h);
-      bf16x8 qa[4], da[4], qb1[4], db1[4];
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) { qa[ks] = frag_rows(lq, 0, ks, lane); da[ks] = frag_rows(ld, 0, ks, lane); }
-      __builtin_amdgcn_sched_barrier(0);
-      // R1
-      floatx16 s1 = rows16(lstat[cur][0], 32, h), d1 = rows16(lstat[cur][1], 32, h);
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        s0 = mfma32(qa[ks], kf[ks], s0);
-        d0 = mfma32(da[ks], vf[ks], d0);
-        qb1[ks] = frag_rows(lq, 32, ks, lane);
-        db1[ks] = frag_rows(ld, 32, ks, lane);
-      }
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) { pin(qb1[ks]); pin(db1[ks]); }
-      pin(s1); pin(d1);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) { VPT_SG(kSgMfma, 1); VPT_SG(kSgDsRead, 2); }
-      __builtin_amdgcn_sched_barrier(0);
-      // R2
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        s1 = mfma32(qb1[ks], kf[ks], s1);
-        d1 = mfma32(db1[ks], vf[ks], d1);
-      }
-      bf16x8 pp0[2], pd0[2];
-      {
-        floatx16 P, dS;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = __builtin_amdgcn_exp2f(s0[i]);
-          P[i] = p;
-          dS[i] = p * d0[i];
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) { pp0[s2] = pack_acc(P, s2); pd0[s2] = pack_acc(dS, s2); pin(pp0[s2]); pin(pd0[s2]); }
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) { VPT_SG(kSgMfma, 1); VPT_SG(kSgValu, 5); }
-      __builtin_amdgcn_sched_barrier(0);
-      // R3
-      bf16x8 pp1[2], pd1[2];
-      {
-        floatx16 P, dS;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = __builtin_amdgcn_exp2f(s1[i]);
-          P[i] = p;
-          dS[i] = p * d1[i];
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) { pp1[s2] = pack_acc(P, s2); pd1[s2] = pack_acc(dS, s2); }
-      }
-      {
-        // all 8 transposed fragments of the region issued first: the in-order LDS returns let each MFMA wait only
-        // for its own pair while the later pairs are in flight
-        bf16x8 tv[2][2], tq[2][2];
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int db = 0; db < 2; ++db) { tv[s2][db] = frag_tr(ld, db, s2, lane); tq[s2][db] = frag_tr(lq, db, s2, lane); }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int db = 0; db < 2; ++db) {
-            dvT[db] = mfma32(tv[s2][db], pp0[s2], dvT[db]);
-            dkT[db] = mfma32(tq[s2][db], pd0[s2], dkT[db]);
-          }
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) { pin(pp1[s2]); pin(pd1[s2]); }
-      VPT_SG(kSgDsRead, 16);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) { VPT_SG(kSgMfma, 1); VPT_SG(kSgValu, 5); }
-      __builtin_amdgcn_sched_barrier(0);
-      // R4
-      {
-        bf16x8 tv[2][2], tq[2][2];
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int db = 0; db < 2; ++db) {
-            tv[s2][db] = frag_tr(ld, db, 2 + s2, lane);
-            tq[s2][db] = frag_tr(lq, db, 2 + s2, lane);
-          }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int db = 0; db < 2; ++db) {
-            dvT[db] = mfma32(tv[s2][db], pp1[s2], dvT[db]);
-            dkT[db] = mfma32(tq[s2][db], pd1[s2], dkT[db]);
-          }
-      }
-      VPT_SG(kSgDsRead, 16);
-      VPT_SG(kSgMfma, 8);
-      __builtin_amdgcn_sched_barrier(0);
-      if (more) settle(nxt, (t + 1) * 64, NST == 3 && t + 2 < nt);
-      continue;
-    }
     floatx16 P[2], dS[2];
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
@@ -946,97 +827,6 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
           __builtin_amdgcn_s_setprio(0);
         }
       }
-      if (younger) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      continue;
-    }
-    if (ABL == 9) {
-      // Software-pipelined body (as dkdv_body's variant 9): R1 the key-half-0 S^T / dP^T chains || half 1's row
-      // fragments; R2 half 1's chains || half 0's bias / exp / dS / pack; R3 half 0's dQ products (transposed reads
-      // first) || half 1's bias / exp / dS / pack; R4 half 1's dQ products. Same operations per accumulator, same
-      // order: bitwise equal.
-      // two copies of the body (with / without the key-bias add) so neither holds a branch between its groups
-      auto run = [&](auto has_bias) {
-      constexpr bool HB = decltype(has_bias)::value;
-      bf16x8 ka[4], va[4], kb1[4], vb1[4];
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) { ka[ks] = frag_rows(lk, 0, ks, lane); va[ks] = frag_rows(lv, 0, ks, lane); }
-      __builtin_amdgcn_sched_barrier(0);
-      floatx16 s0 = nlse, d0 = ndel, s1 = nlse, d1 = ndel;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        s0 = mfma32(ka[ks], qf[ks], s0);
-        d0 = mfma32(va[ks], df[ks], d0);
-        kb1[ks] = frag_rows(lk, 32, ks, lane);
-        vb1[ks] = frag_rows(lv, 32, ks, lane);
-      }
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) { pin(kb1[ks]); pin(vb1[ks]); }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) { VPT_SG(kSgMfma, 1); VPT_SG(kSgDsRead, 1); }
-      __builtin_amdgcn_sched_barrier(0);
-      // R2
-      auto ds_pack = [&](floatx16 sc, const floatx16& dpv, int kb, bf16x8 (&pd)[2]) {
-        if constexpr (HB) {
-#pragma unroll
-          for (int g4 = 0; g4 < 4; ++g4) {
-            const floatx4 bias = *reinterpret_cast<const floatx4*>(&kbl[kv0 - g.kb0 + 32 * kb + 8 * g4 + 4 * h]);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) sc[4 * g4 + e] += bias[e];
-          }
-        }
-        floatx16 d;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) d[i] = __builtin_amdgcn_exp2f(sc[i]) * dpv[i];
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) pd[s2] = pack_acc(d, s2);
-      };
-      bf16x8 pd0[2], pd1[2];
-      ds_pack(s0, d0, 0, pd0);
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        s1 = mfma32(kb1[ks], qf[ks], s1);
-        d1 = mfma32(vb1[ks], df[ks], d1);
-      }
-      pin(pd0[0]); pin(pd0[1]);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) { VPT_SG(kSgMfma, 1); VPT_SG(kSgValu, 4); }
-      __builtin_amdgcn_sched_barrier(0);
-      // R3
-      ds_pack(s1, d1, 1, pd1);
-      {
-        bf16x8 tk[2][2];
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int db = 0; db < 2; ++db) tk[s2][db] = frag_tr(lk, db, s2, lane);
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int db = 0; db < 2; ++db) dqT[db] = mfma32(tk[s2][db], pd0[s2], dqT[db]);
-      }
-      pin(pd1[0]); pin(pd1[1]);
-      VPT_SG(kSgDsRead, 8);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { VPT_SG(kSgMfma, 1); VPT_SG(kSgValu, 6); }
-      __builtin_amdgcn_sched_barrier(0);
-      // R4
-      {
-        bf16x8 tk[2][2];
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int db = 0; db < 2; ++db) tk[s2][db] = frag_tr(lk, db, 2 + s2, lane);
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int db = 0; db < 2; ++db) dqT[db] = mfma32(tk[s2][db], pd1[s2], dqT[db]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      };
-      if (dense) run(std::false_type{});
-      else run(std::true_type{});
       if (younger) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -1334,15 +1124,6 @@ int attn_bwd_impl(AttnArgs& g, int B, int H, int n, int nk, hipStream_t s) {
   }
 #endif
 #ifdef VPT_DIAG
-  if (g_bwd_pipe) {
-    const dim3 grid((nkb + nqb) * H * B);
-    const size_t lds = key_bias_lds_bytes(g);
-    if (g_bwd_pipe == 1) hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, 9, 0>), grid, dim3(256), lds, s, g, nkb, nqb, B);
-    else if (g_bwd_pipe == 2) hipLaunchKernelGGL((attn_bwd_kernel<9, 8, 0>), grid, dim3(256), lds, s, g, nkb, nqb, B);
-    else hipLaunchKernelGGL((attn_bwd_kernel<9, 9, 0>), grid, dim3(256), lds, s, g, nkb, nqb, B);
-    VPT_LAUNCH_CHECK();
-    return VPT_OK;
-  }
   if (g_bwd_nst == 3) {
     hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, 8, 0, 3>), dim3((nkb + nqb) * H * B), dim3(256), key_bias_lds_bytes(g),
                        s, g, nkb, nqb, B);
