@@ -664,6 +664,45 @@ def test_generated_noise_is_gaussian(ops):
     assert abs((v ** 4).mean().item() - 3.0) < 0.05
 
 
+def test_generated_noise_pairs_uncorrelated(ops):
+    """The two draws of a Box-Muller pair (adjacent pixels) and neighbouring pairs are uncorrelated."""
+    B, H, W = 2, 256, 256
+    x = torch.zeros(B, 3, H, W, dtype=torch.float16, device=DEV)
+    p = torch.empty(B * 256, 768, dtype=torch.bfloat16, device=DEV)
+    ops.patchify(x, B, H, W, p, t=torch.zeros(B, device=DEV), seed=99)
+    v = p.float().view(-1, 2)  # (kx even, kx + 1): one pair
+    assert abs(torch.corrcoef(v.t())[0, 1].item()) < 0.01
+    w = p.float().view(-1, 4)  # pair j vs pair j + 1
+    assert abs(torch.corrcoef(torch.stack([w[:, 0], w[:, 2]]))[0, 1].item()) < 0.01
+    q = torch.empty_like(p)
+    ops.patchify(x, B, H, W, q, t=torch.zeros(B, device=DEV), seed=100)
+    assert abs(torch.corrcoef(torch.stack([p.float().flatten(), q.float().flatten()]))[0, 1].item()) < 0.01
+
+
+def test_generated_noise_depends_on_seed_only(ops):
+    """z(t) of two patchify calls with one seed use the same noise: z(0.5) = bf16(0.5 x + 0.5 eps) with eps from
+    z(0) (bf16-rounded there, hence the tolerance); the velocity loss with in-kernel noise is reproducible."""
+    B, H, W = 2, 64, 96
+    np_ = (H // 16) * (W // 16)
+    x = rnd(B, 3, H, W, dtype=torch.float16, seed=70)
+    z0 = torch.empty(B * np_, 768, dtype=torch.bfloat16, device=DEV)
+    z5 = torch.empty_like(z0)
+    ops.patchify(x, B, H, W, z0, t=torch.zeros(B, device=DEV), seed=4242)
+    ops.patchify(x, B, H, W, z5, t=torch.full((B,), 0.5, device=DEV), seed=4242)
+    xp = x.view(B, 3, H // 16, 16, W // 16, 16).permute(0, 2, 4, 1, 3, 5).reshape(-1, 768).float()
+    assert (z5.float() - (0.5 * xp + 0.5 * z0.float())).abs().max().item() < 0.03
+    t = torch.tensor([0.3, 0.75], device=DEV)
+    pred = rnd(B * np_, 768, seed=71)
+    outs = []
+    for _ in range(2):
+        d = torch.empty_like(pred)
+        part = torch.empty(ops.loss_blocks(), device=DEV)
+        loss = torch.empty(1, device=DEV)
+        ops.flow_loss(pred, x, t, B, H, W, d, part, loss, target=1, seed=4242)
+        outs.append((loss.clone(), d))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("target", [0, 1])
 def test_flow_loss(ops, target):
     B, H, W = 2, 64, 32

@@ -20,42 +20,79 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
   return z ^ (z >> 31);
 }
-// Standard normal for element `idx` of stream `seed`, rounded to fp16 like randn_like(fp16 image).
-__device__ __forceinline__ float gauss_fp16(uint64_t seed, uint64_t idx) {
-  const uint64_t h = mix64(seed * 0x632be59bd9b4e019ull ^ mix64(idx));
-  const float u1 = ((float)(uint32_t)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);   // (0,1)
-  const float u2 = (float)((uint32_t)h & 0xffffffu) * (1.0f / 16777216.0f);
-  // Box-Muller on the transcendental units: v_log_f32 (log2; ln u1 = ln2 * log2 u1) and v_cos_f32, whose
-  // argument is in revolutions, so cos(2 pi u2) needs no range reduction (libm logf / cosf made the
-  // noising pass VALU-bound at ~1.3 TB/s)
-  const float r = sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
-  const float g = r * __builtin_amdgcn_cosf(u2);
-  return h2f(f2h(g));
+// Counter-based standard normals, rounded to fp16 like randn_like(fp16 image): pixel pair j = idx / 2 is one
+// Box-Muller draw from two keyed 32-bit hashes of j (lowbias32: 2 multiplies, 3 xor-shifts), element 2j taking
+// r cos(2 pi u2), element 2j+1 r sin(2 pi u2). On the transcendental units: v_log_f32 (log2; ln u1 = ln2 log2 u1),
+// v_cos_f32 / v_sin_f32 (argument in revolutions: no range reduction). 32-bit integer work only and both draws of
+// a pair used: the per-element cost is a quarter of a 64-bit splitmix per element, which kept the noising pass
+// VALU-bound. A pure function of (seed, idx): the loss regenerates the forward's noise.
+struct NoiseKey {
+  uint32_t a, b;
+};
+__device__ __forceinline__ NoiseKey noise_key(uint64_t seed) {
+  const uint64_t m = mix64(seed);
+  return {(uint32_t)m, (uint32_t)(m >> 32)};
 }
-
-// z = t*x + (1-t)*eps written in patch-major im2col layout (col = c*P*P + ky*P + kx).
-// in_kind 0: x fp16 + noise (generated or explicit fp16 `noise`), in_kind 1: x bf16 copied as is.
-__global__ void patchify_kernel(const unsigned short* __restrict__ img, int in_kind, const unsigned short* __restrict__ noise,
-                                const float* __restrict__ t, float noise_scale, uint64_t seed, int B, int H, int W,
-                                bf16_t* __restrict__ out) {
-  const int hp = H / 16, wp = W / 16, np_ = hp * wp;
-  const long total = (long)B * np_ * 96;
-  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= total) return;
-  const long row = gid / 96;
-  const int chunk = gid % 96;
-  const int c = chunk >> 5, rem = chunk & 31, ky = rem >> 1, kx0 = (rem & 1) * 8;
-  const int b = row / np_, p = row % np_;
-  const int y = (p / wp) * 16 + ky, x = (p % wp) * 16 + kx0;
-  const long base = (((long)b * 3 + c) * H + y) * W + x;
-  const uint4 v = *reinterpret_cast<const uint4*>(img + base);
-  const unsigned short* vs = reinterpret_cast<const unsigned short*>(&v);
-  float o[8];
-  if (in_kind == 1) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = bf2f(vs[e]);
-  } else {
-    const float tb = t[b];
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t pair_counter(uint64_t idx) {
+  const uint64_t j = idx >> 1;
+  return (uint32_t)j ^ ((uint32_t)(j >> 32) * 0x85ebca6bu);
+}
+// (radius, angle in revolutions) of pair j
+__device__ __forceinline__ float2 gauss_polar(NoiseKey k, uint32_t j) {
+  const uint32_t w = j * 0x9e3779b9u;
+  const uint32_t h1 = lowbias32(w + k.a), h2 = lowbias32(w ^ k.b);
+  const float u1 = ((float)(h1 >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0,1)
+  const float u2 = (float)(h2 >> 8) * (1.0f / 16777216.0f);            // [0,1)
+  return {sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1)), u2};
+}
+// both elements of pair j (fp16-rounded)
+__device__ __forceinline__ void gauss_pair_fp16(NoiseKey k, uint32_t j, float& g0, float& g1) {
+  const float2 ra = gauss_polar(k, j);
+  g0 = h2f(f2h(ra.x * __builtin_amdgcn_cosf(ra.y)));
+  g1 = h2f(f2h(ra.x * __builtin_amdgcn_sinf(ra.y)));
+}
+// Strips: up to kStripP horizontally adjacent 16x16 patches of one patch row, i.e. 3 x 16 image rows of up to
+// 64 pixels (128 B per row piece: whole cache lines). patchify and the loss stage a strip's pixels through LDS by
+// coalesced 16-B row reads and map them onto the patch layouts from there (the patch layouts' 16-B pieces are 8
+// pixels of one row (patchify) or 2.67 pixels x 3 channels (prediction): read from the NCHW image directly they
+// were 32-B or 2-B gathers).
+constexpr int kStripP = 4;
+struct Strip {
+  int b, py, px0, np;  // batch, patch row, first patch column, patches in the strip
+};
+__device__ __forceinline__ Strip strip_of(long s, int hp, int wp) {
+  const int spr = (wp + kStripP - 1) / kStripP;
+  Strip r;
+  r.b = (int)(s / ((long)hp * spr));
+  const int rem = (int)(s - (long)r.b * hp * spr);
+  r.py = rem / spr;
+  r.px0 = (rem - r.py * spr) * kStripP;
+  r.np = min(kStripP, wp - r.px0);
+  return r;
+}
+// Stage the strip's pixels (fp16 / bf16 bits) into px[c][ky][0, 16 np) and, with want_eps, its noise
+// eps = fp16(noise * noise_scale) (explicit fp16 `noise`, or generated) into eps[c][ky][...]: 16-B pieces of 8 pixels
+// of one image row. (Loading the next strip's pieces into registers one strip ahead was measured slower: the extra
+// registers cost more waves per CU than the overlap gained, r04p.)
+__device__ __forceinline__ void stage_strip(const Strip& st, const unsigned short* __restrict__ img,
+                                            const unsigned short* __restrict__ noise, bool want_eps, NoiseKey key,
+                                            float noise_scale, int H, int W,
+                                            unsigned short (&px)[3][16][16 * kStripP],
+                                            unsigned short (&eps)[3][16][16 * kStripP]) {
+  const int cpr = st.np * 2;  // 16-B pieces per image row of the strip
+  for (int i = threadIdx.x; i < 48 * cpr; i += blockDim.x) {
+    const int rr = i / cpr, cc = i - rr * cpr, c = rr >> 4, ky = rr & 15;
+    const long base = (((long)st.b * 3 + c) * H + st.py * 16 + ky) * W + st.px0 * 16 + cc * 8;
+    *reinterpret_cast<uint4*>(&px[c][ky][cc * 8]) = *reinterpret_cast<const uint4*>(img + base);
+    if (!want_eps) continue;
     float nz[8];
     if (noise) {
       const uint4 nv = *reinterpret_cast<const uint4*>(noise + base);
@@ -63,16 +100,63 @@ __global__ void patchify_kernel(const unsigned short* __restrict__ img, int in_k
 #pragma unroll
       for (int e = 0; e < 8; ++e) nz[e] = h2f(ns[e]);
     } else {
+      const uint32_t j0 = pair_counter((uint64_t)base);  // base is even (W, x multiples of 8)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) nz[e] = gauss_fp16(seed, (uint64_t)(base + e));
+      for (int e = 0; e < 4; ++e) gauss_pair_fp16(key, j0 + e, nz[2 * e], nz[2 * e + 1]);
     }
+    unsigned short ev[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float eps = h2f(f2h(nz[e] * noise_scale));
-      o[e] = tb * h2f(vs[e]) + (1.f - tb) * eps;
-    }
+    for (int e = 0; e < 8; ++e) ev[e] = f2h(nz[e] * noise_scale);
+    *reinterpret_cast<uint4*>(&eps[c][ky][cc * 8]) = *reinterpret_cast<const uint4*>(ev);
   }
-  *reinterpret_cast<uint4*>(out + row * 768 + chunk * 8) = pack8(o);
+}
+
+// z = t*x + (1-t)*eps written in patch-major im2col layout (col = c*P*P + ky*P + kx).
+// in_kind 0: x fp16 + noise (generated or explicit fp16 `noise`), in_kind 1: x bf16 copied as is.
+// An output piece (8 kx of one (c, ky)) is one 16-B piece of an image row, so no transposition is needed -- only
+// the thread order: threads walk a strip's image-row pieces in row order (a wave reads 8 image rows x 128 B, whole
+// lines) and write each piece to its patch row (per wave 4 runs of 256 B). The previous order (output order) read
+// 32-B row pieces of 16 rows per wave.
+__global__ __launch_bounds__(256) void patchify_kernel(const unsigned short* __restrict__ img, int in_kind,
+                                                       const unsigned short* __restrict__ noise,
+                                                       const float* __restrict__ t, float noise_scale, uint64_t seed,
+                                                       int B, int H, int W, bf16_t* __restrict__ out) {
+  const int hp = H / 16, wp = W / 16;
+  const long strips = (long)B * hp * ((wp + kStripP - 1) / kStripP);
+  const long pieces = strips * 96 * kStripP;  // upper bound: partial strips leave their tail threads idle
+  const NoiseKey key = noise_key(seed);
+  for (long gid = (long)blockIdx.x * blockDim.x + threadIdx.x; gid < pieces; gid += (long)gridDim.x * blockDim.x) {
+    const Strip st = strip_of(gid / (96 * kStripP), hp, wp);
+    const int i = (int)(gid % (96 * kStripP));
+    const int cpr = st.np * 2;
+    if (i >= 48 * cpr) continue;
+    const int rr = i / cpr, cc = i - rr * cpr, c = rr >> 4, ky = rr & 15, pl = cc >> 1, kx0 = (cc & 1) * 8;
+    const long base = (((long)st.b * 3 + c) * H + st.py * 16 + ky) * W + st.px0 * 16 + cc * 8;
+    const uint4 v = *reinterpret_cast<const uint4*>(img + base);
+    const unsigned short* vs = reinterpret_cast<const unsigned short*>(&v);
+    float o[8];
+    if (in_kind == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = bf2f(vs[e]);
+    } else {
+      const float tb = t[st.b];
+      float nz[8];
+      if (noise) {
+        const uint4 nv = *reinterpret_cast<const uint4*>(noise + base);
+        const unsigned short* ns = reinterpret_cast<const unsigned short*>(&nv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) nz[e] = h2f(ns[e]);
+      } else {
+        const uint32_t j0 = pair_counter((uint64_t)base);  // base is even (W, x multiples of 8)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gauss_pair_fp16(key, j0 + e, nz[2 * e], nz[2 * e + 1]);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = tb * h2f(vs[e]) + (1.f - tb) * h2f(f2h(nz[e] * noise_scale));
+    }
+    const long row = ((long)st.b * hp + st.py) * wp + st.px0 + pl;
+    *reinterpret_cast<uint4*>(out + row * 768 + c * 256 + ky * 16 + kx0) = pack8(o);
+  }
 }
 
 // Patch rows [B*np][P*P*3] (col = (ky*P + kx)*3 + c) <-> image [B][3][H][W] (bf16), P = 16.
@@ -162,43 +246,61 @@ __global__ void scale_bf16_2d_kernel(const bf16_t* __restrict__ a, long lda, lon
 
 // Flow-matching MSE over patch-layout predictions; also writes d(loss)/d(pred) (bf16, patch layout).
 // target 0 ("image"): mse(pred, x); target 1 ("velocity"): mse((pred-z)/c, (x-z)/c), c = clamp(1-t, eps).
+// Per strip (grid-stride, fixed assignment): the thread's prediction pieces are loaded first (in flight while the
+// strip's pixels / noise are staged through LDS), then each 16-B piece (col = (ky*16 + kx)*3 + c) is mapped onto
+// the staged strip. Per-thread sums in a fixed order, one partial per block: deterministic.
 __global__ __launch_bounds__(256) void loss_kernel(const bf16_t* __restrict__ pred, const unsigned short* __restrict__ img,
                                                    const unsigned short* __restrict__ noise, const float* __restrict__ t,
                                                    float noise_scale, uint64_t seed, int target, float t_eps, int B,
                                                    int H, int W, float inv_numel, bf16_t* __restrict__ dpred,
                                                    float* __restrict__ part) {
   __shared__ float red[256];
-  const int hp = H / 16, wp = W / 16, np_ = hp * wp;
-  const long total = (long)B * np_ * 96;
+  __shared__ __attribute__((aligned(16))) unsigned short px[3][16][16 * kStripP];
+  __shared__ __attribute__((aligned(16))) unsigned short eps[3][16][16 * kStripP];
+  const int hp = H / 16, wp = W / 16;
+  const long strips = (long)B * hp * ((wp + kStripP - 1) / kStripP);
+  const NoiseKey key = noise_key(seed);
+  constexpr int kPer = (96 * kStripP + 255) / 256;  // prediction pieces per thread per strip
   float acc = 0.f;
-  for (long gid = (long)blockIdx.x * blockDim.x + threadIdx.x; gid < total; gid += (long)gridDim.x * blockDim.x) {
-    const long row = gid / 96;
-    const int chunk = gid % 96;
-    const int b = row / np_, p = row % np_;
-    const int y0 = (p / wp) * 16, x0 = (p % wp) * 16;
-    float pr[8], g[8];
-    unpack8(*reinterpret_cast<const uint4*>(pred + row * 768 + chunk * 8), pr);
-    const float tb = t[b];
+  for (long s = blockIdx.x; s < strips; s += gridDim.x) {
+    const Strip st = strip_of(s, hp, wp);
+    const long row0 = ((long)st.b * hp + st.py) * wp + st.px0;
+    uint4 pv[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int i = threadIdx.x + k * 256;
+      pv[k] = i < st.np * 96 ? *reinterpret_cast<const uint4*>(pred + row0 * 768 + i * 8) : make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();  // the previous strip's LDS reads are done
+    stage_strip(st, img, noise, target == 1, key, noise_scale, H, W, px, eps);
+    __syncthreads();
+    const float tb = t[st.b];
     const float cl = fmaxf(1.f - tb, t_eps);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int col = chunk * 8 + e, pix = col / 3, c = col - pix * 3;
-      const long idx = (((long)b * 3 + c) * H + y0 + (pix >> 4)) * W + x0 + (pix & 15);
-      const float xv = h2f(img[idx]);
-      float diff;
-      if (target == 0) {
-        diff = pr[e] - xv;
-        g[e] = 2.f * diff * inv_numel;
-      } else {
-        const float nz = noise ? h2f(noise[idx]) : gauss_fp16(seed, (uint64_t)idx);
-        const float eps = h2f(f2h(nz * noise_scale));
-        const float z = tb * xv + (1.f - tb) * eps;
-        diff = (pr[e] - z) / cl - (xv - z) / cl;
-        g[e] = 2.f * diff * inv_numel / cl;
+    for (int k = 0; k < kPer; ++k) {
+      const int i = threadIdx.x + k * 256;
+      if (i >= st.np * 96) continue;
+      const int pl = i / 96, chunk = i - pl * 96;
+      float pr[8], g[8];
+      unpack8(pv[k], pr);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int col = chunk * 8 + e, pix = col / 3, c = col - pix * 3;
+        const int ky = pix >> 4, kx = pl * 16 + (pix & 15);
+        const float xv = h2f(px[c][ky][kx]);
+        float diff;
+        if (target == 0) {
+          diff = pr[e] - xv;
+          g[e] = 2.f * diff * inv_numel;
+        } else {
+          const float z = tb * xv + (1.f - tb) * h2f(eps[c][ky][kx]);
+          diff = (pr[e] - z) / cl - (xv - z) / cl;
+          g[e] = 2.f * diff * inv_numel / cl;
+        }
+        acc += diff * diff;
       }
-      acc += diff * diff;
+      *reinterpret_cast<uint4*>(dpred + (row0 + pl) * 768 + chunk * 8) = pack8(g);
     }
-    *reinterpret_cast<uint4*>(dpred + row * 768 + chunk * 8) = pack8(g);
   }
   red[threadIdx.x] = acc;
   __syncthreads();
@@ -642,8 +744,8 @@ extern "C" int vpt_patchify(const void* img, int in_kind, const void* noise, con
   VPT_CHECK_ARG(img && out && B > 0, "vpt_patchify: bad args");
   VPT_CHECK_ARG(H % 16 == 0 && W % 16 == 0, "vpt_patchify: H and W must be multiples of the 16-px patch");
   VPT_CHECK_ARG(in_kind == 1 || t, "vpt_patchify: noising needs t");
-  const long total = (long)B * (H / 16) * (W / 16) * 96;
-  hipLaunchKernelGGL(patchify_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream, (const unsigned short*)img,
+  const long pieces = (long)B * (H / 16) * ((W / 16 + kStripP - 1) / kStripP) * 96 * kStripP;
+  hipLaunchKernelGGL(patchify_kernel, grid1(pieces), dim3(256), 0, (hipStream_t)stream, (const unsigned short*)img,
                      in_kind, (const unsigned short*)noise, t, noise_scale, (uint64_t)seed, B, H, W, (bf16_t*)out);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
@@ -696,7 +798,7 @@ extern "C" int vpt_scale_bf16_2d(const void* a, long lda, long rows, int cols, f
   return VPT_OK;
 }
 
-extern "C" int vpt_loss_blocks(void) { return 1024; }
+extern "C" int vpt_loss_blocks(void) { return 4096; }
 
 extern "C" int vpt_flow_loss(const void* pred, const void* img, const void* noise, const float* t, float noise_scale,
                              unsigned long long seed, int target, float t_eps, int B, int H, int W, void* dpred,
