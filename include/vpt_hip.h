@@ -101,6 +101,12 @@ int vpt_gemm_bf16_lora_stacked(const void* A, long lda, const void* B, long ldb,
 int vpt_linear_wgrad(const void* dy, long lddy, const void* x, long ldx, float* dw, long lddw, float* db, long M,
                      int N, int K, int accumulate, int splits, void* workspace, int geometry, int ring_grid,
                      void* stream);
+/* vpt_linear_wgrad plus one unrelated column sum rr_out[c] (=|+=) sum_r rr_part[r][c] over a [rr_R][rr_C] f32 partial
+ * set (the vpt_reduce_rows job of, e.g., an RMSNorm weight gradient), done by extra blocks of the weight gradient's
+ * split-K reduce launch instead of a launch of its own. Fixed summation order (deterministic). */
+int vpt_linear_wgrad_rr(const void* dy, long lddy, const void* x, long ldx, float* dw, long lddw, float* db, long M,
+                        int N, int K, int accumulate, int splits, void* workspace, int geometry, int ring_grid,
+                        const float* rr_part, int rr_R, int rr_C, float* rr_out, int rr_acc, void* stream);
 long vpt_linear_wgrad_workspace_bytes(long M, int N, int K, int splits);
 
 /* Fused SwiGLU MLP GEMMs (src/models/jit/denoiser.py:480-506 SwiGLU, :535-543 FinalLayer):

@@ -200,6 +200,34 @@ def test_linear_wgrad_fused_bias(ops, geo, grid, splits, M, N, K):
     assert rel(b, 2 * ref_b) < 1e-5
 
 
+@pytest.mark.parametrize("geo,splits,bias", [(256, 1, True), (256, 4, True), (256, 3, False), (128, 1, False),
+                                             (128, 2, True), (0, 1, False)])
+def test_linear_wgrad_rows_sum_job(ops, geo, splits, bias):
+    """vpt_linear_wgrad_rr: the weight / bias gradients bitwise what vpt_linear_wgrad gives, and the riding column sum
+    (store and accumulate) within f32 summation error of a float64 sum, bitwise reproducible -- also where no split-K
+    reduce launch would otherwise run (splits 1, no ring bias sums)."""
+    M, N, K = 2100, 768, 512
+    dy = rnd(M, N, seed=160)
+    x = rnd(M, K, seed=161)
+    part = rnd(512, 768, dtype=torch.float32, seed=162)
+    w1, w2 = (torch.empty(N, K, dtype=torch.float32, device=DEV) for _ in range(2))
+    b1, b2 = (torch.empty(N, dtype=torch.float32, device=DEV) for _ in range(2))
+    r1, r2 = torch.empty(768, device=DEV), torch.empty(768, device=DEV)
+    ops.linear_wgrad(dy, x, w1, splits=splits, bias_out=b1 if bias else None, geometry=geo)
+    ops.linear_wgrad(dy, x, w2, splits=splits, bias_out=b2 if bias else None, geometry=geo, rows_sum=(part, r1, False))
+    assert torch.equal(w1, w2)
+    if bias:
+        assert torch.equal(b1, b2)
+    ref = part.double().sum(0)
+    tol = 1e-5 * part.abs().sum(0).max().item()
+    assert (r1.double() - ref).abs().max().item() < tol
+    ops.linear_wgrad(dy, x, w2, splits=splits, geometry=geo, rows_sum=(part, r2, False))
+    assert torch.equal(r1, r2)
+    base = r1.clone()
+    ops.linear_wgrad(dy, x, w2, splits=splits, geometry=geo, rows_sum=(part, r1, True))
+    assert (r1.double() - (base.double() + ref)).abs().max().item() < 2 * tol
+
+
 @pytest.mark.parametrize("M", [5192, 33360])
 def test_swiglu_fused_epilogues_match_unfused(ops, M):
     """The fused SwiGLU ring epilogues the bench runs (forward sw=1: W1|W2 GEMM -> x12, h; backward sw=2:

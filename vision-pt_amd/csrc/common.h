@@ -156,3 +156,36 @@ extern "C" void vpt_set_error(const char* msg);
       return VPT_ELAUNCH;                                    \
     }                                                        \
   } while (0)
+
+// Column sums of a [R][C] f32 partial set for columns [16 cb, 16 cb + 16): out[c] (=|+=) sum_r in[r][c]. One block of
+// 4 * RG threads (4 lanes x float4 = 16 columns, RG row groups): each row group strides over the rows in a fixed
+// order, then a fixed pairwise tree over the row groups in `red` (deterministic, no atomics). Used by vpt_reduce_rows
+// and, as an extra job riding a weight gradient's split-K reduce launch, by vpt_linear_wgrad_rr.
+template <int RG>
+__device__ __forceinline__ void colsum_block(const float* __restrict__ in, int R, int C, float* __restrict__ out,
+                                             int accumulate, int cb, floatx4 (&red)[RG][4]) {
+  const int cl = threadIdx.x & 3, rg = threadIdx.x >> 2;
+  const int c = cb * 16 + cl * 4;
+  floatx4 s = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    if (C % 4 == 0) {
+#pragma unroll 4
+      for (int r = rg; r < R; r += RG) s += *reinterpret_cast<const floatx4*>(in + (long)r * C + c);
+    } else {
+      for (int r = rg; r < R; r += RG)
+        for (int e = 0; e < 4; ++e)
+          if (c + e < C) s[e] += in[(long)r * C + c + e];
+    }
+  }
+  red[rg][cl] = s;
+  __syncthreads();
+#pragma unroll
+  for (int st = RG / 2; st >= 1; st >>= 1) {
+    if (rg < st) red[rg][cl] += red[rg + st][cl];
+    __syncthreads();
+  }
+  if (rg == 0 && c < C) {
+    const floatx4 t = red[0][cl];
+    for (int e = 0; e < 4 && c + e < C; ++e) out[c + e] = accumulate ? out[c + e] + t[e] : t[e];
+  }
+}

@@ -1265,12 +1265,28 @@ int launch_geo(const GemmArgs& g, int splits, int geo, hipStream_t s) {
   return launch<AK, BK_, 128, 128, 2, 2>(g, splits, s);
 }
 
+// A column-sum job that rides a split-K reduce launch (vpt_linear_wgrad_rr): out[c] (=|+=) sum_r part[r][c].
+struct ColSumJob {
+  const float* part;
+  int R, C;
+  float* out;
+  int acc;
+};
+
 // Fixed-order sum of the split-K partial slabs (blocks [0, cblocks)) and, in the same launch, of the
-// per-split row sums of a fused bias gradient (blocks from cblocks: rout[m] (+)= sum_z rpart[z][m]).
-__global__ void splitk_reduce_kernel(const float* __restrict__ part, long n, int splits, long stride,
-                                     void* out, int out_mode, long cblocks, const float* __restrict__ rpart,
-                                     int rsplits, int rn, float* rout, int racc, const bf16_t* __restrict__ bias,
-                                     const bf16_t* __restrict__ resid, long ldr, int ncols) {
+// per-split row sums of a fused bias gradient (blocks [cblocks, xblock0): rout[m] (+)= sum_z rpart[z][m]) and of an
+// unrelated column-sum job (blocks from xblock0, 16 columns each: colsum_block<64>).
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, long n, int splits,
+                                                            long stride, void* out, int out_mode, long cblocks,
+                                                            const float* __restrict__ rpart, int rsplits, int rn,
+                                                            float* rout, int racc, const bf16_t* __restrict__ bias,
+                                                            const bf16_t* __restrict__ resid, long ldr, int ncols,
+                                                            long xblock0, ColSumJob xj) {
+  if ((long)blockIdx.x >= xblock0) {
+    __shared__ floatx4 red[64][4];
+    colsum_block<64>(xj.part, xj.R, xj.C, xj.out, xj.acc, (int)((long)blockIdx.x - xblock0), red);
+    return;
+  }
   if ((long)blockIdx.x >= cblocks) {
     const long m = ((long)blockIdx.x - cblocks) * blockDim.x + threadIdx.x;
     if (m >= rn) return;
@@ -1332,7 +1348,7 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
               void* workspace, float alpha, int geo_req, int ring_grid, void* stream, float* rsum_out = nullptr,
               int rsum_acc = 0, bool* rsum_done = nullptr, const void* A2 = nullptr, long lda2 = 0,
               const void* B2 = nullptr, long ldb2 = 0, int K2 = 0, const void* const* B2g = nullptr, int G = 0,
-              int g_n = 0, int alpha_cols = 0);
+              int g_n = 0, int alpha_cols = 0, const ColSumJob* xj = nullptr);
 
 }  // namespace
 
@@ -1473,7 +1489,7 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
               int N, int K, const void* bias, const void* resid, long ldr, int out_mode, int act, int splits,
               void* workspace, float alpha, int geo_req, int ring_grid, void* stream, float* rsum_out, int rsum_acc,
               bool* rsum_done, const void* A2, long lda2, const void* B2, long ldb2, int K2,
-              const void* const* B2g, int G, int g_n, int alpha_cols) {
+              const void* const* B2g, int G, int g_n, int alpha_cols, const ColSumJob* xj) {
   VPT_CHECK_ARG(A && B && C, "vpt_gemm_bf16: null operand");
   VPT_CHECK_ARG(alpha_cols >= 0 && alpha_cols % 128 == 0, "vpt_gemm_bf16: alpha_cols a multiple of 128");
   VPT_CHECK_ARG(M > 0 && N > 0 && K > 0, "vpt_gemm_bf16: empty shape");
@@ -1548,14 +1564,16 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
   else if (a_kmajor && !b_kmajor) rc = launch_geo<true, false>(g, splits, geo, s);
   else if (!a_kmajor && b_kmajor) rc = launch_geo<false, true>(g, splits, geo, s);
   else rc = launch_geo<false, false>(g, splits, geo, s);
-  if (rc != VPT_OK || (splits == 1 && !rs)) return rc;
+  if (rc != VPT_OK || (splits == 1 && !rs && !xj)) return rc;
   const long n = splits > 1 ? (long)M * N : 0;
   const int threads = 256;
   const long cblocks = (n / 4 + threads - 1) / threads;
   const long rblocks = rs ? (M + threads - 1) / threads : 0;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(cblocks + rblocks), dim3(threads), 0, s, (const float*)workspace, n,
-                     splits, (long)M * N, C, final_mode, cblocks, rpart, splits, M, rsum_out, rsum_acc,
-                     splits > 1 ? (const bf16_t*)bias : nullptr, splits > 1 ? (const bf16_t*)resid : nullptr, ldr, N);
+  const long xblocks = xj ? (xj->C + 15) / 16 : 0;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(cblocks + rblocks + xblocks), dim3(threads), 0, s,
+                     (const float*)workspace, n, splits, (long)M * N, C, final_mode, cblocks, rpart, splits, M, rsum_out,
+                     rsum_acc, splits > 1 ? (const bf16_t*)bias : nullptr, splits > 1 ? (const bf16_t*)resid : nullptr,
+                     ldr, N, cblocks + rblocks, xj ? *xj : ColSumJob{});
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
@@ -1625,18 +1643,42 @@ extern "C" long vpt_linear_wgrad_workspace_bytes(long M, int N, int K, int split
   return ring > cs ? ring : cs;
 }
 
-extern "C" int vpt_linear_wgrad(const void* dy, long lddy, const void* x, long ldx, float* dw, long lddw, float* db,
-                                long M, int N, int K, int accumulate, int splits, void* workspace, int geometry,
-                                int ring_grid, void* stream) {
+namespace {
+int linear_wgrad_impl(const void* dy, long lddy, const void* x, long ldx, float* dw, long lddw, float* db, long M,
+                      int N, int K, int accumulate, int splits, void* workspace, int geometry, int ring_grid,
+                      void* stream, const ColSumJob* xj) {
   VPT_CHECK_ARG(dy && x && dw && M > 0 && M < (1L << 31), "vpt_linear_wgrad: bad args");
   VPT_CHECK_ARG(!db || workspace, "vpt_linear_wgrad: a bias gradient needs the workspace");
   VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256, "vpt_linear_wgrad: geometry 0, 128 or 256");
   bool done = false;
+  // the column-sum job (its own buffers) rides the reduce launch that follows the GEMM, which gemm_impl then issues
+  // even without split-K slabs or bias row sums
   const int rc = gemm_impl(dy, lddy, 0, x, ldx, 0, dw, lddw, N, K, (int)M, nullptr, nullptr, 0,
                            accumulate ? OUT_F32_ACC : OUT_F32, ACT_NONE, splits, workspace, 1.f, geometry, ring_grid,
-                           stream, db, accumulate, &done);
+                           stream, db, accumulate, &done, nullptr, 0, nullptr, 0, 0, nullptr, 0, 0, 0, xj);
   if (rc != VPT_OK || !db || done) return rc;
   return vpt_bias_grad(dy, lddy, M, N, (float*)workspace, db, accumulate, stream);
+}
+}  // namespace
+
+extern "C" int vpt_linear_wgrad(const void* dy, long lddy, const void* x, long ldx, float* dw, long lddw, float* db,
+                                long M, int N, int K, int accumulate, int splits, void* workspace, int geometry,
+                                int ring_grid, void* stream) {
+  return linear_wgrad_impl(dy, lddy, x, ldx, dw, lddw, db, M, N, K, accumulate, splits, workspace, geometry, ring_grid,
+                           stream, nullptr);
+}
+
+// vpt_linear_wgrad plus one unrelated column sum rr_out[c] (=|+=) sum_r rr_part[r][c] ([rr_R][rr_C] f32, e.g. an
+// RMSNorm weight gradient's partial rows), computed by extra blocks of the weight gradient's split-K reduce launch
+// instead of a launch of its own (vpt_reduce_rows semantics; the 256-thread summation order).
+extern "C" int vpt_linear_wgrad_rr(const void* dy, long lddy, const void* x, long ldx, float* dw, long lddw, float* db,
+                                   long M, int N, int K, int accumulate, int splits, void* workspace, int geometry,
+                                   int ring_grid, const float* rr_part, int rr_R, int rr_C, float* rr_out, int rr_acc,
+                                   void* stream) {
+  VPT_CHECK_ARG(rr_part && rr_out && rr_R > 0 && rr_C > 0, "vpt_linear_wgrad_rr: bad column-sum job");
+  const ColSumJob xj{rr_part, rr_R, rr_C, rr_out, rr_acc};
+  return linear_wgrad_impl(dy, lddy, x, ldx, dw, lddw, db, M, N, K, accumulate, splits, workspace, geometry, ring_grid,
+                           stream, &xj);
 }
 
 // ---- fused SwiGLU GEMMs (the JiT MLP, denoiser.py:480-506; FinalLayer 535-543) ---------------------

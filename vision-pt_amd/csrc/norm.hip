@@ -259,30 +259,7 @@ template <int RG>
 __global__ __launch_bounds__(4 * RG) void reduce_rows_kernel(const float* __restrict__ in, int R, int C,
                                                              float* __restrict__ out, int accumulate) {
   __shared__ floatx4 red[RG][4];
-  const int cl = threadIdx.x & 3, rg = threadIdx.x >> 2;
-  const int c = blockIdx.x * 16 + cl * 4;
-  floatx4 s = {0.f, 0.f, 0.f, 0.f};
-  if (c < C) {
-    if (C % 4 == 0) {
-#pragma unroll 4
-      for (int r = rg; r < R; r += RG) s += *reinterpret_cast<const floatx4*>(in + (long)r * C + c);
-    } else {
-      for (int r = rg; r < R; r += RG)
-        for (int e = 0; e < 4; ++e)
-          if (c + e < C) s[e] += in[(long)r * C + c + e];
-    }
-  }
-  red[rg][cl] = s;
-  __syncthreads();
-#pragma unroll
-  for (int st = RG / 2; st >= 1; st >>= 1) {
-    if (rg < st) red[rg][cl] += red[rg + st][cl];
-    __syncthreads();
-  }
-  if (rg == 0 && c < C) {
-    const floatx4 t = red[0][cl];
-    for (int e = 0; e < 4 && c + e < C; ++e) out[c + e] = accumulate ? out[c + e] + t[e] : t[e];
-  }
+  colsum_block<RG>(in, R, C, out, accumulate, blockIdx.x, red);
 }
 
 }  // namespace

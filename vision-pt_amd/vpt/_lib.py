@@ -27,6 +27,7 @@ SIGNATURES: dict[str, list] = {
     "vpt_gemm_bf16_tiled": [P, L, I, P, L, I, P, L, I, I, I, P, P, L, I, I, I, P, F, I, I, P],
     "vpt_gemm_bf16_lora": [P, L, P, L, I, P, L, P, L, I, P, L, I, I, I, P, P, L, I, I, P, I, P],
     "vpt_linear_wgrad": [P, L, P, L, P, L, P, L, I, I, I, I, P, I, I, P],
+    "vpt_linear_wgrad_rr": [P, L, P, L, P, L, P, L, I, I, I, I, P, I, I, P, I, I, P, I, P],
     "vpt_linear_wgrad_workspace_bytes": [L, I, I, I],
     "vpt_gemm_swiglu_fwd": [P, L, P, L, P, P, L, P, L, I, I, I, P],
     "vpt_gemm_swiglu_bwd_workspace": [I, I, I],

@@ -282,15 +282,16 @@ class JiTEngine:
         ws = pool.get("wgrad_ws", (self._ws_elems(max(M, M2)),), F32)
         f, g = self.fin, self.g
 
-        def wgrad(dy, xin, out, bias=None):
-            """weight gradient, and with `bias` the bias gradient in the same GEMM (vpt_linear_wgrad)"""
+        def wgrad(dy, xin, out, bias=None, rows_sum=None):
+            """weight gradient, and with `bias` the bias gradient in the same GEMM (vpt_linear_wgrad); rows_sum = an
+            RMSNorm / QK-norm weight gradient's partial-row sum riding its reduce launch (vpt_linear_wgrad_rr)"""
             Mr, N = dy.shape
             K = xin.shape[1]
             s = ops.wgrad_splits(N, K, Mr)
             while s > 1 and ops.linear_wgrad_workspace_bytes(Mr, N, K, s) > ws.numel() * 4:
                 s -= 1
             ops.linear_wgrad(dy, xin, out.view(N, K), accumulate=acc, splits=s, workspace=ws,
-                             bias_out=None if bias is None else bias.view(-1))
+                             bias_out=None if bias is None else bias.view(-1), rows_sum=rows_sum)
 
         # --- final layer
         f3, fh, f12, xnf, xf = (pool.get(n, s) for n, s in (("f3", (M2, D)), ("fh", (M2, F)), ("f12", (M2, 2 * F)),
@@ -346,9 +347,8 @@ class JiTEngine:
             dxn2 = ops.linear_dgrad(dx12, w["pw12"], out=pool.get("d_b", (M, D)))
             dxm, part = ops.rmsnorm_bwd(dxn2, xm, rstd2, w["pn2"], dres=dx, dx=pool.get("dx_b", (M, D)),
                                         dw_part=pool.get("rms_part", (ops.rmsnorm_bwd_blocks(max(M, M2)), D), F32))
-            ops.reduce_rows(part[:ops.rmsnorm_bwd_blocks(M)], w["gn2"], acc)
-            # attention
-            wgrad(dxm, o, w["gwo"], w["gbo"])
+            # attention (norm2's weight gradient: its partial rows summed by the o-projection wgrad's reduce launch)
+            wgrad(dxm, o, w["gwo"], w["gbo"], rows_sum=(part[:ops.rmsnorm_bwd_blocks(M)], w["gn2"], acc))
             do = ops.linear_dgrad(dxm, w["pwo"], out=pool.get("d_o", (M, D)))
             a5 = (ops._t4(qk, B, rows, Hh, 0), ops._t4(qk, B, rows, Hh, D), ops._t4(qkv, B, rows, Hh, 2 * D),
                   ops._t4(o, B, rows, Hh, 0), ops._t4(do, B, rows, Hh, 0), lse, delta, st["kbias"])
@@ -359,7 +359,7 @@ class JiTEngine:
                                     w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, ops._t4(dqkv, B, rows, Hh, 0),
                                     ops._t4(dqkv, B, rows, Hh, D), qk_dw, ops._t4(dqkv, B, rows, Hh, 2 * D),
                                     B, Hh, rows, n_i, n_pre, scale)
-                ops.reduce_rows(qk_dw[:ops.attn_bwd_dw_rows(B, Hh, n_i)], w["gqk_norm"], acc)
+                qk_job = (qk_dw[:ops.attn_bwd_dw_rows(B, Hh, n_i)], w["gqk_norm"], acc)
             else:
                 dqk = pool.get("d_qk", (M, 2 * D))
                 if n_i < rows:
@@ -368,8 +368,8 @@ class JiTEngine:
                              ops._t4(dqkv, B, rows, Hh, 2 * D), B, Hh, rows, n_i, n_pre, scale)
                 qpart = ops.qknorm_rope_bwd(dqk, qkv, w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, rows, dqkv,
                                             dw_part=pool.get("qk_part", (ops.qknorm_rope_blocks(M), 128), F32))
-                ops.reduce_rows(qpart[:ops.qknorm_rope_blocks(M)], w["gqk_norm"], acc)
-            wgrad(dqkv, xn1, w["gwqkv"], w["gbqkv"])
+                qk_job = (qpart[:ops.qknorm_rope_blocks(M)], w["gqk_norm"], acc)
+            wgrad(dqkv, xn1, w["gwqkv"], w["gbqkv"], rows_sum=qk_job)
             dxn1 = ops.linear_dgrad(dqkv, w["pwqkv"], out=pool.get("d_b", (M, D)))
             dx_new, part = ops.rmsnorm_bwd(dxn1, x_in, rstd1, w["pn1"], dres=dxm, dx=pool.get("dx_a", (M, D)),
                                            dw_part=pool.get("rms_part", (ops.rmsnorm_bwd_blocks(max(M, M2)), D), F32))

@@ -310,9 +310,12 @@ def linear_wgrad_workspace_bytes(M: int, N: int, K: int, splits: int) -> int:
     return int(call("vpt_linear_wgrad_workspace_bytes", M, N, K, splits))
 
 
-def linear_wgrad(dy, x, out, accumulate=False, splits=1, workspace=None, bias_out=None, geometry=0, ring_grid=0):
+def linear_wgrad(dy, x, out, accumulate=False, splits=1, workspace=None, bias_out=None, geometry=0, ring_grid=0,
+                 rows_sum=None):
     """dW (=|+=) dy.T @ x in f32 (dy [M,N], x [M,K], out [N,K]) — nn.Linear weight gradient — and, with
-    bias_out [N] f32, the bias gradient (=|+=) column sums of dy in the same ring GEMM (vpt_linear_wgrad)."""
+    bias_out [N] f32, the bias gradient (=|+=) column sums of dy in the same ring GEMM (vpt_linear_wgrad).
+    rows_sum = (part [R, C] f32, out [C] f32, accumulate): an unrelated reduce_rows job done by extra blocks of the
+    weight gradient's reduce launch (vpt_linear_wgrad_rr) instead of a launch of its own."""
     M, N = dy.shape
     K = x.shape[1]
     _chk(dy, BF16, "dy")
@@ -326,10 +329,22 @@ def linear_wgrad(dy, x, out, accumulate=False, splits=1, workspace=None, bias_ou
     if workspace is None or workspace.numel() * workspace.element_size() < need:
         workspace = torch.empty((need + 3) // 4, dtype=F32, device=dy.device)
 
+    if rows_sum is not None:
+        rp, ro, racc = rows_sum
+        _chk(rp, F32, "rows_sum part")
+        _chk(ro, F32, "rows_sum out")
+        if not rp.is_contiguous() or rp.dim() != 2 or ro.numel() != rp.shape[1] or not ro.is_contiguous():
+            raise ValueError("rows_sum: part [R, C] and out [C], contiguous f32")
+
     def run():
-        call("vpt_linear_wgrad", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(), out.stride(0),
-             _p(bias_out), M, N, K, int(accumulate), splits, workspace.data_ptr(), int(geometry), int(ring_grid),
-             stream())
+        if rows_sum is None:
+            call("vpt_linear_wgrad", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(),
+                 out.stride(0), _p(bias_out), M, N, K, int(accumulate), splits, workspace.data_ptr(), int(geometry),
+                 int(ring_grid), stream())
+        else:
+            call("vpt_linear_wgrad_rr", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(),
+                 out.stride(0), _p(bias_out), M, N, K, int(accumulate), splits, workspace.data_ptr(), int(geometry),
+                 int(ring_grid), rp.data_ptr(), rp.shape[0], rp.shape[1], ro.data_ptr(), int(racc), stream())
     pr = PROBES.get("gemm")
     if pr is None:
         run()
