@@ -42,6 +42,10 @@ int vpt_attn_set_fused_workspace(void* ws);
 /* Backward kernel pair: 1 = 64 rows per wave (production default), 0 = the 32-row pair (A/B). */
 int vpt_attn_set_rows64(int on);
 int vpt_attn_set_bwd_stages(int n);
+/* Attention forward / backward block order: 1 = XCD-contiguous (a (batch, head)'s blocks on one XCD), 0 = linear. */
+int vpt_attn_set_xcd_order(int on);
+/* QK-norm attention forward: S^T chain with its K fragments read before the MFMAs (1) or hipcc's order (0). */
+int vpt_attn_set_fwd_order(int on);
 int vpt_gemm_set_swb_one_group(int on);
 /* NF4 GEMM timing ablations (WRONG results): 0 off, 1 = no dequant, 2 = no NF4 code loads / dequant. */
 int vpt_gemm_set_nf4_ablation(int a);

@@ -19,7 +19,14 @@ from vpt import ops  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--xcd", type=int, default=None, help="block order (diagnostic library): 1 XCD-contiguous, 0 linear")
+    ap.add_argument("--only", default=None, help="run only the fwd_qknorm and plain bwd launches")
     args = ap.parse_args()
+    if args.xcd is not None:
+        from vpt import _lib
+        if not _lib.DIAG:
+            raise SystemExit("--xcd needs the diagnostic library (VPT_DIAG=1)")
+        _lib.lib.vpt_attn_set_xcd_order(args.xcd)
     dev = torch.device("cuda", 0)
     B, H, n, nd = 8, 12, 4170, 4106
     D = 64 * H
@@ -42,14 +49,14 @@ def main():
     part = torch.empty(ops.attn_bwd_dw_rows(B, H, n), 128, device=dev)
     q4, k4, v4 = ops._t4(qk, B, n, H, 0), ops._t4(qk, B, n, H, D), ops._t4(qkv, B, n, H, 2 * D)
     o4, do4 = ops._t4(o, B, n, H, 0), ops._t4(do, B, n, H, 0)
-    for _ in range(args.iters):
+    for _ in range(0 if args.only else args.iters):
         ops.attn_fwd(q4, k4, v4, o4, lse, kb, B, H, n, n, nd)
     for _ in range(args.iters):
         ops.attn_fwd_qknorm(q4, k4, v4, o4, lse, kb, wq, wk, B, H, n, n, nd)
     for _ in range(args.iters):
         ops.attn_bwd(q4, k4, v4, o4, do4, lse, delta, kb, ops._t4(dqk, B, n, H, 0), ops._t4(dqk, B, n, H, D),
                      ops._t4(dqkv, B, n, H, 2 * D), B, H, n, n, nd)
-    for _ in range(args.iters):
+    for _ in range(0 if args.only else args.iters):
         ops.attn_bwd_qknorm(q4, k4, v4, o4, do4, lse, delta, kb, ops._t4(qkv, B, n, H, 0), ops._t4(qkv, B, n, H, D),
                             wq, wk, cos, sin, ops._t4(dqkv, B, n, H, 0), ops._t4(dqkv, B, n, H, D), part,
                             ops._t4(dqkv, B, n, H, 2 * D), B, H, n, n, nd)

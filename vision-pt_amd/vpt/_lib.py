@@ -127,6 +127,8 @@ DIAG_SIGNATURES: dict[str, list] = {
     "vpt_attn_set_fused_workspace": [P],
     "vpt_attn_set_rows64": [I],
     "vpt_attn_set_bwd_stages": [I],
+    "vpt_attn_set_xcd_order": [I],
+    "vpt_attn_set_fwd_order": [I],
     "vpt_gemm_set_swb_one_group": [I],
     "vpt_gemm_set_nf4_ablation": [I],
 }
