@@ -63,14 +63,16 @@ int g_variant = 0;  // backward kernel variant (vpt_attn_set_variant; 1, 2 = tim
 int g_waves = 4;    // waves per block (vpt_attn_set_variant 3 -> 8-wave blocks, A/B only)
 float g_tau = kTau; // forward lazy-rescale threshold (vpt_attn_set_rescale_threshold)
 int g_bwd_nst = 2;  // backward LDS ring stages (vpt_attn_set_bwd_stages, A/B)
-int g_fwd_ord = 0;  // forward S^T chain with its K fragments read first (vpt_attn_set_fwd_order, A/B)
+int g_fwd_ord = 1;  // forward S^T chain with its K fragments read first (vpt_attn_set_fwd_order, A/B)
 int g_xcd = 1;      // block order of the forward / backward grids (vpt_attn_set_xcd_order, A/B)
 int g_rows64 = 0;   // backward variants (vpt_attn_set_rows64 bit mask, A/B): 1 = 64-key dK/dV, 2 = 64-query dQ
                     // at 2 waves / SIMD, 4 = 64-query dQ at 1 wave / SIMD; 0 = the 32-row pair
 #else
 constexpr int g_variant = 0, g_waves = 4;
 constexpr float g_tau = kTau;
-constexpr int g_xcd = 1, g_fwd_ord = 0;  // XCD-contiguous block order (r04s: -1.1 % fwd, -1.8 % bwd, 4x less HBM traffic)
+// XCD-contiguous block order (r04s: -1.1 % fwd, -1.8 % bwd, 4x less HBM traffic; +0.38 % per C3 step, r04t) and the
+// forward's S^T chain with its K fragments read first (+0.32 % per C3 step, r04t)
+constexpr int g_xcd = 1, g_fwd_ord = 1;
 #endif
 
 // Reductions over the lane pair (l, l^32) with v_permlane32_swap (VALU, no LDS round trip): the two
@@ -990,7 +992,10 @@ extern "C" int vpt_attn_fwd(const void* q, long q_sb, long q_sh, long q_sr,
   g.scale = scale; g.scale_log2 = scale * 1.4426950408889634f;
   g.tau = g_tau;
   g.kb0 = g.n_dense / 64 * 64;
-  if (g_waves != 8)
+  if (g_waves != 8 && g_fwd_ord)
+    hipLaunchKernelGGL((attn_fwd_kernel<4, false, true>), dim3((n + 127) / 128, H, B), dim3(256), key_bias_lds_bytes(g),
+                       (hipStream_t)stream, g);
+  else if (g_waves != 8)
     hipLaunchKernelGGL((attn_fwd_kernel<4>), dim3((n + 127) / 128, H, B), dim3(256), key_bias_lds_bytes(g),
                        (hipStream_t)stream, g);
   else
