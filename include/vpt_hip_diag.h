@@ -46,6 +46,8 @@ int vpt_attn_set_bwd_stages(int n);
 int vpt_attn_set_xcd_order(int on);
 /* QK-norm attention forward: S^T chain with its K fragments read before the MFMAs (1) or hipcc's order (0). */
 int vpt_attn_set_fwd_order(int on);
+/* Attention backward: transposed-fragment prefetch in the dK/dV (bit 1) / dQ (bit 2) products; 0 = production. */
+int vpt_attn_set_bwd_prefetch(int mask);
 int vpt_gemm_set_swb_one_group(int on);
 /* NF4 GEMM timing ablations (WRONG results): 0 off, 1 = no dequant, 2 = no NF4 code loads / dequant. */
 int vpt_gemm_set_nf4_ablation(int a);

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--setter", default="vpt_attn_set_xcd_order")
+    ap.add_argument("--value", type=int, default=1, help="the B value (A = 0)")
     args = ap.parse_args()
     if not _lib.DIAG:
         raise SystemExit("needs the diagnostic library (VPT_DIAG=1)")
@@ -60,7 +61,7 @@ def main():
 
     outs = {}
     for x in (0, 1):
-        setter(x)
+        setter(x * args.value)
         fwd()
         bwd()
         torch.cuda.synchronize()
@@ -70,7 +71,7 @@ def main():
     res = {f"{k}{x}": [] for k in ("fwd", "bwd") for x in (0, 1)}
     for r in range(args.rounds):
         for x in ((0, 1) if r % 2 == 0 else (1, 0)):
-            setter(x)
+            setter(x * args.value)
             for name, fn in (("fwd", fwd), ("bwd", bwd)):
                 fn()
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.iters + 1)]
@@ -82,7 +83,7 @@ def main():
                 res[f"{name}{x}"].append(statistics.median(ev[i].elapsed_time(ev[i + 1]) for i in range(args.iters)))
     med = {k: round(statistics.median(v), 4) for k, v in res.items()}
     setter(0)
-    print(json.dumps({"setter": args.setter, "bitwise_equal": equal, "median_ms": med,
+    print(json.dumps({"setter": args.setter, "value": args.value, "bitwise_equal": equal, "median_ms": med,
                       "fwd_1_vs_0": round(med["fwd1"] / med["fwd0"], 4),
                       "bwd_1_vs_0": round(med["bwd1"] / med["bwd0"], 4)}), flush=True)
 

@@ -64,6 +64,7 @@ int g_waves = 4;    // waves per block (vpt_attn_set_variant 3 -> 8-wave blocks,
 float g_tau = kTau; // forward lazy-rescale threshold (vpt_attn_set_rescale_threshold)
 int g_bwd_nst = 2;  // backward LDS ring stages (vpt_attn_set_bwd_stages, A/B)
 int g_fwd_ord = 1;  // forward S^T chain with its K fragments read first (vpt_attn_set_fwd_order, A/B)
+int g_bwd_pf = 0;   // backward transposed-fragment prefetch (vpt_attn_set_bwd_prefetch bit mask, A/B)
 int g_xcd = 1;      // block order of the forward / backward grids (vpt_attn_set_xcd_order, A/B)
 int g_rows64 = 0;   // backward variants (vpt_attn_set_rows64 bit mask, A/B): 1 = 64-key dK/dV, 2 = 64-query dQ
                     // at 2 waves / SIMD, 4 = 64-query dQ at 1 wave / SIMD; 0 = the 32-row pair
@@ -637,7 +638,7 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
     const int nxt = NST == 2 ? (cur ^ 1) : (t + 1) % NST;
     const char* lq = lds[cur][0];
     const char* ld = lds[cur][1];
-    if (ABL == 8) {
+    if (ABL == 8 || ABL == 9) {
       // Explicitly ordered body: the row fragments and row constants of query block qb+1 are read while
       // block qb's S / dP chains run (s_setprio 1 around every MFMA group), P and dS are packed to bf16
       // as soon as they exist, and sched_barriers keep hipcc from sinking the reads back to their uses.
@@ -674,6 +675,34 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
         for (int s2 = 0; s2 < 2; ++s2) { pp[qb][s2] = pack_acc(P, s2); pd[qb][s2] = pack_acc(dS, s2); }
       }
       __builtin_amdgcn_sched_barrier(0);
+      if (ABL == 9) {
+        // the transposed Q / dO fragments of step st + 1 are read before step st's four MFMAs (two register sets), so
+        // no dV / dK MFMA waits on a read issued right before it
+        bf16x8 tv[2][2], tq[2][2];
+        auto rd = [&](int st) {
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            tv[st & 1][db] = frag_tr(ld, db, st, lane);
+            tq[st & 1][db] = frag_tr(lq, db, st, lane);
+          }
+        };
+        rd(0);
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          if (st + 1 < 4) rd(st + 1);
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            dvT[db] = mfma32(tv[st & 1][db], pp[st >> 1][st & 1], dvT[db]);
+            dkT[db] = mfma32(tq[st & 1][db], pd[st >> 1][st & 1], dkT[db]);
+          }
+          __builtin_amdgcn_s_setprio(0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (more) settle(nxt, (t + 1) * 64, NST == 3 && t + 2 < nt);
+        continue;
+      }
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb)
 #pragma unroll
@@ -891,16 +920,38 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
 #pragma unroll
       for (int i = 0; i < 16; ++i) dS[kb][i] = __builtin_amdgcn_exp2f(s[i]) * dp[i];
     }
+    if (ABL == 9) {
+      // the transposed K fragments of step st + 1 are read before step st's two MFMAs (two register sets)
+      bf16x8 tk[2][2], pd[2][2];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 pd = pack_acc(dS[kb], s2);
+        for (int s2 = 0; s2 < 2; ++s2) pd[kb][s2] = pack_acc(dS[kb], s2);
 #pragma unroll
-        for (int db = 0; db < 2; ++db)
-          dqT[db] = mfma32(ABL == 2 ? frag_rows(lk, 32 * db, 2 * kb + s2, lane) : frag_tr(lk, db, 2 * kb + s2, lane), pd,
-                           dqT[db]);
+      for (int db = 0; db < 2; ++db) tk[0][db] = frag_tr(lk, db, 0, lane);
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        if (st + 1 < 4) {
+#pragma unroll
+          for (int db = 0; db < 2; ++db) tk[(st + 1) & 1][db] = frag_tr(lk, db, st + 1, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int db = 0; db < 2; ++db) dqT[db] = mfma32(tk[st & 1][db], pd[st >> 1][st & 1], dqT[db]);
+        __builtin_amdgcn_sched_barrier(0);
       }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 pd = pack_acc(dS[kb], s2);
+#pragma unroll
+          for (int db = 0; db < 2; ++db)
+            dqT[db] = mfma32(ABL == 2 ? frag_rows(lk, 32 * db, 2 * kb + s2, lane) : frag_tr(lk, db, 2 * kb + s2, lane), pd,
+                             dqT[db]);
+        }
+    }
     if (younger) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1175,6 +1226,17 @@ int attn_bwd_impl(AttnArgs& g, int B, int H, int n, int nk, hipStream_t s) {
   }
 #endif
 #ifdef VPT_DIAG
+  if (g_bwd_pf) {  // A/B: transposed-fragment prefetch in the dK/dV (bit 1) / dQ (bit 2) products
+    const dim3 grid((nkb + nqb) * H * B);
+    if (g_bwd_pf == 1)
+      hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, 9>), grid, dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
+    else if (g_bwd_pf == 2)
+      hipLaunchKernelGGL((attn_bwd_kernel<9, 8>), grid, dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
+    else
+      hipLaunchKernelGGL((attn_bwd_kernel<9, 9>), grid, dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
+    VPT_LAUNCH_CHECK();
+    return VPT_OK;
+  }
   if (g_bwd_nst == 3) {
     hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, 8, 0, 3>), dim3((nkb + nqb) * H * B), dim3(256), key_bias_lds_bytes(g),
                        s, g, nkb, nqb, B);

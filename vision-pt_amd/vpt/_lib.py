@@ -129,6 +129,7 @@ DIAG_SIGNATURES: dict[str, list] = {
     "vpt_attn_set_bwd_stages": [I],
     "vpt_attn_set_xcd_order": [I],
     "vpt_attn_set_fwd_order": [I],
+    "vpt_attn_set_bwd_prefetch": [I],
     "vpt_gemm_set_swb_one_group": [I],
     "vpt_gemm_set_nf4_ablation": [I],
 }
