@@ -51,6 +51,9 @@ int vpt_attn_set_bwd_prefetch(int mask);
 int vpt_gemm_set_swb_one_group(int on);
 /* NF4 GEMM timing ablations (WRONG results): 0 off, 1 = no dequant, 2 = no NF4 code loads / dequant. */
 int vpt_gemm_set_nf4_ablation(int a);
+/* Co-running-kernel probe: `blocks` one-wave workgroups holding a CU each (lds_bytes of LDS) for `ticks` of the 100-MHz
+ * clock (sink: a device float[64], never written in practice). */
+int vpt_diag_occupy(int blocks, long ticks, int lds_bytes, float* sink, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1617,6 +1617,29 @@ extern "C" int vpt_gemm_set_debug(unsigned long long* buf) {
   g_dbg = buf;
   return VPT_OK;
 }
+
+// Co-running-kernel probe: `blocks` one-wave workgroups that hold a CU each (dynamic LDS) for `ticks` of the 100-MHz
+// constant clock and exit -- a stand-in for the RCCL / side-stream kernels that share the chip with a persistent GEMM.
+namespace {
+__global__ void occupy_kernel(long ticks, float* sink) {
+  extern __shared__ float hold[];
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  float acc = 0.f;
+  while ((long)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) {
+    __builtin_amdgcn_s_sleep(4);
+    acc += 1.f;
+  }
+  if (acc < 0.f) { hold[threadIdx.x] = acc; sink[threadIdx.x] = hold[threadIdx.x]; }  // never taken; keeps the LDS
+}
+}  // namespace
+
+extern "C" int vpt_diag_occupy(int blocks, long ticks, int lds_bytes, float* sink, void* stream) {
+  VPT_CHECK_ARG(blocks > 0 && blocks <= 4096 && ticks > 0 && ticks <= 1000000 && lds_bytes >= 0 && lds_bytes <= 163840,
+                "vpt_diag_occupy: blocks 1..4096, ticks 1..1e6 (10 ms), lds <= 160 KB");
+  hipLaunchKernelGGL(occupy_kernel, dim3(blocks), dim3(64), lds_bytes, (hipStream_t)stream, ticks, sink);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
 #endif  // VPT_DIAG
 
 extern "C" long vpt_gemm_workspace_bytes(int M, int N, int K, int splits) {

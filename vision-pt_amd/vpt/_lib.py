@@ -132,6 +132,7 @@ DIAG_SIGNATURES: dict[str, list] = {
     "vpt_attn_set_bwd_prefetch": [I],
     "vpt_gemm_set_swb_one_group": [I],
     "vpt_gemm_set_nf4_ablation": [I],
+    "vpt_diag_occupy": [I, L, I, P, P],
 }
 _RESTYPES = {
     "vpt_lora_wgrad_workspace": C.c_long,
