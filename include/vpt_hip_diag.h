@@ -24,7 +24,8 @@ int vpt_gemm_set_geometry(int geo);
 /* u64 buffer receiving per-wave K-step segment cycle sums (2566: [256][8][8]) or realtime stamps
  * (2567: [grid][4][4]); nullptr disables. */
 int vpt_gemm_set_debug(unsigned long long* buf);
-/* Persistent ring grid override (0 = per-call / default). */
+/* Ring grid override for every ring GEMM (0 = per-call / default: one block per item; 256 = the persistent walk with
+ * one block per CU). */
 int vpt_gemm_set_ring_grid(int blocks);
 /* Ring epilogue stagger in 10-ns ticks: half the blocks start that much later (0 = off, production). */
 int vpt_gemm_set_stagger(int ticks);

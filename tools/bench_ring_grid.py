@@ -1,5 +1,5 @@
-"""bench.py under the diagnostic library with the ring GEMMs' grid forced (vpt_gemm_set_ring_grid): 0 = persistent
-(one block per CU walking items), 65536 = one block per item -- for same-box A/B of the step with the side-stream
+"""bench.py under the diagnostic library with the ring GEMMs' grid forced (vpt_gemm_set_ring_grid): 256 = persistent
+(one block per CU walking items), 0 = the default, one block per item -- for same-box A/B of the step with the side-stream
 optimizer overlap on (--overlap on), where the optimizer's kernels share the chip with the backward's GEMMs.
 
   python tools/bench_ring_grid.py RING_GRID [bench.py args...]

@@ -41,7 +41,7 @@ def main():
     main_s, side = torch.cuda.current_stream(), torch.cuda.Stream()
     ticks = int(args.T * 100)
     res = {}
-    for mode, rg in (("persistent", 0), ("per_item", 65536)):
+    for mode, rg in (("persistent", 256), ("per_item", 0)):
         lib.vpt_gemm_set_ring_grid(rg)
         for name, fn in gemms.items():
             for k in (0, 8, 32, 128):

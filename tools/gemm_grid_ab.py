@@ -73,7 +73,7 @@ def main():
     res = {(k, m): [] for k in calls for m in (0, 1)}
     for rd in range(args.rounds):
         for m in ((0, 1) if rd % 2 == 0 else (1, 0)):
-            _lib.lib.vpt_gemm_set_ring_grid(65536 if m else 0)
+            _lib.lib.vpt_gemm_set_ring_grid(0 if m else 256)
             for k, fn in calls.items():
                 res[(k, m)].append(timeit(fn))
     _lib.lib.vpt_gemm_set_ring_grid(0)

@@ -383,7 +383,14 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_bf16_kernel(GemmArgs g
 // (finite, in-bounds) addresses and its k >= K lanes of the A fragments are zeroed in registers.
 constexpr int RBK = 32;
 constexpr int RSTAGES = 4;
-constexpr int kRingGrid = 256;  // persistent ring grid: one block per CU (GemmArgs::ring_grid overrides)
+// Default ring grid (GemmArgs::ring_grid = 0): one block per work item, the dispatcher placing each block wherever a CU
+// is free. Against the persistent walk (256 blocks, one per CU, items at a stride of 256, the next item's first tiles
+// DMA'd under the epilogue) it is level at N = 1 (r04za: +0.4 % over the 12 GEMMs of a block, -0.08 % per C3 step),
+// +0.3 % per step with the optimizer on a side stream (r04zc), and it tolerates kernels beside it: with 8 CUs held for
+// 150 us by another kernel, the persistent q|k|v forward took 204 us (its 8 displaced blocks started 150 us late)
+// against 156 us (r04za) -- RCCL's all-reduce channels hold CUs that way during the N > 1 backward. ring_grid > 0
+// keeps the persistent walk with that many blocks.
+constexpr int kRingGrid = 256;  // the persistent walk: one block per CU (the 4-wave diagnostic ring's default)
 
 __device__ __forceinline__ int kmaj32_off(int row, int chunk) {  // [R][32] bf16, 64-B rows
   return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4);
@@ -1194,8 +1201,9 @@ template <bool AK, bool BK_, bool PP, int ABL = 0, bool DMAC = false, bool STAMP
 int launch_ring(const GemmArgs& g, int splits, hipStream_t s) {
   constexpr int LDS = RSTAGES * 2 * 256 * RBK * 2;  // the epilogue stages through ring stage 3
   const int items = ((g.M + 255) / 256) * ((g.N + 255) / 256) * splits;
-  const int rg = g.ring_grid > 0 ? g.ring_grid : kRingGrid;
-  const int grid = items < rg ? items : rg;
+  // the stamped / timeline diagnostic builds size their buffers for the persistent 256-block walk
+  const int rg = g.ring_grid > 0 ? g.ring_grid : (STAMP || TL) ? 256 : items;
+  const int grid = rg < items ? rg : items;
   const int epi = SW ? EPI_PLAIN : epi_mode(g);
   GemmArgs ga = g;
   ga.stagger = ring_stagger();
@@ -1593,7 +1601,8 @@ extern "C" int vpt_gemm_set_geometry(int geo) {
   return VPT_OK;
 }
 
-// Persistent ring grid size (blocks); 0 restores one block per CU (256).
+// Ring grid size (blocks) for every ring GEMM: 0 restores the default (one block per item); 256 = the persistent walk
+// with one block per CU.
 extern "C" int vpt_gemm_set_ring_grid(int blocks) {
   VPT_CHECK_ARG(blocks >= 0 && blocks <= 65536, "vpt_gemm_set_ring_grid: 0..65536");
   g_ring_grid_override = blocks;
