@@ -638,7 +638,7 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
     const int nxt = NST == 2 ? (cur ^ 1) : (t + 1) % NST;
     const char* lq = lds[cur][0];
     const char* ld = lds[cur][1];
-    if (ABL == 8 || ABL == 9) {
+    if (ABL == 8 || ABL == 9 || ABL == 10) {
       // Explicitly ordered body: the row fragments and row constants of query block qb+1 are read while
       // block qb's S / dP chains run (s_setprio 1 around every MFMA group), P and dS are packed to bf16
       // as soon as they exist, and sched_barriers keep hipcc from sinking the reads back to their uses.
@@ -650,13 +650,13 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
       for (int qb = 0; qb < 2; ++qb) {
         floatx16 s = cs, dp = cd;
         __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
+        if (ABL != 10) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           s = mfma32(qa[ks], kf[ks], s);
           dp = mfma32(da[ks], vf[ks], dp);
         }
-        __builtin_amdgcn_s_setprio(0);
+        if (ABL != 10) __builtin_amdgcn_s_setprio(0);
         if (qb == 0) {
           cs = rows16(lstat[cur][0], 32, h);
           cd = rows16(lstat[cur][1], 32, h);
@@ -691,13 +691,13 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
         for (int st = 0; st < 4; ++st) {
           if (st + 1 < 4) rd(st + 1);
           __builtin_amdgcn_sched_barrier(0);
-          __builtin_amdgcn_s_setprio(1);
+          if (ABL != 10) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int db = 0; db < 2; ++db) {
             dvT[db] = mfma32(tv[st & 1][db], pp[st >> 1][st & 1], dvT[db]);
             dkT[db] = mfma32(tq[st & 1][db], pd[st >> 1][st & 1], dkT[db]);
           }
-          __builtin_amdgcn_s_setprio(0);
+          if (ABL != 10) __builtin_amdgcn_s_setprio(0);
           __builtin_amdgcn_sched_barrier(0);
         }
         if (more) settle(nxt, (t + 1) * 64, NST == 3 && t + 2 < nt);
@@ -710,13 +710,13 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
           bf16x8 tv[2], tq[2];
 #pragma unroll
           for (int db = 0; db < 2; ++db) { tv[db] = frag_tr(ld, db, 2 * qb + s2, lane); tq[db] = frag_tr(lq, db, 2 * qb + s2, lane); }
-          __builtin_amdgcn_s_setprio(1);
+          if (ABL != 10) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int db = 0; db < 2; ++db) {
             dvT[db] = mfma32(tv[db], pp[qb][s2], dvT[db]);
             dkT[db] = mfma32(tq[db], pd[qb][s2], dkT[db]);
           }
-          __builtin_amdgcn_s_setprio(0);
+          if (ABL != 10) __builtin_amdgcn_s_setprio(0);
         }
       if (more) settle(nxt, (t + 1) * 64, NST == 3 && t + 2 < nt);
       continue;
@@ -1228,7 +1228,9 @@ int attn_bwd_impl(AttnArgs& g, int B, int H, int n, int nk, hipStream_t s) {
 #ifdef VPT_DIAG
   if (g_bwd_pf) {  // A/B: transposed-fragment prefetch in the dK/dV (bit 1) / dQ (bit 2) products
     const dim3 grid((nkb + nqb) * H * B);
-    if (g_bwd_pf == 1)
+    if (g_bwd_pf == 4)  // the ordered dK/dV body without its s_setprio around the MFMA groups
+      hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, 10>), grid, dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
+    else if (g_bwd_pf == 1)
       hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, 9>), grid, dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
     else if (g_bwd_pf == 2)
       hipLaunchKernelGGL((attn_bwd_kernel<9, 8>), grid, dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
