@@ -1001,6 +1001,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs g, int nkb, i
   else dq_body<DQ, 4, NST>(g, bx, r % g.H, r / g.H, lds, kbl, &lstat[0][0][0]);
 }
 constexpr int kDqBody = 0;  // production dQ body (0 = compiler-scheduled, 8 = explicitly ordered)
+// production dK/dV body: the explicitly ordered body without s_setprio around its MFMA groups (10); with them (8) the
+// other wave on the SIMD waits out each prioritised MFMA group before its exp / pack phase can issue: kernel -1.1 %,
+// +0.18 % per C3 step without (same-box A/B r04zg, bitwise equal)
+constexpr int kDkdvBody = 10;
 
 // Dynamic LDS of the key-bias array (fill_key_bias); n <= 32768 keeps it within 128 KB.
 size_t key_bias_lds_bytes(const AttnArgs& g) { return (size_t)((g.nk + 63) / 64 * 64 - g.kb0) * sizeof(float); }
@@ -1228,8 +1232,8 @@ int attn_bwd_impl(AttnArgs& g, int B, int H, int n, int nk, hipStream_t s) {
 #ifdef VPT_DIAG
   if (g_bwd_pf) {  // A/B: transposed-fragment prefetch in the dK/dV (bit 1) / dQ (bit 2) products
     const dim3 grid((nkb + nqb) * H * B);
-    if (g_bwd_pf == 4)  // the ordered dK/dV body without its s_setprio around the MFMA groups
-      hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, 10>), grid, dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
+    if (g_bwd_pf == 4)  // the ordered dK/dV body WITH s_setprio around its MFMA groups (the previous production body)
+      hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, 8>), grid, dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
     else if (g_bwd_pf == 1)
       hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, 9>), grid, dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
     else if (g_bwd_pf == 2)
@@ -1246,7 +1250,7 @@ int attn_bwd_impl(AttnArgs& g, int B, int H, int n, int nk, hipStream_t s) {
     return VPT_OK;
   }
 #endif
-  hipLaunchKernelGGL((attn_bwd_kernel<kDqBody>), dim3((nkb + nqb) * H * B), dim3(256), key_bias_lds_bytes(g), s, g, nkb,
+  hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, kDkdvBody>), dim3((nkb + nqb) * H * B), dim3(256), key_bias_lds_bytes(g), s, g, nkb,
                      nqb, B);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
