@@ -40,6 +40,7 @@ def main():
             "ATTN_PF_KV": lambda on: _lib.lib.vpt_attn_set_bwd_prefetch(1 if on else 0),
             "ATTN_PF_Q": lambda on: _lib.lib.vpt_attn_set_bwd_prefetch(2 if on else 0),
             "ATTN_PF": lambda on: _lib.lib.vpt_attn_set_bwd_prefetch(3 if on else 0),
+            "ATTN_DQ_ORD_NOPRIO": lambda on: _lib.lib.vpt_attn_set_bwd_prefetch(5 if on else 0),
             "ATTN_PRIO": lambda on: _lib.lib.vpt_attn_set_bwd_prefetch(4 if on else 0),
             "RING_PER_ITEM": lambda on: _lib.lib.vpt_gemm_set_ring_grid(0 if on else 256)}
     for k in knobs:

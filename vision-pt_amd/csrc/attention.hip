@@ -839,7 +839,7 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
     const char* lk = lds[cur][0];
     const char* lv = lds[cur][1];
     const bool dense = kv0 + 64 <= g.n_dense;
-    if (ABL == 8) {
+    if (ABL == 8 || ABL == 10) {
       // Explicitly ordered body: both key halves' S^T / dP^T chains back to back (the second half's row fragments
       // read under the first chain), then the first half's exp / dS while the second chain drains, the dQ
       // products of the first half, the second half's exp / dS, its dQ products -- so no exp waits on the
@@ -850,24 +850,24 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
       floatx16 sc[2], dp[2];
       sc[0] = nlse; dp[0] = ndel;
       __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
+      if (ABL != 10) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         sc[0] = mfma32(ka[ks], qf[ks], sc[0]);
         dp[0] = mfma32(va[ks], df[ks], dp[0]);
       }
-      __builtin_amdgcn_s_setprio(0);
+      if (ABL != 10) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) { ka[ks] = frag_rows(lk, 32, ks, lane); va[ks] = frag_rows(lv, 32, ks, lane); }
       __builtin_amdgcn_sched_barrier(0);
       sc[1] = nlse; dp[1] = ndel;
-      __builtin_amdgcn_s_setprio(1);
+      if (ABL != 10) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         sc[1] = mfma32(ka[ks], qf[ks], sc[1]);
         dp[1] = mfma32(va[ks], df[ks], dp[1]);
       }
-      __builtin_amdgcn_s_setprio(0);
+      if (ABL != 10) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -889,10 +889,10 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
           bf16x8 tk[2];
 #pragma unroll
           for (int db = 0; db < 2; ++db) tk[db] = frag_tr(lk, db, 2 * kb + s2, lane);
-          __builtin_amdgcn_s_setprio(1);
+          if (ABL != 10) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int db = 0; db < 2; ++db) dqT[db] = mfma32(tk[db], pd[kb][s2], dqT[db]);
-          __builtin_amdgcn_s_setprio(0);
+          if (ABL != 10) __builtin_amdgcn_s_setprio(0);
         }
       }
       if (younger) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -1234,6 +1234,8 @@ int attn_bwd_impl(AttnArgs& g, int B, int H, int n, int nk, hipStream_t s) {
     const dim3 grid((nkb + nqb) * H * B);
     if (g_bwd_pf == 4)  // the ordered dK/dV body WITH s_setprio around its MFMA groups (the previous production body)
       hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, 8>), grid, dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
+    else if (g_bwd_pf == 5)  // the explicitly ordered dQ body without s_setprio
+      hipLaunchKernelGGL((attn_bwd_kernel<10, kDkdvBody>), grid, dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
     else if (g_bwd_pf == 1)
       hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, 9>), grid, dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B);
     else if (g_bwd_pf == 2)
