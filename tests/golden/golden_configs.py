@@ -10,6 +10,12 @@ def micro_config() -> OracleConfig:
                         context_start_block=1)
 
 
+def micro_fuse_config() -> OracleConfig:
+    """micro_config with do_context_fuse=True (denoiser.py:1092-1113, config.py:46)."""
+    return OracleConfig(hidden_size=192, depth=3, num_heads=3, bottleneck_dim=32, context_dim=64,
+                        context_start_block=1, do_context_fuse=True)
+
+
 def c1_config() -> OracleConfig:
     """BASELINE config 1: JiT tiny (2 layers, d=256), context in both blocks."""
     return OracleConfig(hidden_size=256, depth=2, num_heads=4, bottleneck_dim=128, context_dim=256,

@@ -10,6 +10,8 @@ Fixtures:
                          2 x 64x48 images, 8 context tokens, one padded) — fp32 reference forward,
                          image- and velocity-target losses, full gradients of the small
                          parameters and (norm, sum, first 64) of every parameter gradient.
+  jit_micro_fuse.safetensors  the same with do_context_fuse=True (context tokens appended once at
+                         context_start_block and carried through the later blocks, denoiser.py:1087-1113).
   jit_c1.safetensors     BASELINE config 1 (D=256, 4 heads, depth 2, ctx_dim 256, context in both
                          blocks, 4 x 256^2): loss, output checksums, per-parameter grad norms.
   ops.safetensors        timestep embedding (t = 0..9999 subsample + fractional), RoPE tables of
@@ -62,7 +64,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference"
 sys.path.insert(0, ROOT)
 from oracle.jit_oracle import OracleConfig, make_weights  # noqa: E402
-from tests.golden.golden_configs import c1_config, make_batch, micro_config  # noqa: E402
+from tests.golden.golden_configs import c1_config, make_batch, micro_config, micro_fuse_config  # noqa: E402
 
 torch.set_num_threads(8)
 
@@ -117,6 +119,7 @@ def ref_config(R, oc: OracleConfig):
     return R.cfg.DenoiserConfig(
         patch_size=oc.patch_size, hidden_size=oc.hidden_size, depth=oc.depth, num_heads=oc.num_heads,
         bottleneck_dim=oc.bottleneck_dim, context_dim=oc.context_dim, context_start_block=oc.context_start_block,
+        do_context_fuse=oc.do_context_fuse,
         rope_axes_dims=oc.rope_axes_dims, rope_axes_lens=oc.rope_axes_lens, rope_zero_centered=oc.rope_zero_centered)
 
 
@@ -498,6 +501,25 @@ def bf16_error_fixture(R, meta):
         save_file(out, path, metadata=dict(meta, names=json.dumps(names)))
 
 
+def micro_fixture(R, meta, oc: OracleConfig, name: str):
+    """jit_micro (context appended before every block from context_start_block and stripped after it) and
+    jit_micro_fuse (do_context_fuse=True: appended once at context_start_block and carried to the end,
+    denoiser.py:1087-1113): both loss targets, the same weights and batch."""
+    V = 20
+    w = make_weights(oc, seed=1, n_classes=V)
+    batch = make_batch(oc, 2, 64, 48, 8, V, seed=2)
+    out = {k: v for k, v in batch.items()}
+    for lt in ("image", "velocity"):
+        loss, pred, z, grads = run_reference(R, oc, w, batch, lt)
+        out[f"{lt}/loss"] = loss.reshape(1)
+        out[f"{lt}/pred"] = pred
+        grad_summary(f"{lt}/", grads, out)
+    out["z"] = z
+    out["wsum"] = torch.stack([w[k].double().sum().float() for k in sorted(w)])
+    save_file({k: v.contiguous() for k, v in out.items()}, os.path.join(HERE, name + ".safetensors"),
+              metadata=dict(meta, do_context_fuse=str(oc.do_context_fuse)))
+
+
 def main():
     R = import_reference()
     meta = {"torch": torch.__version__, "threads": str(torch.get_num_threads()), "reference": REF}
@@ -524,25 +546,18 @@ def main():
         timestep_fixture(meta)
         print("timestep", os.path.getsize(os.path.join(HERE, "timestep.safetensors")))
         return
+    if len(sys.argv) > 1 and sys.argv[1] == "fuse":
+        micro_fixture(R, meta, micro_fuse_config(), "jit_micro_fuse")
+        print("jit_micro_fuse", os.path.getsize(os.path.join(HERE, "jit_micro_fuse.safetensors")))
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "sdxl":
         sdxl_block_fixture(meta)
         print("sdxl_block", os.path.getsize(os.path.join(HERE, "sdxl_block.safetensors")))
         return
 
     # ---------------- micro
-    oc = micro_config()
-    V = 20
-    w = make_weights(oc, seed=1, n_classes=V)
-    batch = make_batch(oc, 2, 64, 48, 8, V, seed=2)
-    out = {k: v for k, v in batch.items()}
-    for lt in ("image", "velocity"):
-        loss, pred, z, grads = run_reference(R, oc, w, batch, lt)
-        out[f"{lt}/loss"] = loss.reshape(1)
-        out[f"{lt}/pred"] = pred
-        grad_summary(f"{lt}/", grads, out)
-    out["z"] = z
-    out["wsum"] = torch.stack([w[k].double().sum().float() for k in sorted(w)])
-    save_file({k: v.contiguous() for k, v in out.items()}, os.path.join(HERE, "jit_micro.safetensors"), metadata=meta)
+    micro_fixture(R, meta, micro_config(), "jit_micro")
+    micro_fixture(R, meta, micro_fuse_config(), "jit_micro_fuse")
 
     # ---------------- C1 tiny (BASELINE config 1)
     oc = c1_config()
@@ -611,7 +626,7 @@ def main():
     init_fixture(R, meta)
     sdxl_spatial_fixture(meta)
     saving_fixture(meta)
-    for f in ("jit_micro", "jit_c1", "ops", "sampler", "sdxl_block", "timestep", "init", "sdxl_spatial", "saving"):
+    for f in ("jit_micro", "jit_micro_fuse", "jit_c1", "ops", "sampler", "sdxl_block", "timestep", "init", "sdxl_spatial", "saving"):
         print(f, os.path.getsize(os.path.join(HERE, f + ".safetensors")))
 
 

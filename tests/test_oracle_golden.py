@@ -38,9 +38,17 @@ def _run_oracle(oc, weights, fx, loss_target):
     return loss.detach(), pred.detach(), grads
 
 
+@pytest.fixture(scope="module")
+def micro_fuse():
+    return load_file(os.path.join(GOLD, "jit_micro_fuse.safetensors"))
+
+
+@pytest.mark.parametrize("fuse", [False, True], ids=["strip", "fuse"])
 @pytest.mark.parametrize("target", ["image", "velocity"])
-def test_oracle_matches_reference_micro(micro, target):
-    oc = GC.micro_config()
+def test_oracle_matches_reference_micro(micro, micro_fuse, target, fuse):
+    """fuse: do_context_fuse=True (denoiser.py:1092-1113): context appended once, carried to the last block."""
+    oc = GC.micro_fuse_config() if fuse else GC.micro_config()
+    micro = micro_fuse if fuse else micro
     w = O.make_weights(oc, seed=1, n_classes=20)
     wsum = torch.stack([w[k].double().sum().float() for k in sorted(w)])
     assert torch.equal(wsum, micro["wsum"]), "weight generator drifted from the fixture"
@@ -53,6 +61,11 @@ def test_oracle_matches_reference_micro(micro, target):
         assert rel(g.reshape(-1)[:64], micro[f"{target}/ghead/{n}"]) < 1e-3 or gn < 1e-9, n
         if f"{target}/gfull/{n}" in micro:
             assert rel(g.reshape(-1), micro[f"{target}/gfull/{n}"]) < 1e-4, n
+
+
+def test_fuse_fixture_differs_from_strip(micro, micro_fuse):
+    """The two context modes give different outputs on the same weights and batch (the branch is exercised)."""
+    assert rel(micro_fuse["image/pred"], micro["image/pred"]) > 1e-3
 
 
 def test_oracle_matches_reference_c1():

@@ -1,10 +1,10 @@
-"""Same-process A/B of a diagnostic attention switch (VPT_DIAG=1) at the C3 shape (JiT-B/16, B=8, 1024^2: n = 4170
+"""Same-process A/B of a diagnostic attention switch (diagnostic library) at the C3 shape (JiT-B/16, B=8, 1024^2: n = 4170
 rows, 12 heads, QK-normed inputs): --setter vpt_attn_set_xcd_order (linear vs XCD-contiguous block order: a (batch,
 head)'s blocks on one XCD), vpt_attn_set_fwd_order (the forward's S^T chain with its K fragments read first). Forward
 (fixed reference) and backward launches timed with HIP events on the launching stream, values 0 and 1 interleaved over
 rounds (medians); outputs checked bitwise equal between the two.
 
-  VPT_DIAG=1 python tools/attn_ab.py --setter vpt_attn_set_xcd_order [--rounds 8] [--iters 10]
+  python tools/attn_ab.py --setter vpt_attn_set_xcd_order [--rounds 8] [--iters 10]
 """
 import argparse
 import json
@@ -27,8 +27,7 @@ def main():
     ap.add_argument("--setter", default="vpt_attn_set_xcd_order")
     ap.add_argument("--value", type=int, default=1, help="the B value (A = 0)")
     args = ap.parse_args()
-    if not _lib.DIAG:
-        raise SystemExit("needs the diagnostic library (VPT_DIAG=1)")
+    _lib.use_diag()
     setter = getattr(_lib.lib, args.setter)
     dev = torch.device("cuda", 0)
     B, H, n, nd = 8, 12, 4170, 4106

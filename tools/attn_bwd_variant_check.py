@@ -2,10 +2,9 @@
 dq / dk / dv, then interleaved HIP-event timing (medians).
   --knob stages --value 3: 3-stage LDS rings (vpt_attn_set_bwd_stages)
 
-  VPT_DIAG=1 python tools/attn_bwd_variant_check.py --knob stages --value 3 [--rounds 6]
+  python tools/attn_bwd_variant_check.py --knob stages --value 3 [--rounds 6]
 """
 import os
-os.environ.setdefault("VPT_DIAG", "1")
 import argparse  # noqa: E402
 import json  # noqa: E402
 import sys  # noqa: E402
@@ -16,6 +15,8 @@ sys.path.insert(0, os.path.join(ROOT, "vision-pt_amd"))
 import torch  # noqa: E402
 
 from vpt import _lib, ops  # noqa: E402
+
+_lib.use_diag()
 
 
 def main():

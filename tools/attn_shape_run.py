@@ -24,8 +24,7 @@ def main():
     args = ap.parse_args()
     if args.xcd is not None:
         from vpt import _lib
-        if not _lib.DIAG:
-            raise SystemExit("--xcd needs the diagnostic library (VPT_DIAG=1)")
+        _lib.use_diag()
         _lib.lib.vpt_attn_set_xcd_order(args.xcd)
     dev = torch.device("cuda", 0)
     B, H, n, nd = 8, 12, 4170, 4106

@@ -7,7 +7,6 @@ optimizer overlap on (--overlap on), where the optimizer's kernels share the chi
 import os
 import sys
 
-os.environ["VPT_DIAG"] = "1"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "vision-pt_amd"))
 sys.path.insert(0, ROOT)
@@ -15,6 +14,8 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402,F401  (before the library: HIP is initialised the way the bench does it)
 
 from vpt import _lib  # noqa: E402
+
+_lib.use_diag()
 
 rg = int(sys.argv[1])
 _lib.lib.vpt_gemm_set_ring_grid(rg)

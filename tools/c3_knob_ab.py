@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     args = ap.parse_args()
     knobs = args.knobs.split(",")
-    # diagnostic-library switches (run with VPT_DIAG=1): name -> setter(on)
+    # diagnostic-library switches (loads the diagnostic library): name -> setter(on)
     from vpt import _lib
     diag = {"ATTN_BWD_STAGES3": lambda on: _lib.lib.vpt_attn_set_bwd_stages(3 if on else 2),
             "SWB_AHEAD": lambda on: _lib.lib.vpt_gemm_set_swb_one_group(0 if on else 1),
@@ -46,7 +46,7 @@ def main():
     for k in knobs:
         if k in diag:
             if not _lib.DIAG:
-                raise SystemExit(f"{k}: needs the diagnostic library (VPT_DIAG=1)")
+                _lib.use_diag()
             continue
         if not isinstance(getattr(engine, k), bool):
             raise SystemExit(f"{k}: not a boolean knob of vpt.engine")

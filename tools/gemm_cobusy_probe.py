@@ -1,10 +1,10 @@
-"""How a persistent ring GEMM tolerates kernels running beside it (diagnostic library, VPT_DIAG=1): on a side stream,
+"""How a persistent ring GEMM tolerates kernels running beside it (diagnostic library): on a side stream,
 `k` one-wave workgroups each hold a CU for T us (vpt_diag_occupy: a stand-in for RCCL's all-reduce channels or the
 side-stream optimizer at N > 1), and the GEMM is launched on the main stream right after; its time (HIP events on
 the main stream) against k, for the persistent grid (one block per CU, items walked in a fixed stride) and for one
 block per item (ring grid = items; the dispatcher places blocks wherever CUs are free).
 
-  VPT_DIAG=1 python tools/gemm_cobusy_probe.py [--T 150]
+  python tools/gemm_cobusy_probe.py [--T 150]
 """
 import argparse
 import json
@@ -25,8 +25,7 @@ def main():
     ap.add_argument("--T", type=float, default=150.0, help="occupier duration, us")
     ap.add_argument("--reps", type=int, default=7)
     args = ap.parse_args()
-    if not _lib.DIAG:
-        raise SystemExit("needs the diagnostic library (VPT_DIAG=1)")
+    _lib.use_diag()
     lib = _lib.lib
     dev = torch.device("cuda", 0)
     M, D, F = 8 * 4170, 768, 2048

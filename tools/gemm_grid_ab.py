@@ -2,7 +2,7 @@
 at the C3 bench shapes (M = 8 x 4170): every ring GEMM of a JiT-B/16 block (forward, fused SwiGLU forward / backward,
 input and weight gradients). Diagnostic library (vpt_gemm_set_ring_grid). Prints per-shape medians (us) and the sum.
 
-  VPT_DIAG=1 python tools/gemm_grid_ab.py [--rounds 5]
+  python tools/gemm_grid_ab.py [--rounds 5]
 """
 import argparse
 import json
@@ -34,8 +34,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--M", type=int, default=8 * 4170)
     args = ap.parse_args()
-    if not _lib.DIAG:
-        raise SystemExit("needs the diagnostic library (VPT_DIAG=1)")
+    _lib.use_diag()
     dev = "cuda"
     M, D, F = args.M, 768, 2048
     r = lambda *s: torch.randn(*s, device=dev).bfloat16()  # noqa: E731

@@ -4,7 +4,6 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/$1
 mkdir -p $O
-export VPT_DIAG=1
 for sv in $(echo $2 | tr , ' '); do
   s=${sv%%:*}; v=${sv#*:}; [ "$v" = "$sv" ] && v=1
   timeout -k 10 200 python -u tools/attn_ab.py --setter $s --value $v > $O/ab_${s}_$v.json 2> $O/ab_${s}_$v.err || { tail -20 $O/ab_${s}_$v.err; exit 1; }

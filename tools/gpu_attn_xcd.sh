@@ -4,7 +4,6 @@ set -e
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$1
 mkdir -p $O
-export VPT_DIAG=1
 timeout -k 10 200 python -u $R/tools/attn_ab.py --setter vpt_attn_set_xcd_order > $O/xcd_ab.json 2> $O/xcd_ab.err
 cat $O/xcd_ab.json
 cd /tmp && export TMPDIR=/tmp

@@ -4,9 +4,6 @@ known-good reference bar. Interleaved rounds in one process (guide §5.4 rule 24
 
   python tools/kernel_bench.py [--rounds 5]
 """
-import os
-os.environ.setdefault("VPT_DIAG", "1")  # A/B switches live in libvpt_hip_diag.so only
-
 import argparse
 import json
 import os
@@ -17,7 +14,9 @@ sys.path.insert(0, os.path.join(ROOT, "vision-pt_amd"))
 
 import torch  # noqa: E402
 
-from vpt import ops  # noqa: E402
+from vpt import _lib, ops  # noqa: E402
+
+_lib.use_diag()  # A/B switches live in libvpt_hip_diag.so only
 
 
 def timeit(fn, iters=10):

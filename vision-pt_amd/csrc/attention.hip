@@ -545,6 +545,7 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnArgs g) {
 // delta[b,h,q] = -sum_d dO[q,d] * O[q,d] (stored negated: it is the dP chains' initial accumulator);
 // 8 lanes per (b,h,q) row.
 __global__ void attn_bwd_pre_kernel(AttnArgs g, int H, long rows_total) {
+#pragma clang fp contract(off)  // each product rounded, then summed (no fma): the results of the SLP-packed build
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long row = gid >> 3;
   const int part = gid & 7;

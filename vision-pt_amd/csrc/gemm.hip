@@ -1702,7 +1702,9 @@ extern "C" int vpt_linear_wgrad(const void* dy, long lddy, const void* x, long l
 
 // vpt_linear_wgrad plus one unrelated column sum rr_out[c] (=|+=) sum_r rr_part[r][c] ([rr_R][rr_C] f32, e.g. an
 // RMSNorm weight gradient's partial rows), computed by extra blocks of the weight gradient's split-K reduce launch
-// instead of a launch of its own (vpt_reduce_rows semantics; the 256-thread summation order).
+// instead of a launch of its own (vpt_reduce_rows semantics with its 64-row-group summation order, colsum_block<64>;
+// vpt_reduce_rows itself switches to 256 row groups at R >= 256, so for such R the two sum in different, each fixed,
+// orders: deterministic, not bitwise equal to the standalone reduce).
 extern "C" int vpt_linear_wgrad_rr(const void* dy, long lddy, const void* x, long ldx, float* dw, long lddw, float* db,
                                    long M, int N, int K, int accumulate, int splits, void* workspace, int geometry,
                                    int ring_grid, const float* rr_part, int rr_R, int rr_C, float* rr_out, int rr_acc,

@@ -22,9 +22,9 @@ LIB_DIAG = PKG_ROOT / "lib" / "libvpt_hip_diag.so"
 ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
-# Per-unit extra flags. gemm.hip: no SLP packing of the epilogues' f32 math into v_pk_*_f32 (packed f32 ops
-# beside MFMAs cost issue cycles: guide, 'price of one filler beside MFMAs').
-UNIT_FLAGS = {"gemm.hip": ["-fno-slp-vectorize"]}
+# Per-unit extra flags. gemm.hip, attention.hip: no SLP packing of f32 math into v_pk_*_f32 (packed f32 ops beside
+# MFMAs cost issue cycles: guide, 'price of one filler beside MFMAs'; attention backward -1.9 %, r05a in-process A/B).
+UNIT_FLAGS = {"gemm.hip": ["-fno-slp-vectorize"], "attention.hip": ["-fno-slp-vectorize"]}
 
 
 def _needs(obj: Path, deps: list[Path]) -> bool:
@@ -34,11 +34,12 @@ def _needs(obj: Path, deps: list[Path]) -> bool:
     return any(d.stat().st_mtime > t for d in deps)
 
 
-def _compile(src: Path, diag: bool = False) -> Path:
-    obj = (BUILD_DIAG if diag else BUILD) / (src.stem + ".o")
+def _compile(src: Path, diag: bool = False, bdir: Path | None = None, flags: dict | None = None) -> Path:
+    obj = (bdir or (BUILD_DIAG if diag else BUILD)) / (src.stem + ".o")
+    unit_flags = UNIT_FLAGS if flags is None else flags
     deps = [src] + sorted(CSRC.glob("*.h")) + (sorted((CSRC / "diag").glob("*.inc")) if diag else [])
     if _needs(obj, deps):
-        cmd = [HIPCC, *CFLAGS, *UNIT_FLAGS.get(src.name, []), *(["-DVPT_DIAG"] if diag else []), "-c", str(src), "-o",
+        cmd = [HIPCC, *CFLAGS, *unit_flags.get(src.name, []), *(["-DVPT_DIAG"] if diag else []), "-c", str(src), "-o",
                str(obj)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
@@ -73,6 +74,35 @@ def build(verbose: bool = False, diag: bool = False) -> Path:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
     if verbose:
         print(f"built {lib}")
+    return lib
+
+
+def build_variant(name: str, flags: dict, diag: bool = False) -> Path:
+    """tools/ only: the same sources with other per-unit flags (e.g. {"attention.hip": ["-fno-slp-vectorize"]}), into
+    build_var/<name>/ and lib/var/libvpt_hip_<name>.so, for an in-process A/B against the production library
+    (vpt._lib.load_library / use_library). Rebuilt from scratch every call (the flags are not tracked)."""
+    bdir = PKG_ROOT / "build_var" / name
+    lib = PKG_ROOT / "lib" / "var" / f"libvpt_hip_{name}.so"
+    if diag:
+        _gen_diag_sources()
+    bdir.mkdir(parents=True, exist_ok=True)
+    lib.parent.mkdir(parents=True, exist_ok=True)
+    for o in bdir.glob("*.o"):
+        o.unlink()
+    srcs = sorted(CSRC.glob("*.hip"))
+    base_flags = UNIT_FLAGS
+
+    def obj(src):  # a unit whose flags match the production (or diag) build links that build's object, rebuilt if stale
+        if flags.get(src.name, []) == base_flags.get(src.name, []):
+            return _compile(src, diag)
+        return _compile(src, diag, bdir, flags)
+
+    with cf.ThreadPoolExecutor(min(len(srcs), 8)) as ex:
+        objs = list(ex.map(obj, srcs))
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(lib)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
     return lib
 
 

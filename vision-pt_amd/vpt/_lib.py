@@ -8,7 +8,6 @@ this module raises. Every entry point returns an int status; nonzero raises Runt
 from __future__ import annotations
 
 import ctypes as C
-import os
 from pathlib import Path
 
 from ._build import LIB, LIB_DIAG
@@ -115,7 +114,7 @@ SIGNATURES: dict[str, list] = {
     "vpt_build_info": [],
 }
 # Diagnostic-only entry points (include/vpt_hip_diag.h): exported by libvpt_hip_diag.so, loaded only
-# when VPT_DIAG=1 (tools/), never by the product path.
+# explicitly by tools/ (use_diag()), never by the product path.
 DIAG_SIGNATURES: dict[str, list] = {
     "vpt_gemm_set_geometry": [I],
     "vpt_gemm_set_stagger": [I],
@@ -163,12 +162,41 @@ def _load(path: Path, diag: bool = False) -> C.CDLL:
     return lib
 
 
-DIAG = os.environ.get("VPT_DIAG", "0") == "1"
-LIB_PATH = LIB_DIAG if DIAG else LIB
-lib = _load(LIB_PATH, DIAG)
 ABI_VERSION = 3  # the signatures in SIGNATURES / include/vpt_hip.h
-if lib.vpt_abi_version() != ABI_VERSION:
-    raise ImportError(f"{LIB_PATH}: ABI {lib.vpt_abi_version()} != {ABI_VERSION} expected by these bindings; rebuild it")
+
+
+def load_library(path: Path | str, diag: bool = False) -> C.CDLL:
+    """Loads one build of the C ABI and checks its ABI version (does not route calls through it)."""
+    path = Path(path)
+    lib_ = _load(path, diag)
+    if lib_.vpt_abi_version() != ABI_VERSION:
+        raise ImportError(f"{path}: ABI {lib_.vpt_abi_version()} != {ABI_VERSION} expected by these bindings; rebuild it")
+    return lib_
+
+
+# The product library. No environment read and no fallback: tools/ that need the diagnostic twin (or another build of
+# the same sources, for a compile-flag A/B) switch to it explicitly with use_library() / use_diag().
+DIAG = False
+LIB_PATH = LIB
+lib = load_library(LIB)
+
+
+def use_library(lib_or_path, diag: bool = False) -> C.CDLL:
+    """tools/ only: routes every later call() through another build (a loaded CDLL or a path)."""
+    global lib, LIB_PATH, DIAG
+    if isinstance(lib_or_path, C.CDLL):
+        lib = lib_or_path
+        LIB_PATH = Path(lib_or_path._name)
+    else:
+        lib = load_library(lib_or_path, diag)
+        LIB_PATH = Path(lib_or_path)
+    DIAG = diag
+    return lib
+
+
+def use_diag() -> C.CDLL:
+    """tools/ only: the -DVPT_DIAG twin libvpt_hip_diag.so (process-wide A/B switches, timing ablations)."""
+    return use_library(LIB_DIAG, diag=True)
 
 
 def call(name: str, *args):

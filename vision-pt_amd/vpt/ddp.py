@@ -71,10 +71,15 @@ class GradSync:
     clip_grad_norm (after_backward, src/models/for_training.py:98-109): the global L2 norm of the mean
     gradient needs every bucket, so landing buckets only contribute partial sums of squares (side stream);
     finish() forms the coefficient on the device (no host sync) and steps every bucket with it.
-    clip_grad_value: a clamp inside the optimizer kernel, so it keeps the overlap."""
+    clip_grad_value: a clamp inside the optimizer kernel, so it keeps the overlap.
+
+    force_collective=True runs every bucket's all-reduce (and the wire cast) even at world size 1, so the
+    collective path -- RCCL's stream-ordered wait inside the side-stream context, the wire cast before it on the
+    compute stream -- can be exercised on a one-GPU box (a SUM over one rank is the identity)."""
 
     def __init__(self, grads: torch.Tensor, buckets: list[tuple[str, int, int]], group=None, wire: str = "f32",
-                 overlap: bool = True, clip_grad_norm: float | None = None, clip_grad_value: float | None = None):
+                 overlap: bool = True, clip_grad_norm: float | None = None, clip_grad_value: float | None = None,
+                 force_collective: bool = False):
         if wire not in ("f32", "bf16"):
             raise ValueError(f"wire dtype must be 'f32' or 'bf16', got {wire!r}")
         self.grads = grads
@@ -87,10 +92,13 @@ class GradSync:
         self.buckets_span = (spans[0][0], spans[-1][1])
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        if force_collective and not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("GradSync(force_collective=True) needs an initialised process group")
+        self.collective = self.world > 1 or force_collective
         self.wire = wire
         self.cuda = grads.is_cuda
         self.comm = torch.empty(grads.numel(), dtype=torch.bfloat16, device=grads.device) \
-            if wire == "bf16" and self.world > 1 else None
+            if wire == "bf16" and self.collective else None
         self.overlap = overlap  # land (reduce-wait + step) each bucket as it is launched
         self.side = torch.cuda.Stream(device=grads.device) if (self.cuda and overlap) else None
         self.configure_clipping(clip_grad_norm, clip_grad_value)
@@ -134,7 +142,7 @@ class GradSync:
         if name in self.works or name in self.landed:
             return
         lo, hi = self.index[name]
-        if self.world > 1:
+        if self.collective:
             buf = self._to_wire(lo, hi) if self.comm is not None else self.grads[lo:hi]
             self.works[name] = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         else:
@@ -193,7 +201,7 @@ class GradSync:
             self.scale = grad_scale / self.world
         if self.apply_fn is None:
             raise RuntimeError("GradSync.finish: no optimizer callback (arm() or finish(apply_fn))")
-        if self.world == 1 and not self.overlap and self.clip_norm is None and not self.landed:
+        if not self.collective and not self.overlap and self.clip_norm is None and not self.landed:
             # one process, serial: the buckets tile the flat buffer, so ONE optimizer launch covers them all
             lo, hi = self.buckets_span
             self.apply_fn(lo, hi, self.scale, self.grads[lo:hi], **self._clip_kw())
@@ -235,11 +243,12 @@ class LossLog:
     171-183) as ONE async all-reduce of a 2-float [loss_sum, count] tensor per step. The reduced pair is
     copied to pinned host memory behind an event and read `depth - 1` steps later, so the host never
     waits for the step it just enqueued (the reference's per-step gather + .item() is a full sync).
-    world 1: no collective."""
+    world 1: no collective (force_collective=True: the all-reduce anyway, as GradSync's)."""
 
-    def __init__(self, device, group=None, depth: int = 3):
+    def __init__(self, device, group=None, depth: int = 3, force_collective: bool = False):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.collective = self.world > 1 or force_collective
         dev = torch.device(device)
         self.cuda = dev.type == "cuda"
         self.slots = [torch.zeros(2, dtype=torch.float32, device=dev) for _ in range(depth)]
@@ -255,7 +264,7 @@ class LossLog:
         buf = self.slots[i]
         buf[0].copy_(loss.reshape(()))
         buf[1].fill_(1.0)
-        work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True) if self.world > 1 else None
+        work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True) if self.collective else None
         ev = None
         if self.cuda:
             if work is not None:

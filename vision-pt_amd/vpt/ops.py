@@ -651,12 +651,16 @@ def bias_grad(dy, out, part=None, accumulate=False):
 
 def embed_gather(table, ids, out):
     R = ids.numel()
+    if R == 0:  # a context-free batch (n_ctx = 0): nothing to gather
+        return out
     call("vpt_embed_gather", table.data_ptr(), ids.data_ptr(), R, table.shape[1], out.data_ptr(), stream())
     return out
 
 
 def embed_scatter_add(drows, ids, pad_id, dtable):
     R = ids.numel()
+    if R == 0:
+        return
     call("vpt_embed_scatter_add", drows.data_ptr(), ids.data_ptr(), R, dtable.shape[1], pad_id, dtable.data_ptr(),
          stream())
 

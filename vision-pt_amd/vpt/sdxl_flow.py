@@ -233,9 +233,11 @@ class SDXLFlowMatchQLoRA:
         back(0, de0)                               # (+ dx64: the input map is frozen, z needs no gradient)
 
     # ------------------------------------------------------------------ the step
-    def sample_t(self) -> torch.Tensor:
-        """sample_timestep(latents.shape, ...) (flow_match.py:127-140), t in (0, 1) f32 [B] on the device."""
-        return sample_timestep((self.B, 4, *self.latent), "cpu", generator=self.gen, **self.sampling).to(self.device)
+    def sample_t(self, shape=None) -> torch.Tensor:
+        """sample_timestep(latents.shape, ...) (flow_match.py:127-140), t in (0, 1) f32 [B] on the device. `shape` = the
+        batch's latent shape (resolution-dependent samplers such as flux_shift use its h, w); default the model's."""
+        shape = tuple(shape) if shape is not None else (self.B, 4, *self.latent)
+        return sample_timestep(shape, "cpu", generator=self.gen, **self.sampling).to(self.device)
 
     def step(self, latents: torch.Tensor, ctx: torch.Tensor, pooled: torch.Tensor, sizes: torch.Tensor,
              t: torch.Tensor | None = None, eps: torch.Tensor | None = None, backward: bool = True,
@@ -243,7 +245,7 @@ class SDXLFlowMatchQLoRA:
         """latents bf16 [B, 4, L, L]; ctx bf16 [B * n_ctx, context_dim]; pooled [B, 1280]; sizes [B, 6]
         (original_size, crop_coords_top_left, target_size). Returns (loss device f32 [1], v)."""
         B = self.B
-        t = self.sample_t() if t is None else t.to(self.device, F32)
+        t = self.sample_t(latents.shape) if t is None else t.to(self.device, F32)
         t1000 = t * 1000.0                          # the model's timestep (0~1000)
         z = torch.empty_like(latents)
         eps_buf = torch.empty_like(latents) if eps is None else None
