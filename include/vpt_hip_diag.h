@@ -49,7 +49,17 @@ int vpt_attn_set_xcd_order(int on);
 int vpt_attn_set_fwd_order(int on);
 /* Attention backward: transposed-fragment prefetch in the dK/dV (bit 1) / dQ (bit 2) products; 0 = production. */
 int vpt_attn_set_bwd_prefetch(int mask);
+/* Attention backward partner waves: bit 0 = s_setprio 1 for the odd-slot wave of each SIMD, bit 1 = its block starts
+   (v >> 2) x 10 ns late; 0 = production. */
+int vpt_attn_set_bwd_partner(int v);
 int vpt_gemm_set_swb_one_group(int on);
+/* SwiGLU-backward ring GEMM timing ablations (WRONG results): 0 off, 3 = no epilogue, 4 = dx12 stores dropped,
+   6 = every item's x12 operands from the first tile (L2-resident). */
+int vpt_gemm_set_swb_ablation(int a);
+/* 256x128 two-blocks-per-CU ring (gemm_r2.hip) in place of the 256x256 ring, by launch kind: bit 0 = k-major A (forward,
+   input gradient), 1 = mn-major A (weight gradient), 2 = fused SwiGLU forward, 3 = fused SwiGLU backward, 4 = fused
+   QK-norm + RoPE forward; 0 = production. */
+int vpt_gemm_set_r2(int mask);
 /* NF4 GEMM timing ablations (WRONG results): 0 off, 1 = no dequant, 2 = no NF4 code loads / dequant. */
 int vpt_gemm_set_nf4_ablation(int a);
 /* Co-running-kernel probe: `blocks` one-wave workgroups holding a CU each (lds_bytes of LDS) for `ticks` of the 100-MHz

@@ -59,7 +59,21 @@ def attn_case(dev):
         ops.attn_bwd(q4, k4, v4, o4, do4, lse, delta, kb, ops._t4(dqk, B, n, H, 0), ops._t4(dqk, B, n, H, D),
                      ops._t4(dqkv, B, n, H, 2 * D), B, H, n, n, nd)
 
-    return fwd, bwd, (o, lse, dqk, dqkv)
+    def check(heads=2):
+        """max |error| of o and of lse (log2 units, stored negated) vs a torch fp32 reference, batch 0, heads < `heads`."""
+        eo, el = 0.0, 0.0
+        for h in range(heads):
+            q = qk[:n, h * 64:(h + 1) * 64].float()
+            k = qk[:n, D + h * 64:D + (h + 1) * 64].float()
+            v = qkv[:n, 2 * D + h * 64:2 * D + (h + 1) * 64].float()
+            s = q @ k.T + kb[0][None, :]                     # log2 units (q pre-scaled by scale * log2 e)
+            ref_lse = -torch.logsumexp(s * 0.6931471805599453, 1) / 0.6931471805599453
+            ref_o = torch.softmax(s * 0.6931471805599453, 1) @ v
+            el = max(el, (lse[0, h] - ref_lse).abs().max().item())
+            eo = max(eo, (o[:n, h * 64:(h + 1) * 64].float() - ref_o).abs().max().item())
+        return {"o_max_abs_err": eo, "lse_max_abs_err": el}
+
+    return fwd, bwd, (o, lse, dqk, dqkv), check
 
 
 def time_launches(fn, iters):
@@ -89,18 +103,23 @@ def main():
     out = {"variants": names}
     what = args.what.split(",")
     if "attn" in what:
-        fwd, bwd, res = attn_case(dev)
+        fwd, bwd, res, check = attn_case(dev)
         ref = None
-        eq = {}
-        for nm in names:
-            _lib.use_library(libs[nm])
-            fwd()
-            bwd()
-            torch.cuda.synchronize()
-            got = [t.clone() for t in res]
-            if ref is None:
-                ref = got
-            eq[nm] = all(torch.equal(a, b) for a, b in zip(ref, got))
+        eq, err = {}, {}
+        for rep in range(2):  # each variant twice, in turn: run-to-run and library-to-library equality
+            for nm in names:
+                _lib.use_library(libs[nm])
+                fwd()
+                torch.cuda.synchronize()
+                if rep == 0:
+                    err[nm] = check()
+                bwd()
+                torch.cuda.synchronize()
+                got = [t.clone() for t in res]
+                if ref is None:
+                    ref = got
+                eq[f"{nm}#{rep}"] = {k: (torch.equal(a, b), (a.float() - b.float()).abs().max().item())
+                                     for k, a, b in zip(("o", "lse", "dqk", "dqkv"), ref, got)}
         tm = {f"{k}_{nm}": [] for k in ("fwd", "bwd") for nm in names}
         for r in range(args.rounds):
             order = names if r % 2 == 0 else names[::-1]
@@ -109,7 +128,7 @@ def main():
                 tm[f"fwd_{nm}"].append(time_launches(fwd, args.iters))
                 tm[f"bwd_{nm}"].append(time_launches(bwd, args.iters))
         med = {k: round(statistics.median(v), 4) for k, v in tm.items()}
-        out["attn"] = {"bitwise_equal_to_first": eq, "median_ms": med,
+        out["attn"] = {"bitwise_equal_to_first": eq, "fwd_vs_fp32": err, "median_ms": med,
                        "ratio_to_first": {k: round(v / med[k.split("_")[0] + "_" + names[0]], 4) for k, v in med.items()}}
         print(json.dumps(out["attn"]), flush=True)
     if "step" in what:

@@ -73,6 +73,9 @@ def main():
         i = args.index("--tag")
         tag = args[i + 1]
         del args[i:i + 2]
+    c5 = "--c5" in args
+    if c5:
+        args.remove("--c5")
     fdir, wdir, kdir, out = args[:4]
     mdir = args[4] if len(args) > 4 else None
     fetch, nf = _counter(fdir, "FETCH_SIZE")
@@ -125,6 +128,13 @@ def main():
                 d["mfma_util"] = round(busy * 8 / (gui * 1024), 4)
         res["_mfma_method"] = ("rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE (one pass); "
                                "mfma_util = MFMA_BUSY x 8 / (GRBM_GUI_ACTIVE x 1024 SIMDs)")
+    if c5 and "gemm" in res:
+        # the C5 step's GEMM kernels (gemm_ring / gemm_bf16 + split-K reduces) are its base+LoRA GEMMs (842 launches per
+        # step in the bench's probe) and 68 plain ones (conditioning MLPs, skeleton maps): the kernel names do not tell
+        # them apart, so the LoRA GEMM's entry is the per-launch mean over all of them (LoRA launches: ~93 % of the
+        # launches, ~96 % of the GEMM time)
+        res["gemm_lora"] = dict(res["gemm"], note="per-launch mean over every GEMM-kernel dispatch of the C5 step "
+                                                  "(842 base+LoRA + 68 plain GEMM launches per step)")
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 

@@ -53,6 +53,8 @@ struct AttnArgs {
   float* dwq; float* dwk;               // per-workgroup partial weight gradients, rows of 64 at stride dw_ld
   long dw_ld;
   int xcd;  // block order: 1 = XCD-contiguous (xcd_remap), 0 = linear
+  int pm;   // backward partner-wave treatment (diagnostic build only; 0 in production): bit 0 = s_setprio 1 for the
+            // wave in an odd slot of its SIMD, bit 1 = that wave's block starts pm >> 2 ticks (10 ns) late
 };
 
 constexpr float kNegInf = -__builtin_huge_valf();
@@ -68,6 +70,7 @@ int g_bwd_pf = 0;   // backward transposed-fragment prefetch (vpt_attn_set_bwd_p
 int g_xcd = 1;      // block order of the forward / backward grids (vpt_attn_set_xcd_order, A/B)
 int g_rows64 = 0;   // backward variants (vpt_attn_set_rows64 bit mask, A/B): 1 = 64-key dK/dV, 2 = 64-query dQ
                     // at 2 waves / SIMD, 4 = 64-query dQ at 1 wave / SIMD; 0 = the 32-row pair
+int g_pm = 0;       // backward partner-wave priority / stagger (vpt_attn_set_bwd_partner, A/B)
 #else
 constexpr int g_variant = 0, g_waves = 4;
 constexpr float g_tau = kTau;
@@ -982,6 +985,21 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs g, int nkb, i
   __shared__ __attribute__((aligned(16))) char lds[NST][2][8192];
   __shared__ __attribute__((aligned(16))) float lstat[NST][2][64];
   extern __shared__ __attribute__((aligned(16))) float kbl[];
+#ifdef VPT_DIAG
+  if (g.pm) {
+    // Two blocks share each CU, one wave of each per SIMD, running the same program: partner waves that start together
+    // stay in step (both in their exp / pack phase, then both in their MFMA phase). The wave in an odd slot of its SIMD
+    // (HW_ID[3:0]) takes static priority (guide: two waves per SIMD, item 4) and / or starts its block late (item 9).
+    const unsigned slot = __builtin_amdgcn_s_getreg((3 << 11) | 4) & 15u;  // hwreg(HW_REG_HW_ID, 0, 4)
+    if (slot & 1u) {
+      if (g.pm & 1) __builtin_amdgcn_s_setprio(1);
+      if (g.pm & 2) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)(g.pm >> 2)) __builtin_amdgcn_s_sleep(1);
+      }
+    }
+  }
+#endif
   int bid = blockIdx.x;
   bool kv;
   int bx, r;
@@ -1134,6 +1152,9 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
   g.kb0 = g.n_dense / 64 * 64;
   g.nq_pad = (n + 63) / 64 * 64;
   g.H = H;
+#ifdef VPT_DIAG
+  g.pm = g_pm;
+#endif
   return attn_bwd_impl(g, B, H, n, nk, (hipStream_t)stream);
 }
 

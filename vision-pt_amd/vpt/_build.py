@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import os
+import re
 import subprocess
 import sys
 from pathlib import Path
@@ -24,7 +25,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
 # Per-unit extra flags. gemm.hip, attention.hip: no SLP packing of f32 math into v_pk_*_f32 (packed f32 ops beside
 # MFMAs cost issue cycles: guide, 'price of one filler beside MFMAs'; attention backward -1.9 %, r05a in-process A/B).
-UNIT_FLAGS = {"gemm.hip": ["-fno-slp-vectorize"], "attention.hip": ["-fno-slp-vectorize"]}
+UNIT_FLAGS = {"gemm.hip": ["-fno-slp-vectorize"], "gemm_r2.hip": ["-fno-slp-vectorize"],
+              "attention.hip": ["-fno-slp-vectorize"]}
 
 
 def _needs(obj: Path, deps: list[Path]) -> bool:
@@ -34,10 +36,26 @@ def _needs(obj: Path, deps: list[Path]) -> bool:
     return any(d.stat().st_mtime > t for d in deps)
 
 
+def _headers(src: Path) -> list[Path]:
+    """csrc/*.h files a source includes, directly or through another header."""
+    out, todo = [], [src]
+    while todo:
+        for name in re.findall(r'#include "([^"/]+\.h)"', todo.pop().read_text()):
+            h = CSRC / name
+            if h.exists() and h not in out:
+                out.append(h)
+                todo.append(h)
+    return sorted(out)
+
+
 def _compile(src: Path, diag: bool = False, bdir: Path | None = None, flags: dict | None = None) -> Path:
     obj = (bdir or (BUILD_DIAG if diag else BUILD)) / (src.stem + ".o")
     unit_flags = UNIT_FLAGS if flags is None else flags
-    deps = [src] + sorted(CSRC.glob("*.h")) + (sorted((CSRC / "diag").glob("*.inc")) if diag else [])
+    text = src.read_text()
+    # diag/*.inc: a dependency of the units that include it (directly or through another .inc)
+    incs = [f for f in sorted((CSRC / "diag").glob("*.inc")) if f.name in text] if diag else []
+    incs += [f for f in sorted((CSRC / "diag").glob("*.inc")) if diag and any(f.name in i.read_text() for i in incs)]
+    deps = [src] + _headers(src) + incs
     if _needs(obj, deps):
         cmd = [HIPCC, *CFLAGS, *unit_flags.get(src.name, []), *(["-DVPT_DIAG"] if diag else []), "-c", str(src), "-o",
                str(obj)]

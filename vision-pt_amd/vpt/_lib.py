@@ -129,7 +129,10 @@ DIAG_SIGNATURES: dict[str, list] = {
     "vpt_attn_set_xcd_order": [I],
     "vpt_attn_set_fwd_order": [I],
     "vpt_attn_set_bwd_prefetch": [I],
+    "vpt_attn_set_bwd_partner": [I],
     "vpt_gemm_set_swb_one_group": [I],
+    "vpt_gemm_set_swb_ablation": [I],
+    "vpt_gemm_set_r2": [I],
     "vpt_gemm_set_nf4_ablation": [I],
     "vpt_diag_occupy": [I, L, I, P, P],
 }
