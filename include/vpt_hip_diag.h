@@ -58,7 +58,7 @@ int vpt_gemm_set_swb_one_group(int on);
 int vpt_gemm_set_swb_ablation(int a);
 /* 256x128 two-blocks-per-CU ring (gemm_r2.hip) in place of the 256x256 ring, by launch kind: bit 0 = k-major A (forward,
    input gradient), 1 = mn-major A (weight gradient), 2 = fused SwiGLU forward, 3 = fused SwiGLU backward, 4 = fused
-   QK-norm + RoPE forward; 0 = production. */
+   QK-norm + RoPE forward; production = 8. */
 int vpt_gemm_set_r2(int mask);
 /* NF4 GEMM timing ablations (WRONG results): 0 off, 1 = no dequant, 2 = no NF4 code loads / dequant. */
 int vpt_gemm_set_nf4_ablation(int a);

@@ -44,11 +44,11 @@ def main():
             "ATTN_PRIO": lambda on: _lib.lib.vpt_attn_set_bwd_prefetch(4 if on else 0),
             "RING_PER_ITEM": lambda on: _lib.lib.vpt_gemm_set_ring_grid(0 if on else 256),
             # the 256x128 two-blocks-per-CU ring (gemm_r2.hip) by launch kind (vpt_gemm_set_r2 bit mask)
-            "GEMM_R2": lambda on: _lib.lib.vpt_gemm_set_r2(31 if on else 0),
+            "GEMM_R2": lambda on: _lib.lib.vpt_gemm_set_r2(31 if on else 8),
             "GEMM_R2_SWB": lambda on: _lib.lib.vpt_gemm_set_r2(8 if on else 0),
-            "GEMM_R2_KMAJ": lambda on: _lib.lib.vpt_gemm_set_r2(1 if on else 0),
-            "GEMM_R2_WGRAD": lambda on: _lib.lib.vpt_gemm_set_r2(2 if on else 0),
-            "GEMM_R2_FWD": lambda on: _lib.lib.vpt_gemm_set_r2(20 if on else 0)}
+            "GEMM_R2_KMAJ": lambda on: _lib.lib.vpt_gemm_set_r2(9 if on else 8),
+            "GEMM_R2_WGRAD": lambda on: _lib.lib.vpt_gemm_set_r2(10 if on else 8),
+            "GEMM_R2_FWD": lambda on: _lib.lib.vpt_gemm_set_r2(28 if on else 8)}
     for k in knobs:
         if k in diag:
             if not _lib.DIAG:

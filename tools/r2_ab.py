@@ -36,8 +36,15 @@ def main():
     ap.add_argument("--M", type=int, default=8 * 4106)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--mask", type=int, default=31)
+    ap.add_argument("--lib", default=None, help="a diagnostic variant build lib/var/libvpt_hip_<name>.so")
+    ap.add_argument("--only", default=None, help="cases whose name contains this")
+    ap.add_argument("--stagger", type=int, default=0, help="R2 start stagger of the second blocks (10-ns ticks)")
     args = ap.parse_args()
-    _lib.use_diag()
+    if args.lib:
+        from vpt._build import PKG_ROOT
+        _lib.use_library(PKG_ROOT / "lib" / "var" / f"libvpt_hip_{args.lib}.so", diag=True)
+    else:
+        _lib.use_diag()
     dev = "cuda"
     M, D, F = args.M, 768, 2048
     g = torch.Generator(device=dev).manual_seed(0)
@@ -70,7 +77,7 @@ def main():
         "dgrad N768 K2304": (lambda: ops.linear_dgrad(dqkv, wqkv, out=outs["dxqkv"]), ("dxqkv",), 2 * M * D * 3 * D),
         "dgrad N768 K4096": (lambda: ops.linear_dgrad(dx12, w12, out=outs["dx12b"]), ("dx12b",), 2 * M * D * 2 * F),
     }
-    for name, (dyt, xt, key, N, K) in (("wgrad N2304 K768", dqkv, x, "gqkv", 3 * D, D),
+    for name, dyt, xt, key, N, K in (("wgrad N2304 K768", dqkv, x, "gqkv", 3 * D, D),
                                         ("wgrad N768 K768", dy, x, "go", D, D),
                                         ("wgrad N4096 K768", dx12, x, "g12", 2 * F, D),
                                         ("wgrad N768 K2048", dy, h, "g3", D, F)):
@@ -83,9 +90,12 @@ def main():
 
     res = {}
     for name, (fn, names, fl) in cases.items():
+        if args.only and args.only not in name:
+            continue
         got = {}
         for m in (0, args.mask):
             _lib.lib.vpt_gemm_set_r2(m)
+            _lib.lib.vpt_gemm_set_stagger(args.stagger if m else 0)  # the stagger for the R2 side only
             fn()
             torch.cuda.synchronize()
             got[m] = grab(names)
@@ -94,14 +104,16 @@ def main():
         for r in range(args.rounds):
             for m in ((0, args.mask) if r % 2 == 0 else (args.mask, 0)):
                 _lib.lib.vpt_gemm_set_r2(m)
+                _lib.lib.vpt_gemm_set_stagger(args.stagger if m else 0)
                 t[m].append(timeit(fn))
         ring, r2 = statistics.median(t[0]), statistics.median(t[args.mask])
         res[name] = {"bitwise_equal": eq, "ring_us": round(ring, 1), "r2_us": round(r2, 1),
                      "r2_vs_ring": round(r2 / ring, 4), "ring_tflops": round(fl / ring / 1e6, 1),
                      "r2_tflops": round(fl / r2 / 1e6, 1)}
         print(name, json.dumps(res[name]), flush=True)
-    _lib.lib.vpt_gemm_set_r2(0)
-    print(json.dumps({"M": M, "cases": res}))
+    _lib.lib.vpt_gemm_set_r2(8)  # production
+    _lib.lib.vpt_gemm_set_stagger(0)
+    print(json.dumps({"M": M, "lib": args.lib, "stagger": args.stagger, "cases": res}))
 
 
 if __name__ == "__main__":

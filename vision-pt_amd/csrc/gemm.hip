@@ -33,21 +33,20 @@ int launch_r2(const GemmArgs& g, bool ak, bool bk, hipStream_t s);  // gemm_r2.h
 
 namespace {
 
-#ifdef VPT_DIAG
-// A/B (vpt_gemm_set_r2): ring launches that take the 256x128 ring instead, by kind: bit 0 = k-major A (forward /
+// Ring launches that take the 256x128 two-blocks-per-CU ring (gemm_r2.hip) instead, by kind: bit 0 = k-major A (forward /
 // input gradient: plain, residual), bit 1 = mn-major A (weight gradients), bit 2 = fused SwiGLU forward, bit 3 = fused
-// SwiGLU backward, bit 4 = fused QK-norm + RoPE forward
-int g_r2 = 0;
-#endif
-// Whether a ring launch of this kind takes the 256x128 ring (gemm_r2.hip).
-inline bool use_r2(const GemmArgs& g, bool ak) {
+// SwiGLU backward, bit 4 = fused QK-norm + RoPE forward. Production: the SwiGLU backward only -- bitwise equal to the
+// 256x256 ring on every kind, 212 -> 193 us at the C3 shape (its x12 / dx12 epilogue traffic overlaps the CU's other
+// block's K loop), while the other kinds measured level or slower (r05i-r05k, tools/r2_ab.py).
+constexpr int kR2Kinds = 8;
 #ifdef VPT_DIAG
+int g_r2 = kR2Kinds;  // vpt_gemm_set_r2 (A/B)
+#else
+constexpr int g_r2 = kR2Kinds;
+#endif
+inline bool use_r2(const GemmArgs& g, bool ak) {
   const int kind = g.sw == 1 ? 4 : g.sw == 2 ? 8 : g.qk_d > 0 ? 16 : ak ? 1 : 2;
   return (g_r2 & kind) != 0;
-#else
-  (void)g; (void)ak;
-  return false;
-#endif
 }
 
 template <int TM_, int TN_, int WGM, int WGN>
@@ -562,10 +561,17 @@ int launch_ring(const GemmArgs& g, int splits, hipStream_t s) {
 #include "diag/gemm_ring4.inc"
 #endif
 
+// launch_r2 with the (diagnostic) start stagger of ring_stagger()
+inline int launch_r2_st(const GemmArgs& g, bool ak, bool bk, hipStream_t s) {
+  GemmArgs ga = g;
+  ga.stagger = ring_stagger();
+  return launch_r2(ga, ak, bk, s);
+}
+
 template <bool AK, bool BK_>
 int launch_geo(const GemmArgs& g, int splits, int geo, hipStream_t s) {
   if (geo != 128 && geo != 2562 && g.N % 8 != 0) geo = 128;  // ring epilogue stores 8-column chunks
-  if (geo == 256) return use_r2(g, AK) ? launch_r2(g, AK, BK_, s) : launch_ring<AK, BK_, true>(g, splits, s);
+  if (geo == 256) return use_r2(g, AK) ? launch_r2_st(g, AK, BK_, s) : launch_ring<AK, BK_, true>(g, splits, s);
 #ifdef VPT_DIAG
   // diagnostic build only (libvpt_hip_diag.so): A/B geometries, timing ablations with WRONG results
   // (2563, 2564), stamped / timeline builds
@@ -1079,7 +1085,7 @@ extern "C" int vpt_gemm_swiglu_fwd(const void* x, long ldx, const void* w12, lon
   g.k_split = K; g.splits = 1;
   g.out_mode = OUT_BF16; g.act = ACT_NONE; g.alpha = 1.f;
   g.sw = 1;
-  if (use_r2(g, true)) return launch_r2(g, true, true, (hipStream_t)stream);
+  if (use_r2(g, true)) return launch_r2_st(g, true, true, (hipStream_t)stream);
   return launch_ring<true, true, true, 0, false, false, false, 1>(g, 1, (hipStream_t)stream);
 }
 
@@ -1118,7 +1124,7 @@ extern "C" int vpt_gemm_swiglu_bwd(const void* dy, long lddy, const void* w3, lo
   if (g_swb_abl == 4) return launch_ring<true, false, true, 4>(g, 1, (hipStream_t)stream);
   if (g_swb_abl == 6) return launch_ring<true, false, true, 6>(g, 1, (hipStream_t)stream);
 #endif
-  if (use_r2(g, true)) return launch_r2(g, true, false, (hipStream_t)stream);
+  if (use_r2(g, true)) return launch_r2_st(g, true, false, (hipStream_t)stream);
   return launch_ring<true, false, true>(g, 1, (hipStream_t)stream);
 }
 

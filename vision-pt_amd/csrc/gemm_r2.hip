@@ -22,6 +22,18 @@ constexpr int R2A = 256 * RBK * 2;          // A stage bytes (16 KB)
 constexpr int R2STAGE = R2A + R2TN * RBK * 2;  // + B (8 KB)
 constexpr int R2ST = 3;                     // ring stages
 constexpr int R2LDS = R2ST * R2STAGE;       // 72 KB
+// K-step schedule knobs (compile-time; A/B builds of this unit only): PRIO = s_setprio 1 around the MFMAs; SPLIT = the
+// fragment reads in two halves (B + A 0-3, then A 4-7 behind the first 16 MFMAs); DMAMID = tile t+2's DMA issued after
+// the first half of the MFMAs instead of at the top of the step.
+#ifndef VPT_R2_PRIO
+#define VPT_R2_PRIO 1
+#endif
+#ifndef VPT_R2_SPLIT
+#define VPT_R2_SPLIT 0
+#endif
+#ifndef VPT_R2_DMAMID
+#define VPT_R2_DMAMID 0
+#endif
 
 struct R2Item {
   int m0, n0, split, kbeg, kend, nk, klast;
@@ -135,6 +147,13 @@ __global__ __launch_bounds__(256, 2) void gemm_r2_kernel(GemmArgs g) {
   const int tiles = ((g.M + 255) / 256) * tiles_n;
   const int items = tiles * g.splits;
   if ((int)blockIdx.x >= items) return;
+  // The two blocks a CU starts with begin together and, equal in length, would keep reaching their epilogues together.
+  // g.stagger > 0 (10-ns ticks, diagnostic build): the CUs' second blocks of the first wave of the grid (ids 256-511
+  // under the dispatcher's order) start that much later, so the two blocks of a CU alternate K loop and epilogue.
+  if (g.stagger > 0 && blockIdx.x >= 256 && blockIdx.x < 512) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)g.stagger) __builtin_amdgcn_s_sleep(2);
+  }
   const uint32_t smem0 = (uint32_t)(uintptr_t)(VPT_LDS char*)smem;
   const R2Item it = r2_item<AK, BK_, SW>(g, blockIdx.x, items, tiles, tiles_n, wid, lane);
   const int nk = it.nk;
@@ -185,22 +204,34 @@ __global__ __launch_bounds__(256, 2) void gemm_r2_kernel(GemmArgs g) {
 
   for (int kt = 0; kt < nk; ++kt) {
     // tile kt + 2 into the stage of tile kt - 1, which every wave finished reading before the last barrier
-    if (kt + 2 < nk) r2_issue<AK, BK_, SW>(g, it, kt + 2, smem0, wid, lane);
+    if (!VPT_R2_DMAMID && kt + 2 < nk) r2_issue<AK, BK_, SW>(g, it, kt + 2, smem0, wid, lane);
     const char* st = smem + (kt % R2ST) * R2STAGE;
+    const bool mask = kt == nk - 1 && it.klast < RBK;
     bf16x8 bfr[4], af[8];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       bfr[j] = read_frag32<BK_, R2TN>(st + R2A, SW ? ((j & 2) ? R2TN / 2 : 0) + wn * 32 + (j & 1) * 16 : wn * 64 + j * 16,
                                       lane);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) af[i] = read_frag32<AK, 256>(st, wm * 128 + i * 16, lane);
-    if (kt == nk - 1 && it.klast < RBK) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) af[i] = mask_k(af[i], 8 * (lane >> 4), it.klast);
+    for (int i = 0; i < (VPT_R2_SPLIT ? 4 : 8); ++i) {
+      af[i] = read_frag32<AK, 256>(st, wm * 128 + i * 16, lane);
+      if (mask) af[i] = mask_k(af[i], 8 * (lane >> 4), it.klast);
     }
-    __builtin_amdgcn_s_setprio(1);
+    if (VPT_R2_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (VPT_R2_SPLIT) {
+#pragma unroll
+      for (int i = 4; i < 8; ++i) {
+        af[i] = read_frag32<AK, 256>(st, wm * 128 + i * 16, lane);
+        if (mask) af[i] = mask_k(af[i], 8 * (lane >> 4), it.klast);
+      }
+    }
+    if (VPT_R2_DMAMID && kt + 2 < nk) r2_issue<AK, BK_, SW>(g, it, kt + 2, smem0, wid, lane);
+#pragma unroll
+    for (int i = 4; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     if (rs_on) {
@@ -211,7 +242,7 @@ __global__ __launch_bounds__(256, 2) void gemm_r2_kernel(GemmArgs g) {
         racc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(r, ones, racc[f], 0, 0, 0);
       }
     }
-    __builtin_amdgcn_s_setprio(0);
+    if (VPT_R2_PRIO) __builtin_amdgcn_s_setprio(0);
     if (kt + 1 < nk) {
       // this wave's pieces of tile kt + 1 landed (tile kt + 2's six younger ones may still fly), then every wave's
       if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");

@@ -115,47 +115,62 @@ __device__ __forceinline__ void stage_strip(const Strip& st, const unsigned shor
 // in_kind 0: x fp16 + noise (generated or explicit fp16 `noise`), in_kind 1: x bf16 copied as is.
 // An output piece (8 kx of one (c, ky)) is one 16-B piece of an image row, so no transposition is needed -- only
 // the thread order: threads walk a strip's image-row pieces in row order (a wave reads 8 image rows x 128 B, whole
-// lines) and write each piece to its patch row (per wave 4 runs of 256 B). The previous order (output order) read
-// 32-B row pieces of 16 rows per wave.
-__global__ __launch_bounds__(256) void patchify_kernel(const unsigned short* __restrict__ img, int in_kind,
-                                                       const unsigned short* __restrict__ noise,
-                                                       const float* __restrict__ t, float noise_scale, uint64_t seed,
-                                                       int B, int H, int W, bf16_t* __restrict__ out) {
+// lines) and write each piece to its patch row (per wave 4 runs of 256 B).
+// One 128-thread block per strip (blockIdx.x = strip, decoded once in scalar registers); a thread takes the strip's
+// pieces i = tid + 128 k (k < 3: 48 rows x 8 pieces of a full strip), all its image (and explicit-noise) loads issued
+// before any arithmetic. (The earlier grid-stride form decoded every piece's strip with 64-bit divisions by runtime
+// values and held one load in flight per thread: its integer index math and latency, not HBM, set its time.)
+constexpr int kPatchThreads = 128, kPatchPer = 96 * kStripP / kPatchThreads;
+__global__ __launch_bounds__(kPatchThreads) void patchify_kernel(const unsigned short* __restrict__ img, int in_kind,
+                                                                 const unsigned short* __restrict__ noise,
+                                                                 const float* __restrict__ t, float noise_scale,
+                                                                 uint64_t seed, int B, int H, int W,
+                                                                 bf16_t* __restrict__ out) {
   const int hp = H / 16, wp = W / 16;
-  const long strips = (long)B * hp * ((wp + kStripP - 1) / kStripP);
-  const long pieces = strips * 96 * kStripP;  // upper bound: partial strips leave their tail threads idle
+  const Strip st = strip_of(blockIdx.x, hp, wp);
+  const int cpr = st.np * 2;  // 16-B pieces per image row of the strip (8 for a full strip)
+  const long img0 = ((long)st.b * 3 * H + st.py * 16) * W + st.px0 * 16;  // (c = 0, ky = 0, strip column 0)
+  const long row0 = ((long)st.b * hp + st.py) * wp + st.px0;
+  uint4 v[kPatchPer], nv[kPatchPer];
+  long base[kPatchPer];
+  bool ok[kPatchPer];
+#pragma unroll
+  for (int k = 0; k < kPatchPer; ++k) {
+    const int i = threadIdx.x + k * kPatchThreads;
+    ok[k] = i < 48 * cpr;
+    const int rr = cpr == 8 ? i >> 3 : i / cpr, cc = i - rr * cpr, c = rr >> 4, ky = rr & 15;  // full strips: shifts
+    base[k] = img0 + ((long)c * H + ky) * W + cc * 8;
+    v[k] = ok[k] ? *reinterpret_cast<const uint4*>(img + base[k]) : make_uint4(0, 0, 0, 0);
+    nv[k] = ok[k] && in_kind == 0 && noise ? *reinterpret_cast<const uint4*>(noise + base[k]) : make_uint4(0, 0, 0, 0);
+  }
   const NoiseKey key = noise_key(seed);
-  for (long gid = (long)blockIdx.x * blockDim.x + threadIdx.x; gid < pieces; gid += (long)gridDim.x * blockDim.x) {
-    const Strip st = strip_of(gid / (96 * kStripP), hp, wp);
-    const int i = (int)(gid % (96 * kStripP));
-    const int cpr = st.np * 2;
-    if (i >= 48 * cpr) continue;
-    const int rr = i / cpr, cc = i - rr * cpr, c = rr >> 4, ky = rr & 15, pl = cc >> 1, kx0 = (cc & 1) * 8;
-    const long base = (((long)st.b * 3 + c) * H + st.py * 16 + ky) * W + st.px0 * 16 + cc * 8;
-    const uint4 v = *reinterpret_cast<const uint4*>(img + base);
-    const unsigned short* vs = reinterpret_cast<const unsigned short*>(&v);
+  const float tb = in_kind == 1 ? 0.f : t[st.b];
+#pragma unroll
+  for (int k = 0; k < kPatchPer; ++k) {
+    if (!ok[k]) continue;
+    const int i = threadIdx.x + k * kPatchThreads;
+    const int rr = cpr == 8 ? i >> 3 : i / cpr, cc = i - rr * cpr, c = rr >> 4, ky = rr & 15, pl = cc >> 1,
+              kx0 = (cc & 1) * 8;
+    const unsigned short* vs = reinterpret_cast<const unsigned short*>(&v[k]);
     float o[8];
     if (in_kind == 1) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = bf2f(vs[e]);
     } else {
-      const float tb = t[st.b];
       float nz[8];
       if (noise) {
-        const uint4 nv = *reinterpret_cast<const uint4*>(noise + base);
-        const unsigned short* ns = reinterpret_cast<const unsigned short*>(&nv);
+        const unsigned short* ns = reinterpret_cast<const unsigned short*>(&nv[k]);
 #pragma unroll
         for (int e = 0; e < 8; ++e) nz[e] = h2f(ns[e]);
       } else {
-        const uint32_t j0 = pair_counter((uint64_t)base);  // base is even (W, x multiples of 8)
+        const uint32_t j0 = pair_counter((uint64_t)base[k]);  // base is even (W, x multiples of 8)
 #pragma unroll
         for (int e = 0; e < 4; ++e) gauss_pair_fp16(key, j0 + e, nz[2 * e], nz[2 * e + 1]);
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = tb * h2f(vs[e]) + (1.f - tb) * h2f(f2h(nz[e] * noise_scale));
     }
-    const long row = ((long)st.b * hp + st.py) * wp + st.px0 + pl;
-    *reinterpret_cast<uint4*>(out + row * 768 + c * 256 + ky * 16 + kx0) = pack8(o);
+    *reinterpret_cast<uint4*>(out + (row0 + pl) * 768 + c * 256 + ky * 16 + kx0) = pack8(o);
   }
 }
 
@@ -744,8 +759,10 @@ extern "C" int vpt_patchify(const void* img, int in_kind, const void* noise, con
   VPT_CHECK_ARG(img && out && B > 0, "vpt_patchify: bad args");
   VPT_CHECK_ARG(H % 16 == 0 && W % 16 == 0, "vpt_patchify: H and W must be multiples of the 16-px patch");
   VPT_CHECK_ARG(in_kind == 1 || t, "vpt_patchify: noising needs t");
-  const long pieces = (long)B * (H / 16) * ((W / 16 + kStripP - 1) / kStripP) * 96 * kStripP;
-  hipLaunchKernelGGL(patchify_kernel, grid1(pieces), dim3(256), 0, (hipStream_t)stream, (const unsigned short*)img,
+  const long strips = (long)B * (H / 16) * ((W / 16 + kStripP - 1) / kStripP);
+  VPT_CHECK_ARG(strips < (1L << 31), "vpt_patchify: too many strips");
+  hipLaunchKernelGGL(patchify_kernel, dim3((unsigned)strips), dim3(kPatchThreads), 0, (hipStream_t)stream,
+                     (const unsigned short*)img,
                      in_kind, (const unsigned short*)noise, t, noise_scale, (uint64_t)seed, B, H, W, (bf16_t*)out);
   VPT_LAUNCH_CHECK();
   return VPT_OK;

@@ -317,7 +317,7 @@ class JiTEngine:
         delta = pool.get("delta", (B, Hh, rows), F32)
         n_dw = ops.attn_bwd_dw_rows(B, Hh, rows)
         qk_dw = pool.get("qk_dw_part", (n_dw, 128), F32)  # q_norm | k_norm weight-gradient partials
-        pre_zeroed = False
+        pre_zeroed = qk_zeroed = False
         scale = 1.0 / math.sqrt(cfg.head_dim)
         ck = st.get("ckpt", False)
         for i in reversed(range(cfg.depth)):
@@ -362,8 +362,11 @@ class JiTEngine:
                 qk_job = (qk_dw[:ops.attn_bwd_dw_rows(B, Hh, n_i)], w["gqk_norm"], acc)
             else:
                 dqk = pool.get("d_qk", (M, 2 * D))
-                if n_i < rows:
+                if n_i < rows and not qk_zeroed:
+                    # once, at the first pre-context block: the later (earlier-indexed) pre-context blocks never write
+                    # these rows, the post-context blocks before them wrote all rows
                     dqk.view(B, rows, 2 * D)[:, n_i:].zero_()
+                    qk_zeroed = True
                 ops.attn_bwd(*a5, ops._t4(dqk, B, rows, Hh, 0), ops._t4(dqk, B, rows, Hh, D),
                              ops._t4(dqkv, B, rows, Hh, 2 * D), B, Hh, rows, n_i, n_pre, scale)
                 qpart = ops.qknorm_rope_bwd(dqk, qkv, w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, rows, dqkv,
