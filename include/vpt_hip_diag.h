@@ -52,6 +52,8 @@ int vpt_attn_set_bwd_prefetch(int mask);
 /* Attention backward partner waves: bit 0 = s_setprio 1 for the odd-slot wave of each SIMD, bit 1 = its block starts
    (v >> 2) x 10 ns late; 0 = production. */
 int vpt_attn_set_bwd_partner(int v);
+/* QK-norm attention forward: row sums as a third MFMA block (1) or as f32 adds (0, production). */
+int vpt_attn_set_fwd_lsum(int on);
 int vpt_gemm_set_swb_one_group(int on);
 /* SwiGLU-backward ring GEMM timing ablations (WRONG results): 0 off, 3 = no epilogue, 4 = dx12 stores dropped,
    6 = every item's x12 operands from the first tile (L2-resident). */

@@ -71,12 +71,16 @@ int g_xcd = 1;      // block order of the forward / backward grids (vpt_attn_set
 int g_rows64 = 0;   // backward variants (vpt_attn_set_rows64 bit mask, A/B): 1 = 64-key dK/dV, 2 = 64-query dQ
                     // at 2 waves / SIMD, 4 = 64-query dQ at 1 wave / SIMD; 0 = the 32-row pair
 int g_pm = 0;       // backward partner-wave priority / stagger (vpt_attn_set_bwd_partner, A/B)
+int g_fwd_lsm = 0;  // QK-norm forward: row sums on the MFMA pipe (vpt_attn_set_fwd_lsum, A/B)
 #else
 constexpr int g_variant = 0, g_waves = 4;
 constexpr float g_tau = kTau;
 // XCD-contiguous block order (r04s: -1.1 % fwd, -1.8 % bwd, 4x less HBM traffic; +0.38 % per C3 step, r04t) and the
 // forward's S^T chain with its K fragments read first (+0.32 % per C3 step, r04t)
 constexpr int g_xcd = 1, g_fwd_ord = 1;
+// The QK-norm forward's row sums on the MFMA pipe (fwd_body LSM): forward +3.3 %, C3 step -0.49 % (r05n) -- the loop is
+// not VALU-issue bound, and the extra MFMAs cost more than the 32 adds per tile they replace. Off.
+constexpr int g_fwd_lsm = 0;
 #endif
 
 // Reductions over the lane pair (l, l^32) with v_permlane32_swap (VALU, no LDS round trip): the two
@@ -393,9 +397,13 @@ constexpr float kFixMax = 60.f;
 
 // ORD: the S^T chain's 8 K fragments read from LDS before its MFMAs (one counted wait each), instead of hipcc's
 // read-wait-MFMA order in one register quad (which exposes the LDS latency at every MFMA of the chain).
-template <int NW, bool FIX, bool ORD = false>
+// LSM (with FIX; diagnostic A/B, off in production): the row sums l = sum_k p out of the MFMA pipe as a third O^T block,
+// ones . P^T, from the same bf16 P the PV product uses (4 MFMAs per tile in place of 32 v_add_f32 per lane) --
+// o = sum_k bf16(p) v / sum_k bf16(p). Measured slower (g_fwd_lsm).
+template <int NW, bool FIX, bool ORD = false, bool LSM = false>
 __device__ __forceinline__ void fwd_body(const AttnArgs& g, float bound, char (&lds)[2][2][8192], float* kbl, int bx,
                                          int hd, int b) {
+  static_assert(!LSM || FIX, "MFMA row sums with the fixed reference point only");
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5;
   const int q0 = bx * (32 * NW) + wid * 32;
   const bf16_t* Q = g.q.p + b * g.q.sb + hd * g.q.sh;
@@ -405,9 +413,10 @@ __device__ __forceinline__ void fwd_body(const AttnArgs& g, float bound, char (&
   bf16x8 qf[4];  // pre-scaled query: K.Q^T is already in log2 units
   load_row_frags(qf, Q, g.q.sr, q0 + (lane & 31), g.n, lane);
 
-  floatx16 oacc[2];
+  floatx16 oacc[2], lacc;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) { oacc[0][i] = 0.f; oacc[1][i] = 0.f; }
+  for (int i = 0; i < 16; ++i) { oacc[0][i] = 0.f; oacc[1][i] = 0.f; lacc[i] = 0.f; }
+  const bf16x8 ones = as_frag(make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u));
   float m_c = FIX ? bound : 0.f, lsum = 0.f;  // reference point (log2 units), row sum
   floatx16 nm = splat16(-m_c);  // -m_c: the S^T chain's initial accumulator, so it ends at S - m_c
 
@@ -497,9 +506,9 @@ __device__ __forceinline__ void fwd_body(const AttnArgs& g, float bound, char (&
       for (int i = 0; i < 16; ++i) {
         const float p = __builtin_amdgcn_exp2f(sacc[kb][i]);
         sacc[kb][i] = p;
-        ps += p;
+        if (!LSM) ps += p;
       }
-    lsum += ps;
+    if (!LSM) lsum += ps;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -507,19 +516,20 @@ __device__ __forceinline__ void fwd_body(const AttnArgs& g, float bound, char (&
         const bf16x8 pf = pack_acc(sacc[kb], s);
 #pragma unroll
         for (int db = 0; db < 2; ++db) oacc[db] = mfma32(frag_tr(lv, db, 2 * kb + s, lane), pf, oacc[db]);
+        if (LSM) lacc = mfma32(ones, pf, lacc);
       }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of the next tile landed
     __syncthreads();                                    // ... and every wave's; this tile fully read
     cur ^= 1;
   }
-  const float l = pair_sum(lsum);
+  const float l = LSM ? lacc[0] : pair_sum(lsum);  // LSM: every register of the lane holds its query's sum
   const float inv = 1.f / l;
   const int qrow = q0 + (lane & 31);
   store_T(g.o, (long)b * g.o.sb + hd * g.o.sh, oacc, inv, qrow, g.n, lane, false);
   if (lane < 32 && qrow < g.n) g.lse[b * g.l_sb + hd * g.l_sh + qrow] = -(m_c + __log2f(l));  // -LSE, log2
 }
 
-template <int NW, bool QKN = false, bool ORD = false>
+template <int NW, bool QKN = false, bool ORD = false, bool LSM = false>
 __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][8192];
   extern __shared__ __attribute__((aligned(16))) float kbl[];  // key bias of keys kb0.. (fill_key_bias)
@@ -537,7 +547,7 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnArgs g) {
     const float aq = fabsf(bf2f(g.wq[lane])), ak = fabsf(bf2f(g.wk[lane]));
     const float bound = g.scale_log2 * 64.f * wave_max(aq) * wave_max(ak) * 1.0625f;
     if (bound < kFixMax) {
-      fwd_body<NW, true, ORD>(g, bound, lds, kbl, bx, hd, b);
+      fwd_body<NW, true, ORD, LSM>(g, bound, lds, kbl, bx, hd, b);
       return;
     }
   }
@@ -1106,7 +1116,10 @@ extern "C" int vpt_attn_fwd_qknorm(const void* q, long q_sb, long q_sh, long q_s
   g.tau = g_tau;
   g.kb0 = g.n_dense / 64 * 64;
   g.wq = (const bf16_t*)wq; g.wk = (const bf16_t*)wk;
-  if (g_fwd_ord)
+  if (g_fwd_ord && g_fwd_lsm)
+    hipLaunchKernelGGL((attn_fwd_kernel<4, true, true, true>), dim3((n + 127) / 128, H, B), dim3(256),
+                       key_bias_lds_bytes(g), (hipStream_t)stream, g);
+  else if (g_fwd_ord)
     hipLaunchKernelGGL((attn_fwd_kernel<4, true, true>), dim3((n + 127) / 128, H, B), dim3(256), key_bias_lds_bytes(g),
                        (hipStream_t)stream, g);
   else
