@@ -37,6 +37,9 @@ def main():
             "ATTN_XCD": lambda on: _lib.lib.vpt_attn_set_xcd_order(1 if on else 0),
             "ATTN_FWD_ORD": lambda on: _lib.lib.vpt_attn_set_fwd_order(1 if on else 0),
             "ATTN_FWD_LSUM": lambda on: _lib.lib.vpt_attn_set_fwd_lsum(1 if on else 0),
+            "ATTN_BWD_MF16": lambda on: _lib.lib.vpt_attn_set_bwd_mfma16(3 if on else 0),
+            "ATTN_BWD_MF16_KV": lambda on: _lib.lib.vpt_attn_set_bwd_mfma16(1 if on else 0),
+            "ATTN_BWD_MF16_Q": lambda on: _lib.lib.vpt_attn_set_bwd_mfma16(2 if on else 0),
             "ATTN_DQ_ORD": lambda on: _lib.lib.vpt_attn_set_rows64(16 if on else 0),
             "ATTN_PF_KV": lambda on: _lib.lib.vpt_attn_set_bwd_prefetch(1 if on else 0),
             "ATTN_PF_Q": lambda on: _lib.lib.vpt_attn_set_bwd_prefetch(2 if on else 0),

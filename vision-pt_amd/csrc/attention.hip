@@ -72,6 +72,7 @@ int g_rows64 = 0;   // backward variants (vpt_attn_set_rows64 bit mask, A/B): 1 
                     // at 2 waves / SIMD, 4 = 64-query dQ at 1 wave / SIMD; 0 = the 32-row pair
 int g_pm = 0;       // backward partner-wave priority / stagger (vpt_attn_set_bwd_partner, A/B)
 int g_fwd_lsm = 0;  // QK-norm forward: row sums on the MFMA pipe (vpt_attn_set_fwd_lsum, A/B)
+int g_mf16 = 0;     // backward bodies on the 16x16x32 MFMA (vpt_attn_set_bwd_mfma16 bit mask, A/B)
 #else
 constexpr int g_variant = 0, g_waves = 4;
 constexpr float g_tau = kTau;
@@ -95,6 +96,18 @@ __device__ __forceinline__ float pair_sum(float v) {
 }
 
 __device__ __forceinline__ int sigma(int r) { return ((r >> 1) & 7) ^ ((r & 2) << 1); }
+// The 16x16x32 bodies' tile image (dkdv16_body / dq16_body): chunk c of row r at position c ^ (r & 6). Conflict-free for
+// their ds_read_b128 row fragments (row 16t + (lane & 15), chunk 4ks + (lane >> 4): per lane group of the b128 read the
+// 8 even rows -- and the 8 odd ones -- take 8 distinct slots) and their transposed ds_read_b64_tr_b16 reads (rows
+// r0 + 4(lane >> 4) + 0..3 of units 4dt + 0..3: per 32 lanes, rows r0..r0+7 in 8 distinct chunk pairs). The 32x32
+// bodies' sigma is 2-way conflicted on the 16-row pattern.
+__device__ __forceinline__ int sigma16(int r) { return r & 6; }
+template <int SW>
+__device__ __forceinline__ int sig(int r) { return SW ? sigma16(r) : sigma(r); }
+__device__ __forceinline__ int tile16_off(int row, int chunk) { return row * 128 + ((chunk ^ sigma16(row)) << 4); }
+__device__ __forceinline__ int tile16_unit_off(int row, int unit) {
+  return row * 128 + (((unit >> 1) ^ sigma16(row)) << 4) + ((unit & 1) << 3);
+}
 __device__ __forceinline__ int tile_off(int row, int chunk) { return row * 128 + ((chunk ^ sigma(row)) << 4); }
 __device__ __forceinline__ int tile_unit_off(int row, int unit) {
   return row * 128 + (((unit >> 1) ^ sigma(row)) << 4) + ((unit & 1) << 3);
@@ -147,19 +160,19 @@ struct RowPlan {
   uint32_t voff[8 / NW];
   uint32_t wq;  // this wave's first piece within a tile image (bytes)
 };
-template <int NW>
+template <int NW, int SW = 0>
 __device__ __forceinline__ RowPlan<NW> row_plan(long sr, int wid, int lane) {
   RowPlan<NW> p;
 #pragma unroll
   for (int i = 0; i < 8 / NW; ++i) {
     const int q = (8 / NW) * wid + i, row = 8 * q + (lane >> 3);
-    const int c = (lane & 7) ^ sigma(row);
+    const int c = (lane & 7) ^ sig<SW>(row);
     p.voff[i] = (uint32_t)((row * (int)sr + c * 8) * 2);
   }
   p.wq = __builtin_amdgcn_readfirstlane((uint32_t)((8 / NW) * wid * 1024));
   return p;
 }
-template <int NW>
+template <int NW, int SW = 0>
 __device__ __forceinline__ void dma_rows_at(uint32_t lds_tile, const void* head, long sr, int r0, int n,
                                             const RowPlan<NW>& p, int wid, int lane) {
   if (r0 + 64 <= n) {
@@ -170,7 +183,7 @@ __device__ __forceinline__ void dma_rows_at(uint32_t lds_tile, const void* head,
 #pragma unroll
     for (int i = 0; i < 8 / NW; ++i) {
       const int q = (8 / NW) * wid + i, row = 8 * q + (lane >> 3);
-      const int c = (lane & 7) ^ sigma(row);
+      const int c = (lane & 7) ^ sig<SW>(row);
       const int r = min(r0 + row, n - 1);
       dma_x4(head, (uint32_t)(((long)r * sr + c * 8) * 2), lds_tile + p.wq + i * 1024);
     }
@@ -201,6 +214,39 @@ __device__ __forceinline__ bf16x8 frag_tr(const char* lds, int db, int s16, int 
   uint2 lo = lds_read_tr16((const VPT_LDS void*)(lds + tile_unit_off(row, unit)));
   uint2 hi = lds_read_tr16((const VPT_LDS void*)(lds + tile_unit_off(row + 8, unit)));
   return as_frag2(lo, hi);
+}
+// 16x16x32 operands from a tile16 image. Rows: lane row = rbase + (lane&15), k = 32ks + 8(lane>>4) + j.
+__device__ __forceinline__ bf16x8 frag16_rows(const char* lds, int rbase, int ks, int lane) {
+  return as_frag(*reinterpret_cast<const uint4*>(lds + tile16_off(rbase + (lane & 15), 4 * ks + (lane >> 4))));
+}
+// Transposed: lane row = head dim 16dt + (lane&15); k slot j of lane group G = lane>>4 is tile row
+// 32m + 16(j>>2) + 4G + (j&3) -- the order in which two row-adjacent 16x16 accumulators (rows 4G + e) pack.
+__device__ __forceinline__ bf16x8 frag16_tr(const char* lds, int dt, int m, int lane) {
+  const int i16 = lane & 15, row = 32 * m + 4 * (lane >> 4) + (i16 >> 2), unit = 4 * dt + (i16 & 3);
+  uint2 lo = lds_read_tr16((const VPT_LDS void*)(lds + tile16_unit_off(row, unit)));
+  uint2 hi = lds_read_tr16((const VPT_LDS void*)(lds + tile16_unit_off(row + 16, unit)));
+  return as_frag2(lo, hi);
+}
+__device__ __forceinline__ floatx4 mfma16(bf16x8 a, bf16x8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// Two row-adjacent 16x16 accumulators (rows 4G + e and 16 + 4G + e) as one bf16 operand (k slots as frag16_tr).
+__device__ __forceinline__ bf16x8 pack16(const floatx4& a, const floatx4& b) {
+  uint4 v;
+  v.x = pack_bf16x2(a[0], a[1]);
+  v.y = pack_bf16x2(a[2], a[3]);
+  v.z = pack_bf16x2(b[0], b[1]);
+  v.w = pack_bf16x2(b[2], b[3]);
+  return as_frag(v);
+}
+// B operand held in registers for row `row` of a global tensor: lane col = row, d = 32ks + 8(lane>>4) + j.
+__device__ __forceinline__ void load_row_frags16(bf16x8 (&f)[2], const bf16_t* base, long sr, int row, int n, int lane) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (row < n) v = *reinterpret_cast<const uint4*>(base + (long)row * sr + 32 * ks + 8 * (lane >> 4));
+    f[ks] = as_frag(v);
+  }
 }
 // B-operand held in registers for a row of a global tensor: lane col = row (lane&31),
 // elements d = 16s + 8h + j.
@@ -266,6 +312,21 @@ __device__ __forceinline__ void store_T(const OTensor4& t, long base_off, const 
       if (zero) w = make_uint2(0u, 0u);
       *reinterpret_cast<uint2*>(dst + d) = w;
     }
+}
+// store_T for four transposed 16x16 accumulators of one row (16x16x32 bodies): register e of acc[dt] of lane l holds
+// dim 16dt + 4(l>>4) + e of the lane's row.
+__device__ __forceinline__ void store16_T(const OTensor4& t, long base_off, const floatx4 (&acc)[4], float mul, int row,
+                                          int n, int lane, bool zero) {
+  if (row >= n) return;
+  bf16_t* dst = t.p + base_off + (long)row * t.sr + 4 * (lane >> 4);
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    uint2 w;
+    w.x = pack_bf16x2(acc[dt][0] * mul, acc[dt][1] * mul);
+    w.y = pack_bf16x2(acc[dt][2] * mul, acc[dt][3] * mul);
+    if (zero) w = make_uint2(0u, 0u);
+    *reinterpret_cast<uint2*>(dst + 16 * dt) = w;
+  }
 }
 
 // ---- fused QK-RMSNorm + RoPE backward of one q / k row (JiT Attention.q_norm / k_norm + apply_rope,
@@ -796,6 +857,128 @@ __device__ __forceinline__ void dkdv_body(const AttnArgs& g, int bx, int hd, int
                      g.dwk + ((long)(b * g.H + hd) * ((g.nk + 32 * NW - 1) / (32 * NW)) + bx) * g.dw_ld, tid);
 }
 
+// dK/dV body on the 16x16x32 MFMA (diagnostic A/B against dkdv_body's 32x32x16: the same 32 keys per wave, 64-query
+// tiles, products, LDS bytes and VALU; guide MI355X_MICROARCH 'DVFS give-back' item 7: under load the chip can hold a
+// higher clock on one MFMA shape than on the other). Per tile and 32-query half m: S and dP as 2 x 2 accumulators
+// (query tile u, key tile kt) of 2 K steps, P = exp2(S), dS = P dP packed per key tile into one 32-query operand
+// (pack16), then dV^T / dK^T (head-dim tile dt x key tile kt) += dO^T / Q^T (frag16_tr) x P / dS. Self-attention
+// inputs without the fused QK-norm epilogue (g.qkn == 0).
+template <int NW>
+__device__ __forceinline__ void dkdv16_body(const AttnArgs& g, int bx, int hd, int b, char (&lds)[2][2][8192],
+                                            float (&lstat)[2][2][64]) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, G = lane >> 4;
+  const int k0 = bx * (32 * NW) + wid * 32;
+  const bf16_t* Q = g.q.p + b * g.q.sb + hd * g.q.sh;
+  const bf16_t* dO = g.dO.p + b * g.dO.sb + hd * g.dO.sh;
+  const float* LSE = g.lse + b * g.l_sb + hd * g.l_sh;
+  const float* DEL = g.delta_in + b * g.l_sb + hd * g.l_sh;
+
+  bf16x8 kf[2][2], vf[2][2];
+  bool kmasked[2];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int key = k0 + 16 * kt + (lane & 15);
+    load_row_frags16(kf[kt], g.k.p + b * g.k.sb + hd * g.k.sh, g.k.sr, key, g.nk, lane);
+    load_row_frags16(vf[kt], g.v.p + b * g.v.sb + hd * g.v.sh, g.v.sr, key, g.nk, lane);
+    kmasked[kt] = key_bias(g, b, key) == kNegInf;
+  }
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): as in dkdv_body
+
+  floatx4 dv[2][4], dk[2][4];  // [kt][dt]
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { dv[kt][dt][e] = 0.f; dk[kt][dt][e] = 0.f; }
+
+  const int nt = (g.n + 63) / 64;
+  const void* Qu = uniform_ptr(Q);
+  const void* Du = uniform_ptr(dO);
+  const void* Lu = uniform_ptr(LSE);
+  const void* Eu = uniform_ptr(DEL);
+  const uint32_t lb = lds_addr(&lds[0][0][0]);
+  const RowPlan<NW> pq = row_plan<NW, 1>(g.q.sr, wid, lane), pd0 = row_plan<NW, 1>(g.dO.sr, wid, lane);
+  auto stage = [&](int buf, int r0) {
+    dma_rows_at<NW, 1>(lb + buf * 16384, Qu, g.q.sr, r0, g.n, pq, wid, lane);
+    dma_rows_at<NW, 1>(lb + buf * 16384 + 8192, Du, g.dO.sr, r0, g.n, pd0, wid, lane);
+    if (wid == 0) dma_stat(lstat[buf][0], Lu, r0, g.n, lane);
+    else if (wid == 1) dma_stat(lstat[buf][1], Eu, r0, g.n, lane);
+  };
+  auto settle = [&](int buf, int r0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (g.n - r0 < 64) {  // padding query rows zeroed: no dK / dV contribution
+      zero_rows<NW>(lds[buf][0], g.n - r0, tid);
+      zero_rows<NW>(lds[buf][1], g.n - r0, tid);
+      __syncthreads();
+    }
+  };
+  stage(0, 0);
+  settle(0, 0);
+
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    const bool more = t + 1 < nt;
+    if (more) stage(cur ^ 1, (t + 1) * 64);
+    const char* lq = lds[cur][0];
+    const char* ld = lds[cur][1];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      floatx4 s[2][2], dp[2][2];  // [u][kt]: query rows 32m + 16u + 4G + e, key 16kt + (lane & 15)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const floatx4 cs = *reinterpret_cast<const floatx4*>(&lstat[cur][0][32 * m + 16 * u + 4 * G]);
+        const floatx4 cd = *reinterpret_cast<const floatx4*>(&lstat[cur][1][32 * m + 16 * u + 4 * G]);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) { s[u][kt] = cs; dp[u][kt] = cd; }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 qa = frag16_rows(lq, 32 * m + 16 * u, ks, lane);
+          const bf16x8 da = frag16_rows(ld, 32 * m + 16 * u, ks, lane);
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            s[u][kt] = mfma16(qa, kf[kt][ks], s[u][kt]);
+            dp[u][kt] = mfma16(da, vf[kt][ks], dp[u][kt]);
+          }
+        }
+      }
+      bf16x8 pp[2], pd[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        floatx4 P[2], dS[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float p = __builtin_amdgcn_exp2f(s[u][kt][e]);
+            P[u][e] = p;
+            dS[u][e] = p * dp[u][kt][e];
+          }
+        pp[kt] = pack16(P[0], P[1]);
+        pd[kt] = pack16(dS[0], dS[1]);
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 tv = frag16_tr(ld, dt, m, lane);
+        const bf16x8 tq = frag16_tr(lq, dt, m, lane);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          dv[kt][dt] = mfma16(tv, pp[kt], dv[kt][dt]);
+          dk[kt][dt] = mfma16(tq, pd[kt], dk[kt][dt]);
+        }
+      }
+    }
+    if (more) settle(cur ^ 1, (t + 1) * 64);
+  }
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int key = k0 + 16 * kt + (lane & 15);
+    store16_T(g.dv, (long)b * g.dv.sb + hd * g.dv.sh, dv[kt], 1.f, key, g.nk, lane, kmasked[kt]);
+    store16_T(g.dk, (long)b * g.dk.sb + hd * g.dk.sh, dk[kt], 0.69314718055994531f, key, g.nk, lane, kmasked[kt]);
+  }
+}
+
 // ------------------------------------------------------------------ backward dQ
 // Body of one dQ block (query block bx of head hd, batch b); lds = [buf][K / V] tiles, kbl = key bias of keys kb0..
 template <int ABL, int NW, int NST = 2>
@@ -984,6 +1167,110 @@ __device__ __forceinline__ void dq_body(const AttnArgs& g, int bx, int hd, int b
                      dwp, g.dwq + ((long)(b * g.H + hd) * ((g.n + 32 * NW - 1) / (32 * NW)) + bx) * g.dw_ld, tid);
 }
 
+// dQ body on the 16x16x32 MFMA (diagnostic A/B against dq_body, as dkdv16_body): 32 queries per wave as two query
+// tiles qt on the lanes; per key tile and 32-key half m, S^T / dP^T as 2 x 2 accumulators (key tile u, query tile qt)
+// started at -LSE / -delta of the lane's query, the key bias on the context / padding tiles, dS^T packed per query tile,
+// dQ^T (head-dim tile dt x query tile qt) += K^T (frag16_tr) x dS^T. Without the fused QK-norm epilogue.
+template <int NW>
+__device__ __forceinline__ void dq16_body(const AttnArgs& g, int bx, int hd, int b, char (&lds)[2][2][8192], float* kbl) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, G = lane >> 4;
+  const int q0 = bx * (32 * NW) + wid * 32;
+  const bf16_t* K = g.k.p + b * g.k.sb + hd * g.k.sh;
+  const bf16_t* V = g.v.p + b * g.v.sb + hd * g.v.sh;
+
+  bf16x8 qf[2][2], df[2][2];
+  float nlse[2], ndel[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qrow = q0 + 16 * qt + (lane & 15);
+    load_row_frags16(qf[qt], g.q.p + b * g.q.sb + hd * g.q.sh, g.q.sr, qrow, g.n, lane);
+    load_row_frags16(df[qt], g.dO.p + b * g.dO.sb + hd * g.dO.sh, g.dO.sr, qrow, g.n, lane);
+    const long lo = b * g.l_sb + hd * g.l_sh + qrow;
+    nlse[qt] = qrow < g.n ? g.lse[lo] : -__builtin_huge_valf();
+    ndel[qt] = qrow < g.n ? g.delta_in[lo] : 0.f;
+  }
+  floatx4 dq[2][4];  // [qt][dt]
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dq[qt][dt][e] = 0.f;
+
+  const int nt = (g.nk + 63) / 64;
+  const void* Ku = uniform_ptr(K);
+  const void* Vu = uniform_ptr(V);
+  fill_key_bias<NW>(kbl, g, b, tid);
+  const uint32_t lb = lds_addr(&lds[0][0][0]);
+  const RowPlan<NW> pk = row_plan<NW, 1>(g.k.sr, wid, lane), pv = row_plan<NW, 1>(g.v.sr, wid, lane);
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): as in dq_body
+  dma_rows_at<NW, 1>(lb, Ku, g.k.sr, 0, g.nk, pk, wid, lane);
+  dma_rows_at<NW, 1>(lb + 8192, Vu, g.v.sr, 0, g.nk, pv, wid, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int t = 0; t < nt; ++t) {
+    const int kv0 = t * 64;
+    const int cur = t & 1;
+    if (t + 1 < nt) {
+      dma_rows_at<NW, 1>(lb + (cur ^ 1) * 16384, Ku, g.k.sr, kv0 + 64, g.nk, pk, wid, lane);
+      dma_rows_at<NW, 1>(lb + (cur ^ 1) * 16384 + 8192, Vu, g.v.sr, kv0 + 64, g.nk, pv, wid, lane);
+    }
+    const char* lk = lds[cur][0];
+    const char* lv = lds[cur][1];
+    const bool dense = kv0 + 64 <= g.n_dense;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      floatx4 s[2][2], dp[2][2];  // [u][qt]: key rows 32m + 16u + 4G + e, query 16qt + (lane & 15)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { s[u][qt][e] = nlse[qt]; dp[u][qt][e] = ndel[qt]; }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 ka = frag16_rows(lk, 32 * m + 16 * u, ks, lane);
+          const bf16x8 va = frag16_rows(lv, 32 * m + 16 * u, ks, lane);
+#pragma unroll
+          for (int qt = 0; qt < 2; ++qt) {
+            s[u][qt] = mfma16(ka, qf[qt][ks], s[u][qt]);
+            dp[u][qt] = mfma16(va, df[qt][ks], dp[u][qt]);
+          }
+        }
+        if (!dense) {  // scalar branch: only the context / padding key tiles carry a bias
+          const floatx4 bias = *reinterpret_cast<const floatx4*>(&kbl[kv0 - g.kb0 + 32 * m + 16 * u + 4 * G]);
+#pragma unroll
+          for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s[u][qt][e] += bias[e];
+        }
+      }
+      bf16x8 pd[2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        floatx4 dS[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dS[u][e] = __builtin_amdgcn_exp2f(s[u][qt][e]) * dp[u][qt][e];
+        pd[qt] = pack16(dS[0], dS[1]);
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 tk = frag16_tr(lk, dt, m, lane);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) dq[qt][dt] = mfma16(tk, pd[qt], dq[qt][dt]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+    store16_T(g.dq, (long)b * g.dq.sb + hd * g.dq.sh, dq[qt], g.scale, q0 + 16 * qt + (lane & 15), g.n, lane, false);
+}
+
 // The production backward as ONE launch over both block kinds: the dK/dV blocks first (the longer ones),
 // then the dQ blocks. Each kind alone is 3,168 equal blocks at B=8 1024^2 on 512 block slots (2 per CU):
 // 6.19 waves of work run as 7, twice. In one grid the dQ blocks start on the slots the dK/dV tail frees,
@@ -1026,8 +1313,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs g, int nkb, i
     bx = kv ? bid % nkb : bid % nqb;
     r = kv ? bid / nkb : bid / nqb;
   }
-  if (kv) dkdv_body<DKDV, 4, NST>(g, bx, r % g.H, r / g.H, lds, lstat);
-  else dq_body<DQ, 4, NST>(g, bx, r % g.H, r / g.H, lds, kbl, &lstat[0][0][0]);
+  static_assert((DKDV != 16 && DQ != 16) || NST == 2, "16x16x32 bodies: two-stage ring");
+  if (kv) {
+    if constexpr (DKDV == 16) dkdv16_body<4>(g, bx, r % g.H, r / g.H, lds, lstat);
+    else dkdv_body<DKDV, 4, NST>(g, bx, r % g.H, r / g.H, lds, lstat);
+  } else {
+    if constexpr (DQ == 16) dq16_body<4>(g, bx, r % g.H, r / g.H, lds, kbl);
+    else dq_body<DQ, 4, NST>(g, bx, r % g.H, r / g.H, lds, kbl, &lstat[0][0][0]);
+  }
 }
 constexpr int kDqBody = 0;  // production dQ body (0 = compiler-scheduled, 8 = explicitly ordered)
 // production dK/dV body: the explicitly ordered body without s_setprio around its MFMA groups (10); with them (8) the
@@ -1265,6 +1558,18 @@ int attn_bwd_impl(AttnArgs& g, int B, int H, int n, int nk, hipStream_t s) {
   }
 #endif
 #ifdef VPT_DIAG
+  if (g_mf16 && !g.qkn) {  // A/B: the 16x16x32 dK/dV (bit 1) / dQ (bit 2) bodies
+    const dim3 grid((nkb + nqb) * H * B);
+    const size_t kbl_bytes = key_bias_lds_bytes(g);
+    if (g_mf16 == 1)
+      hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, 16>), grid, dim3(256), kbl_bytes, s, g, nkb, nqb, B);
+    else if (g_mf16 == 2)
+      hipLaunchKernelGGL((attn_bwd_kernel<16, kDkdvBody>), grid, dim3(256), kbl_bytes, s, g, nkb, nqb, B);
+    else
+      hipLaunchKernelGGL((attn_bwd_kernel<16, 16>), grid, dim3(256), kbl_bytes, s, g, nkb, nqb, B);
+    VPT_LAUNCH_CHECK();
+    return VPT_OK;
+  }
   if (g_bwd_pf) {  // A/B: transposed-fragment prefetch in the dK/dV (bit 1) / dQ (bit 2) products
     const dim3 grid((nkb + nqb) * H * B);
     if (g_bwd_pf == 4)  // the ordered dK/dV body WITH s_setprio around its MFMA groups (the previous production body)
