@@ -54,8 +54,11 @@ int vpt_attn_set_bwd_prefetch(int mask);
 int vpt_attn_set_bwd_partner(int v);
 /* QK-norm attention forward: row sums as a third MFMA block (1) or as f32 adds (0, production). */
 int vpt_attn_set_fwd_lsum(int on);
-// Backward bodies on the 16x16x32 MFMA: bit 1 dK/dV, bit 2 dQ (0 = production 32x32x16; not with the fused QK-norm).
+// Backward bodies on the 16x16x32 MFMA: bit 1 dK/dV, bit 2 dQ, 7 = both with the ordered dK/dV body (production);
+// 0 = the 32x32x16 bodies. Not with the fused QK-norm backward.
 int vpt_attn_set_bwd_mfma16(int mask);
+// The QK-norm forward's fixed-reference body on the 16x16x32 MFMA (0 = production 32x32x16).
+int vpt_attn_set_fwd_mfma16(int on);
 int vpt_gemm_set_swb_one_group(int on);
 /* SwiGLU-backward ring GEMM timing ablations (WRONG results): 0 off, 3 = no epilogue, 4 = dx12 stores dropped,
    6 = every item's x12 operands from the first tile (L2-resident). */

@@ -503,7 +503,9 @@ def test_attention_bwd_fused_qknorm_rope(ops, n, n_dense, masked):
     p2 = ops.qknorm_rope_bwd(dqk, qkv, wq, wk, cos, sin, rows, dqkv2)
     g2 = dqkv2.float().view(B, rows, 3 * D)
     assert rel(got[:, :n, :2 * D], g2[:, :n, :2 * D]) < 1e-2
-    assert torch.equal(got[:, :n, 2 * D:], g2[:, :n, 2 * D:])  # dV is the same kernel path
+    # dV: the unfused backward runs the 16x16x32 bodies, the fused one the 32x32x16 pair (its epilogue reads that
+    # accumulator layout) -- the same products in another summation order
+    assert rel(got[:, :n, 2 * D:], g2[:, :n, 2 * D:]) < 2e-3
     assert p2 is not None
 
 

@@ -40,6 +40,9 @@ def main():
             "ATTN_BWD_MF16": lambda on: _lib.lib.vpt_attn_set_bwd_mfma16(3 if on else 0),
             "ATTN_BWD_MF16_KV": lambda on: _lib.lib.vpt_attn_set_bwd_mfma16(1 if on else 0),
             "ATTN_BWD_MF16_Q": lambda on: _lib.lib.vpt_attn_set_bwd_mfma16(2 if on else 0),
+            "ATTN_BWD_MF16_ORD": lambda on: _lib.lib.vpt_attn_set_bwd_mfma16(7 if on else 0),
+            "ATTN_BWD_MF16_UNORD": lambda on: _lib.lib.vpt_attn_set_bwd_mfma16(3 if on else 7),
+            "ATTN_FWD_MF16": lambda on: _lib.lib.vpt_attn_set_fwd_mfma16(1 if on else 0),
             "ATTN_DQ_ORD": lambda on: _lib.lib.vpt_attn_set_rows64(16 if on else 0),
             "ATTN_PF_KV": lambda on: _lib.lib.vpt_attn_set_bwd_prefetch(1 if on else 0),
             "ATTN_PF_Q": lambda on: _lib.lib.vpt_attn_set_bwd_prefetch(2 if on else 0),

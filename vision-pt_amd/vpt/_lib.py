@@ -132,6 +132,7 @@ DIAG_SIGNATURES: dict[str, list] = {
     "vpt_attn_set_bwd_partner": [I],
     "vpt_attn_set_fwd_lsum": [I],
     "vpt_attn_set_bwd_mfma16": [I],
+    "vpt_attn_set_fwd_mfma16": [I],
     "vpt_gemm_set_swb_one_group": [I],
     "vpt_gemm_set_swb_ablation": [I],
     "vpt_gemm_set_r2": [I],
