@@ -25,7 +25,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--setter", default="vpt_attn_set_xcd_order")
-    ap.add_argument("--value", type=int, default=1, help="the B value (A = 0)")
+    ap.add_argument("--value", type=int, default=1, help="the B value")
+    ap.add_argument("--base", type=int, default=0, help="the A value")
     args = ap.parse_args()
     _lib.use_diag()
     setter = getattr(_lib.lib, args.setter)
@@ -60,7 +61,7 @@ def main():
 
     outs = {}
     for x in (0, 1):
-        setter(x * args.value)
+        setter(args.value if x else args.base)
         fwd()
         bwd()
         torch.cuda.synchronize()
@@ -74,7 +75,7 @@ def main():
     res = {f"{k}{x}": [] for k in ("fwd", "bwd") for x in (0, 1)}
     for r in range(args.rounds):
         for x in ((0, 1) if r % 2 == 0 else (1, 0)):
-            setter(x * args.value)
+            setter(args.value if x else args.base)
             for name, fn in (("fwd", fwd), ("bwd", bwd)):
                 fn()
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.iters + 1)]
@@ -85,8 +86,8 @@ def main():
                 torch.cuda.synchronize()
                 res[f"{name}{x}"].append(statistics.median(ev[i].elapsed_time(ev[i + 1]) for i in range(args.iters)))
     med = {k: round(statistics.median(v), 4) for k, v in res.items()}
-    setter(0)
-    print(json.dumps({"setter": args.setter, "value": args.value, "bitwise_equal": equal,
+    setter(args.base)
+    print(json.dumps({"setter": args.setter, "value": args.value, "base": args.base, "bitwise_equal": equal,
                       "rel_l2_1_vs_0": {k: float(f"{v:.3g}") for k, v in rel.items()}, "median_ms": med,
                       "fwd_1_vs_0": round(med["fwd1"] / med["fwd0"], 4),
                       "bwd_1_vs_0": round(med["bwd1"] / med["bwd0"], 4)}), flush=True)

@@ -54,7 +54,7 @@ def case(n, nk, n_dense, masked, B=2, H=3):
     ref = torch.einsum("bhqk,bhkd->bhqd", torch.softmax(s, -1), vf)
     ref.backward(heads(do, rq, 0, n))
     out = {}
-    for mask in (0, 1, 2, 3, 7):
+    for mask in (0, 1, 2, 3, 7, 15):
         _lib.lib.vpt_attn_set_bwd_mfma16(mask)
         dq = torch.zeros(B * rq, D, dtype=torch.bfloat16, device=DEV)
         dkv = torch.zeros(B * rk, 2 * D, dtype=torch.bfloat16, device=DEV)

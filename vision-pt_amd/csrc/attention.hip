@@ -1468,6 +1468,24 @@ __device__ __forceinline__ void dq16_body(const AttnArgs& g, int bx, int hd, int
 // so the pair runs in ~(work of both) / slots instead of two rounded-up launches.
 // DKDV: the dK/dV body (8 = explicitly ordered, 0 = compiler-scheduled). ORDER 1 (diagnostic A/B): per (batch,
 // head) its nkb dK/dV blocks then its nqb dQ blocks, heads in sequence (a head's Q / dO / K / V shared in time).
+// The 16x16x32 bodies with NW waves per block (diagnostic A/B of NW = 8: 256 keys / queries per block, one block of
+// 8 waves per CU -- the same 2 waves per SIMD -- so each staged Q / dO (K / V) tile serves twice the waves).
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd16_kernel(AttnArgs g, int nkb, int nqb, int B) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];
+  __shared__ __attribute__((aligned(16))) float lstat[2][2][64];
+  extern __shared__ __attribute__((aligned(16))) float kbl[];
+  int bid = blockIdx.x;
+  const int nk_blocks = nkb * g.H * B;
+  const bool kv = bid < nk_blocks;
+  if (!kv) bid -= nk_blocks;
+  if (g.xcd) bid = xcd_remap(bid, kv ? nk_blocks : nqb * g.H * B);
+  const int bx = kv ? bid % nkb : bid % nqb;
+  const int r = kv ? bid / nkb : bid / nqb;
+  if (kv) dkdv16_body<NW, true>(g, bx, r % g.H, r / g.H, lds, lstat);
+  else dq16_body<NW>(g, bx, r % g.H, r / g.H, lds, kbl);
+}
+
 template <int DQ, int DKDV = 8, int ORDER = 0, int NST = 2>
 __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs g, int nkb, int nqb, int B) {
   __shared__ __attribute__((aligned(16))) char lds[NST][2][8192];
@@ -1765,7 +1783,10 @@ int attn_bwd_impl(AttnArgs& g, int B, int H, int n, int nk, hipStream_t s) {
   if (g_mf16 && g_mf16 != kBwdMf16 && !g.qkn) {  // A/B: the 16x16x32 dK/dV (bit 1) / dQ (bit 2) bodies
     const dim3 grid((nkb + nqb) * H * B);
     const size_t kbl_bytes = key_bias_lds_bytes(g);
-    if (g_mf16 == 1)
+    if (g_mf16 == 15) {  // production bodies in 8-wave blocks
+      const int nkb8 = (nk + 255) / 256, nqb8 = (n + 255) / 256;
+      hipLaunchKernelGGL((attn_bwd16_kernel<8>), dim3((nkb8 + nqb8) * H * B), dim3(512), kbl_bytes, s, g, nkb8, nqb8, B);
+    } else if (g_mf16 == 1)
       hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, 16>), grid, dim3(256), kbl_bytes, s, g, nkb, nqb, B);
     else if (g_mf16 == 2)
       hipLaunchKernelGGL((attn_bwd_kernel<16, kDkdvBody>), grid, dim3(256), kbl_bytes, s, g, nkb, nqb, B);
