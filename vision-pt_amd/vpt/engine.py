@@ -42,6 +42,10 @@ FUSED_QKNORM_FWD = True
 FUSED_QKNORM_BWD = False
 # attention forward with the QK-norm score bound as a fixed softmax reference point (vpt_attn_fwd_qknorm): +0.2 %
 FIXREF_ATTN_FWD = True
+# The backward's weight-gradient GEMMs on a second HIP stream (the input-gradient chain stays on the caller's stream):
+# nothing in the chain reads a weight gradient, so each wgrad runs beside the chain's next kernels and fills the CUs
+# their last, partial round of work items leaves idle. Stream-ordered hand-offs only (events; no host sync).
+CONCURRENT_WGRAD = True
 
 
 class _Pool:
@@ -86,6 +90,7 @@ class JiTEngine:
         self.T = cfg.num_time_tokens
         self._state = None
         self.gradient_checkpointing = False
+        self._wstream = None  # the weight-gradient stream (CONCURRENT_WGRAD), created on first use
         self._bind()
 
     # ------------------------------------------------------------------ parameter views
@@ -281,17 +286,45 @@ class JiTEngine:
         acc = not zero_grads
         ws = pool.get("wgrad_ws", (self._ws_elems(max(M, M2)),), F32)
         f, g = self.fin, self.g
+        # Weight gradients on the side stream: each waits (event) for its inputs on the main stream; the main stream
+        # waits for a wgrad's event before it overwrites a buffer that wgrad reads (the ping-pong gradient buffers, the
+        # partial-row buffers its reduce sums, the recomputed activations under checkpointing) -- see `settle`. The
+        # workspace `ws` is used by the side stream alone, whose launches run in order.
+        side = None
+        if CONCURRENT_WGRAD and self.device.type == "cuda":
+            if self._wstream is None:
+                self._wstream = torch.cuda.Stream(device=self.device)
+            side = self._wstream
+        main = torch.cuda.current_stream(self.device) if side is not None else None
+        on_side = side is not None
 
         def wgrad(dy, xin, out, bias=None, rows_sum=None):
             """weight gradient, and with `bias` the bias gradient in the same GEMM (vpt_linear_wgrad); rows_sum = an
-            RMSNorm / QK-norm weight gradient's partial-row sum riding its reduce launch (vpt_linear_wgrad_rr)"""
+            RMSNorm / QK-norm weight gradient's partial-row sum riding its reduce launch (vpt_linear_wgrad_rr).
+            Returns the side stream's event after it (None without the side stream)."""
             Mr, N = dy.shape
             K = xin.shape[1]
             s = ops.wgrad_splits(N, K, Mr)
             while s > 1 and ops.linear_wgrad_workspace_bytes(Mr, N, K, s) > ws.numel() * 4:
                 s -= 1
-            ops.linear_wgrad(dy, xin, out.view(N, K), accumulate=acc, splits=s, workspace=ws,
-                             bias_out=None if bias is None else bias.view(-1), rows_sum=rows_sum)
+
+            def run():
+                ops.linear_wgrad(dy, xin, out.view(N, K), accumulate=acc, splits=s, workspace=ws,
+                                 bias_out=None if bias is None else bias.view(-1), rows_sum=rows_sum)
+            if side is None or not on_side:
+                run()
+                return None
+            side.wait_stream(main)  # dy, xin and the partial rows are written
+            with torch.cuda.stream(side):
+                run()
+            ev = torch.cuda.Event()
+            ev.record(side)
+            return ev
+
+        def settle(ev):
+            """The main stream waits for the side stream up to `ev` (a wgrad's event; None = nothing pending)."""
+            if ev is not None:
+                main.wait_event(ev)
 
         # --- final layer
         f3, fh, f12, xnf, xf = (pool.get(n, s) for n, s in (("f3", (M2, D)), ("fh", (M2, F)), ("f12", (M2, 2 * F)),
@@ -302,11 +335,12 @@ class JiTEngine:
         wgrad(df3, fh, f["gw3"], f["gb3"])
         df12 = ops.linear_dgrad_swiglu(df3, f["pw3"], f12, pool.get("d_x12", (M2, 2 * F)),
                                        workspace=pool.get("d_h", (M2, F)))
-        wgrad(df12, xnf, f["gw12"], f["gb12"])
+        ev = wgrad(df12, xnf, f["gw12"], f["gb12"])
         dxnf = ops.linear_dgrad(df12, f["pw12"], out=pool.get("d_b", (M2, D)))
         dxf, part = ops.rmsnorm_bwd(dxnf, xf, rstdf, f["pn"], dx=pool.get("d_c", (M2, D)),
                                     dw_part=pool.get("rms_part", (ops.rmsnorm_bwd_blocks(max(M, M2)), D), F32))
         ops.reduce_rows(part[:ops.rmsnorm_bwd_blocks(M2)], f["gn"], acc)
+        settle(ev)  # the blocks below reuse d_x12 and the gradient buffers the final layer's wgrads read
         if on_ready is not None:
             on_ready("final")  # every final_layer.* gradient is enqueued
         dx = pool.get("dx_a", (M, D))
@@ -320,10 +354,23 @@ class JiTEngine:
         pre_zeroed = qk_zeroed = False
         scale = 1.0 / math.sqrt(cfg.head_dim)
         ck = st.get("ckpt", False)
+        ev_qkv = None  # the previous block's q|k|v wgrad (reads d_qkv, the QK-norm partial rows, xn1)
+        ready = None   # that block's name for on_ready, announced once its wgrads are waited for
+
+        def settle_qkv():
+            nonlocal ev_qkv, ready
+            settle(ev_qkv)
+            ev_qkv = None
+            if ready is not None and on_ready is not None:
+                on_ready(ready)  # every gradient of that block is complete in the main stream's order
+            ready = None
+
         for i in reversed(range(cfg.depth)):
             w = self.blk[i]
             tag = "ck." if ck else f"b{i}."
             x_in = pool.get(f"x{i}" if i > 0 else "x0", (M, D))
+            if ck:
+                settle_qkv()  # the recompute below overwrites the ck.* activations the previous block's wgrads read
             if ck:  # recompute the block's intermediates from its saved input (x{i+1} is left untouched)
                 self._block_forward(i, x_in, pool.get("ck.xout", (M, D)), tag, pool, B, rows, n_ctx, n_pre,
                                     st["kbias"], cos_t, sin_t)
@@ -334,11 +381,6 @@ class JiTEngine:
             rstd1, rstd2 = pool.get(tag + "rstd1", (M,), F32), pool.get(tag + "rstd2", (M,), F32)
             lse = pool.get(tag + "lse", (B, Hh, rows), F32)
             n_i = rows if (n_ctx and self._ctx_present(i)) else n_pre
-            if n_i < rows and not pre_zeroed:
-                # the context rows take no gradient in the blocks before context_start_block (q | k rows come from
-                # dqk, zeroed below; v rows are never written there)
-                dqkv.view(B, rows, 3 * D)[:, n_i:].zero_()
-                pre_zeroed = True
             # MLP
             wgrad(dx, h, w["gw3"], w["gb3"])
             dx12 = ops.linear_dgrad_swiglu(dx, w["pw3"], x12, pool.get("d_x12", (M, 2 * F)),
@@ -348,8 +390,14 @@ class JiTEngine:
             dxm, part = ops.rmsnorm_bwd(dxn2, xm, rstd2, w["pn2"], dres=dx, dx=pool.get("dx_b", (M, D)),
                                         dw_part=pool.get("rms_part", (ops.rmsnorm_bwd_blocks(max(M, M2)), D), F32))
             # attention (norm2's weight gradient: its partial rows summed by the o-projection wgrad's reduce launch)
-            wgrad(dxm, o, w["gwo"], w["gbo"], rows_sum=(part[:ops.rmsnorm_bwd_blocks(M)], w["gn2"], acc))
+            ev_o = wgrad(dxm, o, w["gwo"], w["gbo"], rows_sum=(part[:ops.rmsnorm_bwd_blocks(M)], w["gn2"], acc))
             do = ops.linear_dgrad(dxm, w["pwo"], out=pool.get("d_o", (M, D)))
+            settle_qkv()  # d_qkv and the QK-norm partial rows are rewritten below
+            if n_i < rows and not pre_zeroed:
+                # the context rows take no gradient in the blocks before context_start_block (q | k rows come from
+                # dqk, zeroed below; v rows are never written there)
+                dqkv.view(B, rows, 3 * D)[:, n_i:].zero_()
+                pre_zeroed = True
             a5 = (ops._t4(qk, B, rows, Hh, 0), ops._t4(qk, B, rows, Hh, D), ops._t4(qkv, B, rows, Hh, 2 * D),
                   ops._t4(o, B, rows, Hh, 0), ops._t4(do, B, rows, Hh, 0), lse, delta, st["kbias"])
             if FUSED_QKNORM_BWD:
@@ -372,16 +420,26 @@ class JiTEngine:
                 qpart = ops.qknorm_rope_bwd(dqk, qkv, w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, rows, dqkv,
                                             dw_part=pool.get("qk_part", (ops.qknorm_rope_blocks(M), 128), F32))
                 qk_job = (qpart[:ops.qknorm_rope_blocks(M)], w["gqk_norm"], acc)
-            wgrad(dqkv, xn1, w["gwqkv"], w["gbqkv"], rows_sum=qk_job)
+            ev_qkv = wgrad(dqkv, xn1, w["gwqkv"], w["gbqkv"], rows_sum=qk_job)
             dxn1 = ops.linear_dgrad(dqkv, w["pwqkv"], out=pool.get("d_b", (M, D)))
+            settle(ev_o)  # the MLP / o-projection wgrads read dx_a, dx_b and rms_part, rewritten from here on
             dx_new, part = ops.rmsnorm_bwd(dxn1, x_in, rstd1, w["pn1"], dres=dxm, dx=pool.get("dx_a", (M, D)),
                                            dw_part=pool.get("rms_part", (ops.rmsnorm_bwd_blocks(max(M, M2)), D), F32))
             ops.reduce_rows(part[:ops.rmsnorm_bwd_blocks(M)], w["gn1"], acc)
-            if on_ready is not None:
-                on_ready(f"block{i}")  # every blocks.{i}.* gradient is enqueued
+            if side is None:
+                if on_ready is not None:
+                    on_ready(f"block{i}")  # every blocks.{i}.* gradient is enqueued
+            else:
+                ready = f"block{i}"  # announced at the next settle_qkv(), after its q|k|v wgrad
             dx = dx_new
             if n_ctx and self._ctx_refresh(i):
                 ops.ctx_rows(dx, B, n_pre, rows, n_ctx, dctx=dctx, backward=True)
+        settle_qkv()
+        if side is not None:
+            # the embeddings' small GEMMs reuse their gradient buffers back to back (d_h1 / d_a1 per embedder): they
+            # run on the main stream, after every block's weight gradient
+            main.wait_stream(side)
+            on_side = False
         # --- embeddings backward
         dpe2 = pool.get("d_pe2", (M2, D))
         dsize = pool.get("d_size", (6 * B, D))
