@@ -180,6 +180,10 @@ def main():
     ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
                     help="optimizer per gradient bucket on a side stream as each all-reduce lands (auto: N > 1; "
                          "at N = 1 one launch after the backward measured faster: 166.9 vs 166.0 img/s, r03d)")
+    ap.add_argument("--wgrad-stream", default="side", choices=["side", "main"],
+                    help="the backward's weight-gradient GEMMs on a second stream beside the input-gradient chain "
+                         "(vpt.engine.CONCURRENT_WGRAD; side: +2.2 %% per C3 step, r05v) or on the step's stream. The "
+                         "probe pass always runs them on the step's stream, so per-kernel times are not shared")
     ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c5"],
                     help="c3: JiT-B/16 1024^2 bucketed (the headline); c2: JiT-B/16 512^2 B=16; "
                          "c5: SDXL QLoRA transformer stacks")
@@ -204,12 +208,14 @@ def main():
     if world > 1:
         dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
 
+    from vpt import engine as vpt_engine
     from vpt import ops
     from vpt.config import JiT_B_16_Config, JiTTrainingConfig
     from vpt.ddp import GradSync, LossLog, grad_buckets
     from vpt.jit_train import JiTTrainer
     from vpt.optim import RAdamScheduleFreeFlat
 
+    vpt_engine.CONCURRENT_WGRAD = args.wgrad_stream == "side"
     cfg = JiT_B_16_Config()
     trainer = JiTTrainer(cfg, N_CLASSES, JiTTrainingConfig(loss_target="image"), device=device, seed=1234 + rank)
     trainer.engine.init_weights(seed=0)  # identical on every rank (replaces DDP's broadcast)
@@ -259,7 +265,9 @@ def main():
         loss = losslog.pop()  # the last timed step's loss, averaged over ranks
 
     # ---- probe pass (after the timed region): one round of the buckets with HIP events around every
-    # launch of the MFMA ops (algorithmic FLOPs) and the memory-bound ops (algorithmic HBM bytes)
+    # launch of the MFMA ops (algorithmic FLOPs) and the memory-bound ops (algorithmic HBM bytes); the weight gradients
+    # on the step's stream here, so no kernel's time is shared with a concurrent one
+    vpt_engine.CONCURRENT_WGRAD = False
     mfma_ops = ("attn_fwd", "attn_bwd", "gemm")
     hbm_ops = ("rmsnorm_fwd", "rmsnorm_bwd", "qknorm_rope_fwd", "qknorm_rope_bwd", "patchify",
                "flow_loss", "radam_sf_step")
@@ -313,12 +321,14 @@ def main():
                    "optimizer_overlap": "per bucket on a side stream during backward" if overlap else
                    "one launch after the backward",
                    "grad_allreduce": "bf16 wire, per-block buckets overlapped with backward" if world > 1 else None,
-                   "grad_checkpointing": bool(args.grad_ckpt)},
+                   "grad_checkpointing": bool(args.grad_ckpt),
+                   "wgrad_stream": args.wgrad_stream},
         "roofline": roofline_entry(dom, stats[dom], args.workload),
         "roofline_others": {k: roofline_entry(k, stats[k], args.workload) for k in mfma_ops if k != dom},
         "kernels": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in stats.items()},
         "hbm_kernels": hbm,
-        "probe_pass": f"{n_probe} steps after the timed region, HIP events on the launching stream",
+        "probe_pass": f"{n_probe} steps after the timed region, HIP events on the launching stream, weight gradients "
+                      "on the step's stream",
         "model_tflops_per_gpu": round(step_tflop * args.steps / (dt), 2),
         "mfu": round(step_tflop * args.steps / dt / PEAK_BF16_TFLOPS, 4),
         "final_loss": round(loss, 5),

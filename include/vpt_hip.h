@@ -198,6 +198,12 @@ int vpt_qknorm_rope_fwd(const void* qkv, long ldin, const void* wq, const void* 
 int vpt_qknorm_rope_bwd(const void* dqk, long lddqk, const void* qkv, long ldin, const void* wq, const void* wk,
                         const float* cos_t, const float* sin_t, void* dqkv, long lddqkv, float* dw_part, int M,
                         int rows_per_seq, int D, float eps, void* stream);
+/* The same for the rows pos < n_valid of each sequence; rows past it get zero q | k | v gradients in dqkv (lddqkv >=
+ * 3D) without dqk being read -- a pre-context block's context rows (denoiser.py:1092-1113), whose attention backward
+ * covers only the n_valid rows. vpt_qknorm_rope_bwd = n_valid of rows_per_seq. */
+int vpt_qknorm_rope_bwd_rows(const void* dqk, long lddqk, const void* qkv, long ldin, const void* wq, const void* wk,
+                             const float* cos_t, const float* sin_t, void* dqkv, long lddqkv, float* dw_part, int M,
+                             int rows_per_seq, int n_valid, int D, float eps, void* stream);
 int vpt_reduce_rows(const float* in, int R, int C, float* out, int accumulate, void* stream);
 
 /* ---- flow matching input / loss ----------------------------------------------------------------
@@ -227,6 +233,8 @@ int vpt_flow_loss(const void* pred, const void* img, const void* noise, const fl
  *   src/modules/timestep/embedding.py:10-62.
  * assemble/disassemble/ctx_rows: token concatenation and per-block context append/strip,
  *   src/models/jit/denoiser.py:982-993,1078-1113 (+ their backward).
+ * ctx_rows backward: 1 adds the context rows' gradient into dctx (f32), 2 writes it (the backward's first refresh
+ *   block: no zero pass over dctx before); both zero those rows of x.
  * copy_rows: patch-token slice tokens[:, :N_p] (denoiser.py:1115). reverse 0: seq -> dense; 1: dense -> seq;
  *   2: dense -> seq and every other row of each sequence zeroed (the slice's backward into a fresh buffer).
  * embed_gather/scatter_add: nn.Embedding(padding_idx) of ClassEncoder, class_encoder.py:107-144. */
@@ -242,6 +250,18 @@ int vpt_copy_rows(void* seq, long ld_seq, int rows, int row0, int cnt, void* den
 int vpt_embed_gather(const void* table, const long long* ids, long R, int D, void* out, void* stream);
 int vpt_embed_scatter_add(const void* drows, const long long* ids, long R, int D, long long pad_id, float* dtable,
                           void* stream);
+/* The same gradient with overwrite semantics (the whole [V][D] table written: zeros where no id points, the padding
+ * row zero), each row summed in position order -- deterministic; R <= 8192. Replaces the zero_() of the class-embedding
+ * gradient + the scatter of arb_class_to_image.py's nn.Embedding backward (class_encoder.py:16-90). */
+int vpt_embed_grad_set(const void* drows, const long long* ids, long R, int D, long long pad_id, long V, float* dtable,
+                       void* stream);
+/* The JiT step's per-batch inputs in one launch: t_vals = bf16(bf16(t) * tscale) as f32 (arb_class_to_image.py:207),
+ * size_vals [B][6] f32 = original_size | target_size | crop_coords (int64 [B][2] each; denoiser.py's size embedder
+ * input), and key-bias rows kbias[b][0, n_pre + n_ctx) (row stride rows): 0, then 0 / -inf by mask [B][n_ctx] int64
+ * (NULL = all valid) -- the attention-mask expansion of denoiser.py:1078-1090. */
+int vpt_step_inputs(const float* t, int B, float tscale, const long long* orig, const long long* target,
+                    const long long* crop, float* t_vals, float* size_vals, const long long* mask, int n_ctx, int n_pre,
+                    int rows, float* kbias, void* stream);
 
 /* ---- activations / reductions ---------------------------------------------------------------
  * swiglu: silu(x1) * x2, SwiGLU.forward src/models/jit/denoiser.py:499-504 (+ backward).

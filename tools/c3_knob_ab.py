@@ -3,6 +3,7 @@ FIXREF_ATTN_FWD): one JiT-B/16 trainer at C3 (B=8, the 5 buckets round-robin, fu
 steps alternating the knob(s) on / off, so allocation, clocks and box are shared; medians of ms per step.
 
   python tools/c3_knob_ab.py FIXREF_ATTN_FWD [--rounds 6] [--steps 5]
+  python tools/c3_knob_ab.py WGRAD_SPLIT_DIV=2/1      (a non-boolean engine attribute: NAME=ON/OFF)
 """
 import argparse
 import json
@@ -56,13 +57,20 @@ def main():
             "GEMM_R2_KMAJ": lambda on: _lib.lib.vpt_gemm_set_r2(9 if on else 8),
             "GEMM_R2_WGRAD": lambda on: _lib.lib.vpt_gemm_set_r2(10 if on else 8),
             "GEMM_R2_FWD": lambda on: _lib.lib.vpt_gemm_set_r2(28 if on else 8)}
+    vals = {}  # NAME=ON/OFF: a non-boolean vpt.engine attribute and its two values
+    for i, k in enumerate(knobs):
+        if "=" in k:
+            name, v = k.split("=")
+            on, off = (int(x) for x in v.split("/"))
+            knobs[i] = name
+            vals[name] = (on, off)
     for k in knobs:
         if k in diag:
             if not _lib.DIAG:
                 _lib.use_diag()
             continue
-        if not isinstance(getattr(engine, k), bool):
-            raise SystemExit(f"{k}: not a boolean knob of vpt.engine")
+        if k not in vals and not isinstance(getattr(engine, k), bool):
+            raise SystemExit(f"{k}: not a boolean knob of vpt.engine (NAME=ON/OFF for other values)")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     tr = JiTTrainer(JiT_B_16_Config(), bench.N_CLASSES, JiTTrainingConfig(loss_target="image"), device=dev, seed=1)
@@ -82,6 +90,8 @@ def main():
         for k in knobs:
             if k in diag:
                 diag[k](v)
+            elif k in vals:
+                setattr(engine, k, vals[k][0 if v else 1])
             else:
                 setattr(engine, k, v)
 

@@ -443,8 +443,13 @@ __global__ void ctx_rows_kernel(bf16_t* __restrict__ x, int B, int row0, int row
     float f[8];
     unpack8(*reinterpret_cast<const uint4*>(xr), f);
     floatx4* d = reinterpret_cast<floatx4*>(dctx + r * D + ch * 8);
-    d[0] += floatx4{f[0], f[1], f[2], f[3]};
-    d[1] += floatx4{f[4], f[5], f[6], f[7]};
+    if (backward == 2) {  // the first refresh block of the backward: dctx = instead of += (no zero pass before)
+      d[0] = floatx4{f[0], f[1], f[2], f[3]};
+      d[1] = floatx4{f[4], f[5], f[6], f[7]};
+    } else {
+      d[0] += floatx4{f[0], f[1], f[2], f[3]};
+      d[1] += floatx4{f[4], f[5], f[6], f[7]};
+    }
     *reinterpret_cast<uint4*>(xr) = make_uint4(0, 0, 0, 0);
   }
 }
@@ -549,6 +554,79 @@ __global__ void embed_scatter_kernel(const bf16_t* __restrict__ drows, const int
   const long id = ids[r];
   if (id == pad_id) return;
   atomicAdd(dtable + id * D + d, bf2f(drows[gid]));
+}
+
+// The class-embedding gradient with overwrite semantics in one pass (replaces a fill of the whole table + the
+// atomic scatter): each block owns kEmbRows table rows, collects the positions p whose id falls in them (LDS list),
+// orders each row's positions ascending (rank sort of the few entries) and writes every row as the sum of its drows
+// rows in position order -- zeros for rows no id names and for the padding row (nn.Embedding padding_idx, as the
+// scatter skips it). Deterministic, unlike the atomics. Dynamic LDS: R ints (the list) + R ints (sorted), R <= 8192.
+constexpr int kEmbRows = 8;
+__global__ void embed_grad_set_kernel(const bf16_t* __restrict__ drows, const int64_t* __restrict__ ids, int R, int D,
+                                      long pad_id, long V, float* __restrict__ dtable) {
+  extern __shared__ int elist[];  // [R] unsorted keys, then [R] sorted
+  __shared__ int cnt, start[kEmbRows + 1];
+  int* sorted = elist + R;
+  const long r0 = (long)blockIdx.x * kEmbRows;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  for (int p = threadIdx.x; p < R; p += blockDim.x) {
+    const long id = ids[p];
+    if (id >= r0 && id < r0 + kEmbRows && id != pad_id) elist[atomicAdd(&cnt, 1)] = (int)(id - r0) * R + p;
+  }
+  __syncthreads();
+  const int m = cnt;
+  for (int i = threadIdx.x; i < m; i += blockDim.x) {  // keys are distinct: rank = number of smaller keys
+    const int k = elist[i];
+    int rank = 0;
+    for (int j = 0; j < m; ++j) rank += elist[j] < k;
+    sorted[rank] = k;
+  }
+  if (threadIdx.x <= kEmbRows) {  // first sorted entry of row offset threadIdx.x
+    int c = 0;
+    for (int j = 0; j < m; ++j) c += elist[j] < (int)threadIdx.x * R;
+    start[threadIdx.x] = c;
+  }
+  __syncthreads();
+  const int nc = D >> 2;
+  for (int idx = threadIdx.x; idx < kEmbRows * nc; idx += blockDim.x) {
+    const int ro = idx / nc, c = idx % nc;
+    if (r0 + ro >= V) break;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int e = start[ro]; e < start[ro + 1]; ++e) {
+      const int pos = sorted[e] - ro * R;
+      const uint2 w = *reinterpret_cast<const uint2*>(drows + (long)pos * D + 4 * c);
+      acc += floatx4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u), __uint_as_float(w.y << 16),
+                     __uint_as_float(w.y & 0xffff0000u)};
+    }
+    *reinterpret_cast<floatx4*>(dtable + (r0 + ro) * D + 4 * c) = acc;
+  }
+}
+
+// The JiT step's small per-batch inputs in one launch (jit_train.JiTTrainer.step; replaces ~10 torch element-wise
+// launches): t_vals = bf16(bf16(t) * scale) as f32 (arb_class_to_image.py:207's timesteps.to(bf16) * scale), size_vals
+// = [original | target | crop] per sample as f32, and the key-bias rows: 0 over the n_pre image / token rows, 0 / -inf
+// over the n_ctx context rows by the padding mask (all valid without one).
+__global__ void step_inputs_kernel(const float* __restrict__ t, int B, float tscale, const int64_t* __restrict__ orig,
+                                   const int64_t* __restrict__ target, const int64_t* __restrict__ crop,
+                                   float* __restrict__ t_vals, float* __restrict__ size_vals,
+                                   const int64_t* __restrict__ mask, int n_ctx, int n_pre, int rows,
+                                   float* __restrict__ kbias) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long nk = (long)B * (n_pre + n_ctx);
+  if (gid < nk) {
+    const int b = gid / (n_pre + n_ctx), c = gid % (n_pre + n_ctx);
+    float v = 0.f;
+    if (c >= n_pre && mask && mask[(long)b * n_ctx + c - n_pre] == 0) v = -__builtin_huge_valf();
+    kbias[(long)b * rows + c] = v;
+  } else if (gid < nk + B) {
+    const int b = gid - nk;
+    t_vals[b] = bf2f(f2bf(bf2f(f2bf(t[b])) * tscale));
+  } else if (gid < nk + 7L * B) {
+    const int i = gid - nk - B, b = i / 6, j = i % 6;
+    const int64_t* src = j < 2 ? orig : j < 4 ? target : crop;
+    size_vals[i] = (float)src[2 * b + (j & 1)];
+  }
 }
 
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ in, long n, bf16_t* __restrict__ out) {
@@ -921,6 +999,31 @@ extern "C" int vpt_embed_scatter_add(const void* drows, const long long* ids, lo
   VPT_CHECK_ARG(drows && ids && dtable, "vpt_embed_scatter_add: bad args");
   hipLaunchKernelGGL(embed_scatter_kernel, grid1(R * D), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)drows,
                      (const int64_t*)ids, R, D, (long)pad_id, dtable);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_embed_grad_set(const void* drows, const long long* ids, long R, int D, long long pad_id, long V,
+                                  float* dtable, void* stream) {
+  VPT_CHECK_ARG((drows || R == 0) && (ids || R == 0) && dtable && D % 4 == 0 && V > 0, "vpt_embed_grad_set: bad args");
+  VPT_CHECK_ARG(R >= 0 && R <= 8192, "vpt_embed_grad_set: R <= 8192 ids (LDS position lists)");
+  VPT_CHECK_ARG((long)kEmbRows * R < (1L << 31), "vpt_embed_grad_set: key range");
+  hipLaunchKernelGGL(embed_grad_set_kernel, dim3((unsigned)((V + kEmbRows - 1) / kEmbRows)), dim3(256),
+                     (size_t)(2 * R) * sizeof(int), (hipStream_t)stream, (const bf16_t*)drows, (const int64_t*)ids,
+                     (int)R, D, (long)pad_id, V, dtable);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_step_inputs(const float* t, int B, float tscale, const long long* orig, const long long* target,
+                               const long long* crop, float* t_vals, float* size_vals, const long long* mask, int n_ctx,
+                               int n_pre, int rows, float* kbias, void* stream) {
+  VPT_CHECK_ARG(t && orig && target && crop && t_vals && size_vals && kbias && B > 0 && n_ctx >= 0 && n_pre >= 0 &&
+                n_pre + n_ctx <= rows, "vpt_step_inputs: bad args");
+  const long n = (long)B * (n_pre + n_ctx) + 7L * B;
+  hipLaunchKernelGGL(step_inputs_kernel, grid1(n), dim3(256), 0, (hipStream_t)stream, t, B, tscale,
+                     (const int64_t*)orig, (const int64_t*)target, (const int64_t*)crop, t_vals, size_vals,
+                     (const int64_t*)mask, n_ctx, n_pre, rows, kbias);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256) void qknorm_rope_bwd_kernel(const bf16_t* __re
                                                               const float* __restrict__ cs, const float* __restrict__ sn,
                                                               bf16_t* __restrict__ dqkv, long lddqkv,
                                                               float* __restrict__ dw_part, int M, int rows_per_seq,
-                                                              int D, float eps) {
+                                                              int D, float eps, int n_valid) {
   __shared__ float red[256][8];
   const int sub = threadIdx.x, per = D >> 3;   // blockDim = 2 * D / 8
   const int which = sub / per, head = (sub % per) >> 3, part = sub & 7;
@@ -204,6 +204,12 @@ __global__ __launch_bounds__(256) void qknorm_rope_bwd_kernel(const bf16_t* __re
   for (int e = 0; e < 8; ++e) dwp[e] = 0.f;
   for (long row = blockIdx.x; row < M; row += gridDim.x) {
     const long pos = row % rows_per_seq;
+    if (pos >= n_valid) {  // rows past the attention's n (a pre-context block's context rows): zero q | k | v gradients
+      bf16_t* dst = dqkv + row * lddqkv + which * D + head * 64 + part * 8;
+      *reinterpret_cast<uint4*>(dst) = make_uint4(0, 0, 0, 0);
+      if (which == 0) *reinterpret_cast<uint4*>(dst + 2 * D) = make_uint4(0, 0, 0, 0);
+      continue;
+    }
     float fx[8], fg[8];
     unpack8(*reinterpret_cast<const uint4*>(qkv + row * ldin + which * D + head * 64 + part * 8), fx);
     unpack8(*reinterpret_cast<const uint4*>(dqk + row * lddqk + which * D + head * 64 + part * 8), fg);
@@ -308,17 +314,27 @@ extern "C" int vpt_qknorm_rope_fwd(const void* qkv, long ldin, const void* wq, c
   return VPT_OK;
 }
 
-extern "C" int vpt_qknorm_rope_bwd(const void* dqk, long lddqk, const void* qkv, long ldin, const void* wq,
-                                   const void* wk, const float* cos_t, const float* sin_t, void* dqkv, long lddqkv,
-                                   float* dw_part, int M, int rows_per_seq, int D, float eps, void* stream) {
+extern "C" int vpt_qknorm_rope_bwd_rows(const void* dqk, long lddqk, const void* qkv, long ldin, const void* wq,
+                                        const void* wk, const float* cos_t, const float* sin_t, void* dqkv, long lddqkv,
+                                        float* dw_part, int M, int rows_per_seq, int n_valid, int D, float eps,
+                                        void* stream) {
   VPT_CHECK_ARG(dqk && qkv && wq && wk && cos_t && sin_t && dqkv && dw_part, "vpt_qknorm_rope_bwd: null pointer");
   VPT_CHECK_ARG(D % 64 == 0 && D <= 1024, "vpt_qknorm_rope_bwd: heads x 64 with D <= 1024");
+  VPT_CHECK_ARG(n_valid >= 0 && n_valid <= rows_per_seq, "vpt_qknorm_rope_bwd: 0 <= n_valid <= rows_per_seq");
+  VPT_CHECK_ARG(n_valid == rows_per_seq || lddqkv >= 3 * D, "vpt_qknorm_rope_bwd: n_valid < rows needs dqkv's v part");
   if (M == 0) return VPT_OK;
   hipLaunchKernelGGL(qknorm_rope_bwd_kernel, dim3(vpt_qknorm_rope_blocks(M)), dim3(D / 4), 0, (hipStream_t)stream,
                      (const bf16_t*)dqk, lddqk, (const bf16_t*)qkv, ldin, (const bf16_t*)wq, (const bf16_t*)wk, cos_t,
-                     sin_t, (bf16_t*)dqkv, lddqkv, dw_part, M, rows_per_seq, D, eps);
+                     sin_t, (bf16_t*)dqkv, lddqkv, dw_part, M, rows_per_seq, D, eps, n_valid);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
+}
+
+extern "C" int vpt_qknorm_rope_bwd(const void* dqk, long lddqk, const void* qkv, long ldin, const void* wq,
+                                   const void* wk, const float* cos_t, const float* sin_t, void* dqkv, long lddqkv,
+                                   float* dw_part, int M, int rows_per_seq, int D, float eps, void* stream) {
+  return vpt_qknorm_rope_bwd_rows(dqk, lddqk, qkv, ldin, wq, wk, cos_t, sin_t, dqkv, lddqkv, dw_part, M, rows_per_seq,
+                                  rows_per_seq, D, eps, stream);
 }
 
 extern "C" int vpt_reduce_rows(const float* in, int R, int C, float* out, int accumulate, void* stream) {

@@ -46,6 +46,7 @@ SIGNATURES: dict[str, list] = {
     "vpt_qknorm_rope_blocks": [I],
     "vpt_qknorm_rope_fwd": [P, L, P, P, P, P, P, L, I, I, I, F, F, P],
     "vpt_qknorm_rope_bwd": [P, L, P, L, P, P, P, P, P, L, P, I, I, I, F, P],
+    "vpt_qknorm_rope_bwd_rows": [P, L, P, L, P, P, P, P, P, L, P, I, I, I, I, F, P],
     "vpt_reduce_rows": [P, I, I, P, I, P],
     "vpt_patchify": [P, I, P, P, F, U64, I, I, I, P, P],
     "vpt_unpatchify": [P, I, I, I, P, I, P],
@@ -62,6 +63,8 @@ SIGNATURES: dict[str, list] = {
     "vpt_bias_grad": [P, L, L, I, P, P, I, P],
     "vpt_embed_gather": [P, P, L, I, P, P],
     "vpt_embed_scatter_add": [P, P, L, I, LL, P, P],
+    "vpt_embed_grad_set": [P, P, L, I, LL, L, P, P],
+    "vpt_step_inputs": [P, I, F, P, P, P, P, P, P, I, I, I, P, P],
     "vpt_cast_f32_bf16": [P, L, P, P],
     "vpt_radam_sf_step": [P, P, I, P, P, L, F, F, F, F, F, F, F, F, I, P, F, P],
     "vpt_grad_norm_blocks": [],

@@ -46,6 +46,11 @@ FIXREF_ATTN_FWD = True
 # nothing in the chain reads a weight gradient, so each wgrad runs beside the chain's next kernels and fills the CUs
 # their last, partial round of work items leaves idle. Stream-ordered hand-offs only (events; no host sync).
 CONCURRENT_WGRAD = True
+# A/B knobs of the side stream: its HIP priority (0 = the default streams' level, -1 = high: level, r05x) and a factor on
+# the wgrads' split-K count (ops.wgrad_splits sizes it to fill the chip alone)
+WGRAD_STREAM_PRIORITY = 0
+WGRAD_SPLIT_DIV = 1  # 2: C3 step -5.5 % (r05x) -- the wgrads then lag the chain's hand-off waits
+WGRAD_SPLIT_MUL = 1
 
 
 class _Pool:
@@ -268,9 +273,11 @@ class JiTEngine:
         return i == cs or (not self.cfg.do_context_fuse and i > cs)
 
     # ------------------------------------------------------------------ backward
-    def backward(self, dout: torch.Tensor, zero_grads: bool = True, on_ready=None) -> torch.Tensor | None:
+    def backward(self, dout: torch.Tensor, zero_grads: bool = True, on_ready=None,
+                 overwritten: tuple = ()) -> torch.Tensor | None:
         """dout [B*N_p, P*P*C] bf16 gradient of the patch-layout output. Fills self.grads (f32;
-        accumulates when zero_grads=False) and returns d(ctx_raw) [B*n_ctx, context_dim] bf16."""
+        accumulates when zero_grads=False) and returns d(ctx_raw) [B*n_ctx, context_dim] bf16. `overwritten`: gradient
+        names the caller writes with overwrite semantics after this backward (not zeroed here)."""
         st = self._state
         if st is None:
             raise RuntimeError("backward() needs a forward(save=True) first")
@@ -282,7 +289,7 @@ class JiTEngine:
             # every gradient slice below is written with overwrite semantics when acc is False; only the slices this
             # backward does not write (the class-embedding table the trainer scatter-adds into, the context embedder
             # of a context-free batch) are zeroed, instead of a fill over the whole flat buffer
-            self._zero_unwritten_grads(n_ctx)
+            self._zero_unwritten_grads(n_ctx, overwritten)
         acc = not zero_grads
         ws = pool.get("wgrad_ws", (self._ws_elems(max(M, M2)),), F32)
         f, g = self.fin, self.g
@@ -292,8 +299,8 @@ class JiTEngine:
         # workspace `ws` is used by the side stream alone, whose launches run in order.
         side = None
         if CONCURRENT_WGRAD and self.device.type == "cuda":
-            if self._wstream is None:
-                self._wstream = torch.cuda.Stream(device=self.device)
+            if self._wstream is None or self._wstream.priority != WGRAD_STREAM_PRIORITY:
+                self._wstream = torch.cuda.Stream(device=self.device, priority=WGRAD_STREAM_PRIORITY)
             side = self._wstream
         main = torch.cuda.current_stream(self.device) if side is not None else None
         on_side = side is not None
@@ -304,7 +311,9 @@ class JiTEngine:
             Returns the side stream's event after it (None without the side stream)."""
             Mr, N = dy.shape
             K = xin.shape[1]
-            s = ops.wgrad_splits(N, K, Mr)
+            s = max(1, ops.wgrad_splits(N, K, Mr) * WGRAD_SPLIT_MUL // WGRAD_SPLIT_DIV)
+            while s > 1 and Mr // s < 256:
+                s -= 1
             while s > 1 and ops.linear_wgrad_workspace_bytes(Mr, N, K, s) > ws.numel() * 4:
                 s -= 1
 
@@ -346,12 +355,13 @@ class JiTEngine:
         dx = pool.get("dx_a", (M, D))
         ops.copy_rows(dx, rows, 0, np_, dxf, B, reverse=True, zero_rest=True)  # token / context rows: zero
         # --- blocks in reverse
-        dctx = pool.get("dctx", (max(B * n_ctx, 1), D), F32, zero=True)
+        dctx = pool.get("dctx", (max(B * n_ctx, 1), D), F32)  # written by the first refresh block's ctx_rows
+        dctx_set = False
         dqkv = pool.get("d_qkv", (M, 3 * D))
         delta = pool.get("delta", (B, Hh, rows), F32)
         n_dw = ops.attn_bwd_dw_rows(B, Hh, rows)
         qk_dw = pool.get("qk_dw_part", (n_dw, 128), F32)  # q_norm | k_norm weight-gradient partials
-        pre_zeroed = qk_zeroed = False
+        pre_zeroed = False
         scale = 1.0 / math.sqrt(cfg.head_dim)
         ck = st.get("ckpt", False)
         ev_qkv = None  # the previous block's q|k|v wgrad (reads d_qkv, the QK-norm partial rows, xn1)
@@ -393,9 +403,9 @@ class JiTEngine:
             ev_o = wgrad(dxm, o, w["gwo"], w["gbo"], rows_sum=(part[:ops.rmsnorm_bwd_blocks(M)], w["gn2"], acc))
             do = ops.linear_dgrad(dxm, w["pwo"], out=pool.get("d_o", (M, D)))
             settle_qkv()  # d_qkv and the QK-norm partial rows are rewritten below
-            if n_i < rows and not pre_zeroed:
-                # the context rows take no gradient in the blocks before context_start_block (q | k rows come from
-                # dqk, zeroed below; v rows are never written there)
+            if FUSED_QKNORM_BWD and n_i < rows and not pre_zeroed:
+                # the context rows take no gradient in the blocks before context_start_block (the fused backward
+                # writes rows < n_i only; the standalone QK-norm backward below zeroes them itself)
                 dqkv.view(B, rows, 3 * D)[:, n_i:].zero_()
                 pre_zeroed = True
             a5 = (ops._t4(qk, B, rows, Hh, 0), ops._t4(qk, B, rows, Hh, D), ops._t4(qkv, B, rows, Hh, 2 * D),
@@ -410,15 +420,12 @@ class JiTEngine:
                 qk_job = (qk_dw[:ops.attn_bwd_dw_rows(B, Hh, n_i)], w["gqk_norm"], acc)
             else:
                 dqk = pool.get("d_qk", (M, 2 * D))
-                if n_i < rows and not qk_zeroed:
-                    # once, at the first pre-context block: the later (earlier-indexed) pre-context blocks never write
-                    # these rows, the post-context blocks before them wrote all rows
-                    dqk.view(B, rows, 2 * D)[:, n_i:].zero_()
-                    qk_zeroed = True
                 ops.attn_bwd(*a5, ops._t4(dqk, B, rows, Hh, 0), ops._t4(dqk, B, rows, Hh, D),
                              ops._t4(dqkv, B, rows, Hh, 2 * D), B, Hh, rows, n_i, n_pre, scale)
+                # rows >= n_i (a pre-context block's context rows): zero q | k | v gradients, dqk not read there
                 qpart = ops.qknorm_rope_bwd(dqk, qkv, w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, rows, dqkv,
-                                            dw_part=pool.get("qk_part", (ops.qknorm_rope_blocks(M), 128), F32))
+                                            dw_part=pool.get("qk_part", (ops.qknorm_rope_blocks(M), 128), F32),
+                                            n_valid=n_i)
                 qk_job = (qpart[:ops.qknorm_rope_blocks(M)], w["gqk_norm"], acc)
             ev_qkv = wgrad(dqkv, xn1, w["gwqkv"], w["gbqkv"], rows_sum=qk_job)
             dxn1 = ops.linear_dgrad(dqkv, w["pwqkv"], out=pool.get("d_b", (M, D)))
@@ -433,7 +440,8 @@ class JiTEngine:
                 ready = f"block{i}"  # announced at the next settle_qkv(), after its q|k|v wgrad
             dx = dx_new
             if n_ctx and self._ctx_refresh(i):
-                ops.ctx_rows(dx, B, n_pre, rows, n_ctx, dctx=dctx, backward=True)
+                ops.ctx_rows(dx, B, n_pre, rows, n_ctx, dctx=dctx, backward=True, overwrite=not dctx_set)
+                dctx_set = True
         settle_qkv()
         if side is not None:
             # the embeddings' small GEMMs reuse their gradient buffers back to back (d_h1 / d_a1 per embedder): they
@@ -461,6 +469,8 @@ class JiTEngine:
             da1 = ops.silu_bwd(dh1, a1, pool.get("d_a1", (rowsn, D)))
             wgrad(da1, emb_in, g[pre + ".mlp.0.weight"], g[pre + ".mlp.0.bias"])
         dctx_raw = None
+        if n_ctx and not dctx_set:
+            dctx.zero_()  # no refresh block (not reached for a context that enters at a block)
         if n_ctx:
             dctx_b = ops.cast_f32_bf16(dctx, pool.get("dctx_bf16", (B * n_ctx, D)))
             wgrad(dctx_b, st["ctx_raw"], g["context_embedder.weight"], g["context_embedder.bias"])
@@ -468,12 +478,12 @@ class JiTEngine:
                                         out=pool.get("d_ctx_raw", (B * n_ctx, cfg.context_dim)))
         return dctx_raw
 
-    def _zero_unwritten_grads(self, n_ctx: int):
+    def _zero_unwritten_grads(self, n_ctx: int, overwritten: tuple = ()):
         names = ["class_encoder.embedding.weight"]
         if not n_ctx:
             names += ["context_embedder.weight", "context_embedder.bias"]
         for n in names:
-            if n in self.g:
+            if n in self.g and n not in overwritten:
                 self.g[n].zero_()
 
     def _tpe_grad_target(self, acc: bool):
@@ -487,6 +497,6 @@ class JiTEngine:
         D, F = self.D, self.F
         best = 1
         for N, K in ((D, F), (2 * F, D), (3 * D, D), (D, D), (self.fin["pwl"].shape[0], D)):
-            s = ops.wgrad_splits(N, K, M)
+            s = ops.wgrad_splits(N, K, M) * WGRAD_SPLIT_MUL
             best = max(best, ops.linear_wgrad_workspace_bytes(M, N, K, s) // 4 + 1)
         return best

@@ -472,16 +472,18 @@ def qknorm_rope_blocks(M: int) -> int:
     return lib.vpt_qknorm_rope_blocks(M)
 
 
-def qknorm_rope_bwd(dqk, qkv, wq, wk, cos_t, sin_t, rows_per_seq, dqkv, dw_part=None, eps=1e-6):
-    """Writes dqkv[:, :2D]; dw_part [blocks, 128] = (d q_norm.w | d k_norm.w) partials."""
+def qknorm_rope_bwd(dqk, qkv, wq, wk, cos_t, sin_t, rows_per_seq, dqkv, dw_part=None, eps=1e-6, n_valid=None):
+    """Writes dqkv[:, :2D]; dw_part [blocks, 128] = (d q_norm.w | d k_norm.w) partials. n_valid < rows_per_seq: the
+    rows past it get zero q | k | v gradients (dqk not read there)."""
     M = qkv.shape[0]
     D = qkv.shape[1] // 3
+    nv = rows_per_seq if n_valid is None else n_valid
     if dw_part is None:
         dw_part = torch.empty(qknorm_rope_blocks(M), 128, dtype=F32, device=qkv.device)
     _launch("qknorm_rope_bwd", M * 2 * D * 6,  # dq, dk and q, k in; dq, dk out (bf16)
-            lambda: call("vpt_qknorm_rope_bwd", dqk.data_ptr(), dqk.stride(0), qkv.data_ptr(), qkv.stride(0),
+            lambda: call("vpt_qknorm_rope_bwd_rows", dqk.data_ptr(), dqk.stride(0), qkv.data_ptr(), qkv.stride(0),
                          wq.data_ptr(), wk.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(), dqkv.data_ptr(),
-                         dqkv.stride(0), dw_part.data_ptr(), M, rows_per_seq, D, eps, stream()))
+                         dqkv.stride(0), dw_part.data_ptr(), M, rows_per_seq, nv, D, eps, stream()))
     return dw_part
 
 
@@ -616,8 +618,10 @@ def disassemble_tokens(dx, B, np_, rows, dpatches, dsize, dtime, dtpe):
          dtime.data_ptr(), _p(dtpe), stream())
 
 
-def ctx_rows(x, B, row0, rows, n_ctx, ctx=None, dctx=None, backward=False):
-    call("vpt_ctx_rows", x.data_ptr(), B, row0, rows, x.shape[1], _p(ctx), _p(dctx), n_ctx, int(backward), stream())
+def ctx_rows(x, B, row0, rows, n_ctx, ctx=None, dctx=None, backward=False, overwrite=False):
+    """Forward: ctx -> the context rows of x. Backward: those rows of x -> dctx (+=, or = with overwrite), then zeroed."""
+    mode = (2 if overwrite else 1) if backward else 0
+    call("vpt_ctx_rows", x.data_ptr(), B, row0, rows, x.shape[1], _p(ctx), _p(dctx), n_ctx, mode, stream())
 
 
 def swiglu_fwd(x12, h):
@@ -663,6 +667,27 @@ def embed_scatter_add(drows, ids, pad_id, dtable):
         return
     call("vpt_embed_scatter_add", drows.data_ptr(), ids.data_ptr(), R, dtable.shape[1], pad_id, dtable.data_ptr(),
          stream())
+
+
+def embed_grad_set(drows, ids, pad_id, dtable):
+    """dtable[V, D] f32 = the embedding gradient of drows [R, D] bf16 at ids [R] (overwrite; padding row and unnamed
+    rows zero; each row summed in position order)."""
+    R = ids.numel()
+    call("vpt_embed_grad_set", drows.data_ptr() if R else None, ids.data_ptr() if R else None, R, dtable.shape[1],
+         pad_id, dtable.shape[0], dtable.data_ptr(), stream())
+    return dtable
+
+
+EMBED_GRAD_SET_MAX_IDS = 8192
+
+
+def step_inputs(t, tscale, orig, target, crop, t_vals, size_vals, mask, n_ctx, n_pre, rows, kbias):
+    """vpt_step_inputs: t [B] f32, orig / target / crop int64 [B, 2] (device, contiguous), mask int64 [B, n_ctx] or
+    None -> t_vals [B], size_vals [6B] f32 and kbias[:, :n_pre + n_ctx] (row stride rows)."""
+    B = t.numel()
+    call("vpt_step_inputs", t.data_ptr(), B, tscale, orig.data_ptr(), target.data_ptr(), crop.data_ptr(),
+         t_vals.data_ptr(), size_vals.data_ptr(), None if mask is None else mask.data_ptr(), n_ctx, n_pre, rows,
+         kbias.data_ptr(), stream())
 
 
 def copy_rows(seq, rows, row0, cnt, dense, B, reverse=False, zero_rest=False):
