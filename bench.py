@@ -268,6 +268,7 @@ def main():
     # launch of the MFMA ops (algorithmic FLOPs) and the memory-bound ops (algorithmic HBM bytes); the weight gradients
     # on the step's stream here, so no kernel's time is shared with a concurrent one
     vpt_engine.CONCURRENT_WGRAD = False
+    vpt_engine.MICRO_SPLIT = 1
     mfma_ops = ("attn_fwd", "attn_bwd", "gemm")
     hbm_ops = ("rmsnorm_fwd", "rmsnorm_bwd", "qknorm_rope_fwd", "qknorm_rope_bwd", "patchify",
                "flow_loss", "radam_sf_step")

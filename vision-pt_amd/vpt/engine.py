@@ -51,6 +51,22 @@ CONCURRENT_WGRAD = True
 WGRAD_STREAM_PRIORITY = 0
 WGRAD_SPLIT_DIV = 1  # 2: C3 step -5.5 % (r05x) -- the wgrads then lag the chain's hand-off waits
 WGRAD_SPLIT_MUL = 1
+# The forward's transformer blocks as MICRO_SPLIT independent sub-batches (B / MICRO_SPLIT sequences each) on their own
+# streams: every op is row- or sequence-local, so the sub-batches need no exchange and the result is bitwise the
+# one-batch forward; one sub-batch's kernels fill the CUs the other's leave idle in their last, partial round of work
+# items (the GEMMs' wave quantisation, the attention grids' tails). 1 = one stream.
+MICRO_SPLIT = 1
+
+
+class _SubPool:
+    """Row slice h of n of every buffer a _Pool hands out (first dimension = the sub-batch's share)."""
+
+    def __init__(self, pool, h: int, n: int):
+        self.pool, self.h, self.n = pool, h, n
+
+    def get(self, name: str, shape, dtype=BF16, zero: bool = False) -> torch.Tensor:
+        full = self.pool.get(name, (shape[0] * self.n,) + tuple(shape[1:]), dtype, zero)
+        return full[self.h * shape[0]:(self.h + 1) * shape[0]]
 
 
 class _Pool:
@@ -96,6 +112,7 @@ class JiTEngine:
         self._state = None
         self.gradient_checkpointing = False
         self._wstream = None  # the weight-gradient stream (CONCURRENT_WGRAD), created on first use
+        self._mstreams = []   # the sub-batch streams (MICRO_SPLIT)
         self._bind()
 
     # ------------------------------------------------------------------ parameter views
@@ -208,15 +225,37 @@ class JiTEngine:
         x = pool.get("x0", (M, D))
         ops.assemble_tokens(pe2, semb, temb, p["time_position_embeds"], ctx, n_ctx, B, np_, rows, x)
         # --- blocks (denoiser.py:1087-1113)
+        S = MICRO_SPLIT if (MICRO_SPLIT > 1 and B % MICRO_SPLIT == 0 and self.device.type == "cuda") else 1
+        if S > 1:
+            main = torch.cuda.current_stream(self.device)
+            while len(self._mstreams) < S:
+                self._mstreams.append(torch.cuda.Stream(device=self.device))
+            subs = self._mstreams[:S]
+            for st in subs:
+                st.wait_stream(main)  # embeddings / assembled tokens written
+            Bh, Mh = B // S, (B // S) * rows
+            spools = [_SubPool(pool, h, S) for h in range(S)]
         for i, w in enumerate(self.blk):
-            if n_ctx and self._ctx_refresh(i):
-                ops.ctx_rows(x, B, n_pre, rows, n_ctx, ctx=ctx)
             x_next = pool.get(f"x{i + 1}" if save else ("xa" if i % 2 == 0 else "xb"), (M, D))
             # gradient checkpointing (denoiser.py:945-967): only the block inputs x{i} are kept; the block's
             # intermediates go to one scratch set and are recomputed in backward
             tag = ("ck." if self.gradient_checkpointing else f"b{i}.") if save else "s."
-            self._block_forward(i, x, x_next, tag, pool, B, rows, n_ctx, n_pre, kbias, cos_t, sin_t)
+            if S == 1:
+                if n_ctx and self._ctx_refresh(i):
+                    ops.ctx_rows(x, B, n_pre, rows, n_ctx, ctx=ctx)
+                self._block_forward(i, x, x_next, tag, pool, B, rows, n_ctx, n_pre, kbias, cos_t, sin_t)
+            else:
+                for h in range(S):
+                    with torch.cuda.stream(subs[h]):
+                        xh, r0 = x[h * Mh:(h + 1) * Mh], h * Bh
+                        if n_ctx and self._ctx_refresh(i):
+                            ops.ctx_rows(xh, Bh, n_pre, rows, n_ctx, ctx=ctx[r0 * n_ctx:(r0 + Bh) * n_ctx])
+                        self._block_forward(i, xh, x_next[h * Mh:(h + 1) * Mh], tag, spools[h], Bh, rows, n_ctx,
+                                            n_pre, None if kbias is None else kbias[r0:r0 + Bh], cos_t, sin_t)
             x = x_next
+        if S > 1:
+            for st in subs:
+                main.wait_stream(st)
         # --- final layer + (per-patch) output (denoiser.py:1115-1116, 535-543)
         f = self.fin
         M2 = B * np_
