@@ -19,6 +19,7 @@ Activations saved for backward are kept (no recompute): ~28 KB/token/block at D=
 
 from __future__ import annotations
 
+import contextlib
 import math
 
 import torch
@@ -343,6 +344,7 @@ class JiTEngine:
             side = self._wstream
         main = torch.cuda.current_stream(self.device) if side is not None else None
         on_side = side is not None
+        self._wait_inputs = None
 
         def wgrad(dy, xin, out, bias=None, rows_sum=None):
             """weight gradient, and with `bias` the bias gradient in the same GEMM (vpt_linear_wgrad); rows_sum = an
@@ -362,7 +364,10 @@ class JiTEngine:
             if side is None or not on_side:
                 run()
                 return None
-            side.wait_stream(main)  # dy, xin and the partial rows are written
+            if self._wait_inputs is not None:
+                self._wait_inputs()  # every sub-batch lane wrote dy, xin and the partial rows
+            else:
+                side.wait_stream(main)  # dy, xin and the partial rows are written
             with torch.cuda.stream(side):
                 run()
             ev = torch.cuda.Event()
@@ -393,26 +398,76 @@ class JiTEngine:
             on_ready("final")  # every final_layer.* gradient is enqueued
         dx = pool.get("dx_a", (M, D))
         ops.copy_rows(dx, rows, 0, np_, dxf, B, reverse=True, zero_rest=True)  # token / context rows: zero
-        # --- blocks in reverse
+        # --- blocks in reverse. With MICRO_SPLIT = S > 1 (and the side stream) the input-gradient chain runs as S
+        # independent sub-batches on their own streams ("lanes"), like the forward; every weight gradient -- and
+        # norm1's weight-gradient reduce -- covers the whole batch on the side stream once all lanes produced its
+        # inputs. S = 1: one lane, the caller's stream.
+        S = MICRO_SPLIT if (MICRO_SPLIT > 1 and B % MICRO_SPLIT == 0 and side is not None
+                            and not FUSED_QKNORM_BWD) else 1
+        if S > 1:
+            while len(self._mstreams) < S:
+                self._mstreams.append(torch.cuda.Stream(device=self.device))
+            lanes = self._mstreams[:S]
+            for ln in lanes:
+                ln.wait_stream(main)  # the final layer's dx / copy_rows and settle(ev) above
+        else:
+            lanes = [main]
+        Bh, Mh = B // S, M // S
+        nb_h, nq_h = ops.rmsnorm_bwd_blocks(Mh), ops.qknorm_rope_blocks(Mh)
+        spools = [_SubPool(pool, h, S) for h in range(S)] if S > 1 else [pool]
+
+        def rs(t, h):  # sub-batch h's rows of an [M, ...] buffer
+            return t if S == 1 else t[h * Mh:(h + 1) * Mh]
+
+        def bs(t, h):  # sub-batch h's sequences of a [B, ...] buffer
+            return t if (S == 1 or t is None) else t[h * Bh:(h + 1) * Bh]
+
+        def on(h):
+            return torch.cuda.stream(lanes[h]) if S > 1 else contextlib.nullcontext()
+
+        if side is not None:
+            def side_wait():
+                for ln in lanes:
+                    side.wait_stream(ln)
+            wait_inputs = side_wait
+
+            def settle(ev):  # noqa: F811  (every lane waits)
+                if ev is not None:
+                    for ln in lanes:
+                        ln.wait_event(ev)
+        else:
+            wait_inputs = None
+        self._wait_inputs = wait_inputs
+
         dctx = pool.get("dctx", (max(B * n_ctx, 1), D), F32)  # written by the first refresh block's ctx_rows
         dctx_set = False
         dqkv = pool.get("d_qkv", (M, 3 * D))
         delta = pool.get("delta", (B, Hh, rows), F32)
         n_dw = ops.attn_bwd_dw_rows(B, Hh, rows)
         qk_dw = pool.get("qk_dw_part", (n_dw, 128), F32)  # q_norm | k_norm weight-gradient partials
+        part1 = pool.get("rms_part1", (S * nb_h, D), F32)  # norm1's weight-gradient partial rows (per lane: nb_h)
+        part2 = pool.get("rms_part2", (S * nb_h, D), F32)  # norm2's
+        qkp = pool.get("qk_part", (S * nq_h, 128), F32)
         pre_zeroed = False
         scale = 1.0 / math.sqrt(cfg.head_dim)
         ck = st.get("ckpt", False)
-        ev_qkv = None  # the previous block's q|k|v wgrad (reads d_qkv, the QK-norm partial rows, xn1)
-        ready = None   # that block's name for on_ready, announced once its wgrads are waited for
+        kbias = st["kbias"]
+        ev_qkv = None  # the previous block's last side-stream event (its q|k|v wgrad, or norm1's reduce)
+        ready = None   # that block's name for on_ready, announced once its gradients are waited for
 
         def settle_qkv():
             nonlocal ev_qkv, ready
             settle(ev_qkv)
-            ev_qkv = None
             if ready is not None and on_ready is not None:
+                if S > 1:
+                    main.wait_event(ev_qkv)  # the bucket's collective is enqueued on the caller's stream
                 on_ready(ready)  # every gradient of that block is complete in the main stream's order
+            ev_qkv = None
             ready = None
+
+        def wg(dy, xin, out, bias=None, rows_sum=None):
+            """wgrad over the whole batch; the side stream waits for every lane first."""
+            return wgrad(dy, xin, out, bias, rows_sum)
 
         for i in reversed(range(cfg.depth)):
             w = self.blk[i]
@@ -420,9 +475,12 @@ class JiTEngine:
             x_in = pool.get(f"x{i}" if i > 0 else "x0", (M, D))
             if ck:
                 settle_qkv()  # the recompute below overwrites the ck.* activations the previous block's wgrads read
-            if ck:  # recompute the block's intermediates from its saved input (x{i+1} is left untouched)
-                self._block_forward(i, x_in, pool.get("ck.xout", (M, D)), tag, pool, B, rows, n_ctx, n_pre,
-                                    st["kbias"], cos_t, sin_t)
+                # recompute the block's intermediates from its saved input (x{i+1} is left untouched)
+                xo = pool.get("ck.xout", (M, D))
+                for hh in range(S):
+                    with on(hh):
+                        self._block_forward(i, rs(x_in, hh), rs(xo, hh), tag, spools[hh], Bh, rows, n_ctx, n_pre,
+                                            bs(kbias, hh), cos_t, sin_t)
             xn1, qkv, qk, o = (pool.get(tag + n, s) for n, s in (("xn1", (M, D)), ("qkv", (M, 3 * D)),
                                                                  ("qk", (M, 2 * D)), ("o", (M, D))))
             xm, xn2, x12, h = (pool.get(tag + n, s) for n, s in (("xm", (M, D)), ("xn2", (M, D)),
@@ -430,58 +488,90 @@ class JiTEngine:
             rstd1, rstd2 = pool.get(tag + "rstd1", (M,), F32), pool.get(tag + "rstd2", (M,), F32)
             lse = pool.get(tag + "lse", (B, Hh, rows), F32)
             n_i = rows if (n_ctx and self._ctx_present(i)) else n_pre
+            d_x12, d_h, d_b = pool.get("d_x12", (M, 2 * F)), pool.get("d_h", (M, F)), pool.get("d_b", (M, D))
+            dx_b, d_o, dx_a = pool.get("dx_b", (M, D)), pool.get("d_o", (M, D)), pool.get("dx_a", (M, D))
+            dqk = pool.get("d_qk", (M, 2 * D))
             # MLP
-            wgrad(dx, h, w["gw3"], w["gb3"])
-            dx12 = ops.linear_dgrad_swiglu(dx, w["pw3"], x12, pool.get("d_x12", (M, 2 * F)),
-                                           workspace=pool.get("d_h", (M, F)))
-            wgrad(dx12, xn2, w["gw12"], w["gb12"])
-            dxn2 = ops.linear_dgrad(dx12, w["pw12"], out=pool.get("d_b", (M, D)))
-            dxm, part = ops.rmsnorm_bwd(dxn2, xm, rstd2, w["pn2"], dres=dx, dx=pool.get("dx_b", (M, D)),
-                                        dw_part=pool.get("rms_part", (ops.rmsnorm_bwd_blocks(max(M, M2)), D), F32))
+            wg(dx, h, w["gw3"], w["gb3"])
+            for hh in range(S):
+                with on(hh):
+                    ops.linear_dgrad_swiglu(rs(dx, hh), w["pw3"], rs(x12, hh), rs(d_x12, hh), workspace=rs(d_h, hh))
+            wg(d_x12, xn2, w["gw12"], w["gb12"])
+            for hh in range(S):
+                with on(hh):
+                    ops.linear_dgrad(rs(d_x12, hh), w["pw12"], out=rs(d_b, hh))
+                    ops.rmsnorm_bwd(rs(d_b, hh), rs(xm, hh), rs(rstd2, hh), w["pn2"], dres=rs(dx, hh),
+                                    dx=rs(dx_b, hh), dw_part=part2[hh * nb_h:(hh + 1) * nb_h])
+            dxm = dx_b
             # attention (norm2's weight gradient: its partial rows summed by the o-projection wgrad's reduce launch)
-            ev_o = wgrad(dxm, o, w["gwo"], w["gbo"], rows_sum=(part[:ops.rmsnorm_bwd_blocks(M)], w["gn2"], acc))
-            do = ops.linear_dgrad(dxm, w["pwo"], out=pool.get("d_o", (M, D)))
+            ev_o = wg(dxm, o, w["gwo"], w["gbo"], rows_sum=(part2[:S * nb_h], w["gn2"], acc))
+            for hh in range(S):
+                with on(hh):
+                    ops.linear_dgrad(rs(dxm, hh), w["pwo"], out=rs(d_o, hh))
             settle_qkv()  # d_qkv and the QK-norm partial rows are rewritten below
             if FUSED_QKNORM_BWD and n_i < rows and not pre_zeroed:
                 # the context rows take no gradient in the blocks before context_start_block (the fused backward
                 # writes rows < n_i only; the standalone QK-norm backward below zeroes them itself)
                 dqkv.view(B, rows, 3 * D)[:, n_i:].zero_()
                 pre_zeroed = True
-            a5 = (ops._t4(qk, B, rows, Hh, 0), ops._t4(qk, B, rows, Hh, D), ops._t4(qkv, B, rows, Hh, 2 * D),
-                  ops._t4(o, B, rows, Hh, 0), ops._t4(do, B, rows, Hh, 0), lse, delta, st["kbias"])
-            if FUSED_QKNORM_BWD:
+            if FUSED_QKNORM_BWD:  # (S == 1)
                 # attention backward with the QK-RMSNorm + RoPE backward fused into its dQ / dK stores: dqkv receives
                 # the gradients of the raw q | k | v projections directly
+                a5 = (ops._t4(qk, B, rows, Hh, 0), ops._t4(qk, B, rows, Hh, D), ops._t4(qkv, B, rows, Hh, 2 * D),
+                      ops._t4(o, B, rows, Hh, 0), ops._t4(d_o, B, rows, Hh, 0), lse, delta, kbias)
                 ops.attn_bwd_qknorm(*a5, ops._t4(qkv, B, rows, Hh, 0), ops._t4(qkv, B, rows, Hh, D),
                                     w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, ops._t4(dqkv, B, rows, Hh, 0),
                                     ops._t4(dqkv, B, rows, Hh, D), qk_dw, ops._t4(dqkv, B, rows, Hh, 2 * D),
                                     B, Hh, rows, n_i, n_pre, scale)
                 qk_job = (qk_dw[:ops.attn_bwd_dw_rows(B, Hh, n_i)], w["gqk_norm"], acc)
             else:
-                dqk = pool.get("d_qk", (M, 2 * D))
-                ops.attn_bwd(*a5, ops._t4(dqk, B, rows, Hh, 0), ops._t4(dqk, B, rows, Hh, D),
-                             ops._t4(dqkv, B, rows, Hh, 2 * D), B, Hh, rows, n_i, n_pre, scale)
-                # rows >= n_i (a pre-context block's context rows): zero q | k | v gradients, dqk not read there
-                qpart = ops.qknorm_rope_bwd(dqk, qkv, w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, rows, dqkv,
-                                            dw_part=pool.get("qk_part", (ops.qknorm_rope_blocks(M), 128), F32),
-                                            n_valid=n_i)
-                qk_job = (qpart[:ops.qknorm_rope_blocks(M)], w["gqk_norm"], acc)
-            ev_qkv = wgrad(dqkv, xn1, w["gwqkv"], w["gbqkv"], rows_sum=qk_job)
-            dxn1 = ops.linear_dgrad(dqkv, w["pwqkv"], out=pool.get("d_b", (M, D)))
-            settle(ev_o)  # the MLP / o-projection wgrads read dx_a, dx_b and rms_part, rewritten from here on
-            dx_new, part = ops.rmsnorm_bwd(dxn1, x_in, rstd1, w["pn1"], dres=dxm, dx=pool.get("dx_a", (M, D)),
-                                           dw_part=pool.get("rms_part", (ops.rmsnorm_bwd_blocks(max(M, M2)), D), F32))
-            ops.reduce_rows(part[:ops.rmsnorm_bwd_blocks(M)], w["gn1"], acc)
+                for hh in range(S):
+                    with on(hh):
+                        qkh, qkvh, dqkh, dqkvh = rs(qk, hh), rs(qkv, hh), rs(dqk, hh), rs(dqkv, hh)
+                        ops.attn_bwd(ops._t4(qkh, Bh, rows, Hh, 0), ops._t4(qkh, Bh, rows, Hh, D),
+                                     ops._t4(qkvh, Bh, rows, Hh, 2 * D), ops._t4(rs(o, hh), Bh, rows, Hh, 0),
+                                     ops._t4(rs(d_o, hh), Bh, rows, Hh, 0), bs(lse, hh), bs(delta, hh), bs(kbias, hh),
+                                     ops._t4(dqkh, Bh, rows, Hh, 0), ops._t4(dqkh, Bh, rows, Hh, D),
+                                     ops._t4(dqkvh, Bh, rows, Hh, 2 * D), Bh, Hh, rows, n_i, n_pre, scale)
+                        # rows >= n_i (a pre-context block's context rows): zero q | k | v gradients, dqk not read there
+                        ops.qknorm_rope_bwd(dqkh, qkvh, w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, rows,
+                                            dqkvh, dw_part=qkp[hh * nq_h:(hh + 1) * nq_h], n_valid=n_i)
+                qk_job = (qkp[:S * nq_h], w["gqk_norm"], acc)
+            ev_qkv = wg(dqkv, xn1, w["gwqkv"], w["gbqkv"], rows_sum=qk_job)
+            for hh in range(S):
+                with on(hh):
+                    ops.linear_dgrad(rs(dqkv, hh), w["pwqkv"], out=rs(d_b, hh))
+            settle(ev_o)  # the MLP / o-projection wgrads read dx_a, dx_b and part2, rewritten from here on
+            for hh in range(S):
+                with on(hh):
+                    ops.rmsnorm_bwd(rs(d_b, hh), rs(x_in, hh), rs(rstd1, hh), w["pn1"], dres=rs(dxm, hh),
+                                    dx=rs(dx_a, hh), dw_part=part1[hh * nb_h:(hh + 1) * nb_h])
+            if S == 1:
+                ops.reduce_rows(part1[:nb_h], w["gn1"], acc)
+            else:  # over every lane's partial rows: on the side stream, after all lanes
+                side_wait()
+                with torch.cuda.stream(side):
+                    ops.reduce_rows(part1[:S * nb_h], w["gn1"], acc)
+                ev_qkv = torch.cuda.Event()
+                ev_qkv.record(side)
             if side is None:
                 if on_ready is not None:
                     on_ready(f"block{i}")  # every blocks.{i}.* gradient is enqueued
             else:
-                ready = f"block{i}"  # announced at the next settle_qkv(), after its q|k|v wgrad
-            dx = dx_new
+                ready = f"block{i}"  # announced at the next settle_qkv(), after its last side-stream launch
+            dx = dx_a
             if n_ctx and self._ctx_refresh(i):
-                ops.ctx_rows(dx, B, n_pre, rows, n_ctx, dctx=dctx, backward=True, overwrite=not dctx_set)
+                for hh in range(S):
+                    with on(hh):
+                        r0 = hh * Bh * n_ctx
+                        ops.ctx_rows(rs(dx, hh), Bh, n_pre, rows, n_ctx, dctx=dctx[r0:r0 + Bh * n_ctx],
+                                     backward=True, overwrite=not dctx_set)
                 dctx_set = True
         settle_qkv()
+        if S > 1:
+            for ln in lanes:
+                main.wait_stream(ln)
+        self._wait_inputs = None
         if side is not None:
             # the embeddings' small GEMMs reuse their gradient buffers back to back (d_h1 / d_a1 per embedder): they
             # run on the main stream, after every block's weight gradient
