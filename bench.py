@@ -180,10 +180,11 @@ def main():
     ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
                     help="optimizer per gradient bucket on a side stream as each all-reduce lands (auto: N > 1; "
                          "at N = 1 one launch after the backward measured faster: 166.9 vs 166.0 img/s, r03d)")
-    ap.add_argument("--wgrad-stream", default="side", choices=["side", "main"],
-                    help="the backward's weight-gradient GEMMs on a second stream beside the input-gradient chain "
-                         "(vpt.engine.CONCURRENT_WGRAD; side: +2.2 %% per C3 step, r05v) or on the step's stream. The "
-                         "probe pass always runs them on the step's stream, so per-kernel times are not shared")
+    ap.add_argument("--streams", default="multi", choices=["multi", "single"],
+                    help="multi: the engine's concurrent streams (the backward's weight-gradient GEMMs beside the "
+                         "input-gradient chain, vpt.engine.CONCURRENT_WGRAD: +2.2 %% per C3 step, r05v; the blocks as "
+                         "sub-batch lanes, vpt.engine.MICRO_SPLIT); single: every kernel on the step's stream. The probe "
+                         "pass always runs single, so per-kernel times are not shared with a concurrent kernel")
     ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c5"],
                     help="c3: JiT-B/16 1024^2 bucketed (the headline); c2: JiT-B/16 512^2 B=16; "
                          "c5: SDXL QLoRA transformer stacks")
@@ -215,7 +216,11 @@ def main():
     from vpt.jit_train import JiTTrainer
     from vpt.optim import RAdamScheduleFreeFlat
 
-    vpt_engine.CONCURRENT_WGRAD = args.wgrad_stream == "side"
+    if args.streams == "single":
+        vpt_engine.CONCURRENT_WGRAD = False
+        vpt_engine.MICRO_SPLIT = 1
+    timed_streams = dict(wgrad_stream="side" if vpt_engine.CONCURRENT_WGRAD else "step",
+                         sub_batches=vpt_engine.MICRO_SPLIT)
     cfg = JiT_B_16_Config()
     trainer = JiTTrainer(cfg, N_CLASSES, JiTTrainingConfig(loss_target="image"), device=device, seed=1234 + rank)
     trainer.engine.init_weights(seed=0)  # identical on every rank (replaces DDP's broadcast)
@@ -323,7 +328,7 @@ def main():
                    "one launch after the backward",
                    "grad_allreduce": "bf16 wire, per-block buckets overlapped with backward" if world > 1 else None,
                    "grad_checkpointing": bool(args.grad_ckpt),
-                   "wgrad_stream": args.wgrad_stream},
+                   "streams": timed_streams},
         "roofline": roofline_entry(dom, stats[dom], args.workload),
         "roofline_others": {k: roofline_entry(k, stats[k], args.workload) for k in mfma_ops if k != dom},
         "kernels": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in stats.items()},

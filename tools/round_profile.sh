@@ -9,10 +9,10 @@ WL=${2:-c3}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-# per-kernel times and counters with the weight gradients on the step's stream (as the bench's probe pass measures
-# them: a kernel sharing the chip with a concurrent wgrad would read slow); KT_SIDE=1 adds a trace of the default
-# (side-stream) schedule for its wall time
-CMD="$R/bench.py --workload $WL --steps 5 --warmup 2 --no-cpu-baseline --wgrad-stream main"
+# per-kernel times and counters with every kernel on the step's stream (as the bench's probe pass measures them: a
+# kernel sharing the chip with a concurrent one would read slow); KT_SIDE=1 adds a trace of the default (multi-stream)
+# schedule for its wall time
+CMD="$R/bench.py --workload $WL --steps 5 --warmup 2 --no-cpu-baseline --streams single"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktrace -o p -- python $CMD > $O/ktrace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o p -- python $CMD > $O/pmc_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o p -- python $CMD > $O/pmc_write.log 2>&1
