@@ -52,11 +52,13 @@ CONCURRENT_WGRAD = True
 WGRAD_STREAM_PRIORITY = 0
 WGRAD_SPLIT_DIV = 1  # 2: C3 step -5.5 % (r05x) -- the wgrads then lag the chain's hand-off waits
 WGRAD_SPLIT_MUL = 1
-# The forward's transformer blocks as MICRO_SPLIT independent sub-batches (B / MICRO_SPLIT sequences each) on their own
-# streams: every op is row- or sequence-local, so the sub-batches need no exchange and the result is bitwise the
-# one-batch forward; one sub-batch's kernels fill the CUs the other's leave idle in their last, partial round of work
-# items (the GEMMs' wave quantisation, the attention grids' tails). 1 = one stream.
-MICRO_SPLIT = 1
+# The transformer blocks as MICRO_SPLIT independent sub-batches (B / MICRO_SPLIT sequences each) on their own streams,
+# forward and input-gradient chain: every op there is row- or sequence-local, so the sub-batches need no exchange (the
+# forward is bitwise the one-batch forward; the backward's weight gradients still cover the whole batch); one
+# sub-batch's kernels fill the CUs the other's leave idle in their last, partial round of work items (the GEMMs' wave
+# quantisation, the attention grids' tails). 2: C3 step +1.8 % (r05za). 1 = one stream. Needs B % MICRO_SPLIT == 0
+# (else one stream).
+MICRO_SPLIT = 2
 
 
 class _SubPool:
