@@ -28,6 +28,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "vision-pt_amd"))
 sys.path.insert(0, ROOT)
 
+# HIP hardware queues per process (read at HIP's initialisation, so set before torch loads): at N > 1 the step runs six
+# streams -- the step's own, two sub-batch lanes, the weight-gradient stream, the optimizer's bucket stream and RCCL's
+# -- and with HIP's 4 queues some would share one and run behind each other. --hw-queues N (default 8, <= 32).
+_hwq = int(sys.argv[sys.argv.index("--hw-queues") + 1]) if "--hw-queues" in sys.argv else 8
+if not 1 <= _hwq <= 32:
+    raise SystemExit("--hw-queues: 1..32")
+os.environ["GPU_MAX_HW_QUEUES"] = str(_hwq)
+
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -180,6 +188,7 @@ def main():
     ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
                     help="optimizer per gradient bucket on a side stream as each all-reduce lands (auto: N > 1; "
                          "at N = 1 one launch after the backward measured faster: 166.9 vs 166.0 img/s, r03d)")
+    ap.add_argument("--hw-queues", type=int, default=8, help="GPU_MAX_HW_QUEUES for this process (applied at import)")
     ap.add_argument("--streams", default="multi", choices=["multi", "single"],
                     help="multi: the engine's concurrent streams (the backward's weight-gradient GEMMs beside the "
                          "input-gradient chain, vpt.engine.CONCURRENT_WGRAD: +2.2 %% per C3 step, r05v; the blocks as "
@@ -220,7 +229,7 @@ def main():
         vpt_engine.CONCURRENT_WGRAD = False
         vpt_engine.MICRO_SPLIT = 1
     timed_streams = dict(wgrad_stream="side" if vpt_engine.CONCURRENT_WGRAD else "step",
-                         sub_batches=vpt_engine.MICRO_SPLIT)
+                         sub_batches=vpt_engine.MICRO_SPLIT, hw_queues=int(os.environ["GPU_MAX_HW_QUEUES"]))
     cfg = JiT_B_16_Config()
     trainer = JiTTrainer(cfg, N_CLASSES, JiTTrainingConfig(loss_target="image"), device=device, seed=1234 + rank)
     trainer.engine.init_weights(seed=0)  # identical on every rank (replaces DDP's broadcast)
