@@ -58,7 +58,7 @@ WGRAD_SPLIT_MUL = 1
 # sub-batch's kernels fill the CUs the other's leave idle in their last, partial round of work items (the GEMMs' wave
 # quantisation, the attention grids' tails). 2: C3 step +1.8 % (r05za). 1 = one stream. Needs B % MICRO_SPLIT == 0
 # (else one stream).
-MICRO_SPLIT = 2
+MICRO_SPLIT = 1
 
 
 class _SubPool:
