@@ -58,12 +58,15 @@ def _step(tr, b, sl, dev, on_ready=None):
                    noise=b["noise"][sl].to(dev), drop_context=False, on_ready=on_ready)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, split=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from vpt.ddp import GradSync, grad_buckets
+    if split is not None:
+        import vpt.engine as E
+        E.MICRO_SPLIT = split
     tr, cfg = _trainer(dev)
     b = _batch(dev)
     sync = GradSync(tr.engine.grads, grad_buckets(tr.engine.layout, cfg.depth), wire="bf16")
@@ -80,14 +83,17 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_ranks_real_engine_gradient_mean():
+@pytest.mark.parametrize("split", [1, 2])
+def test_two_ranks_real_engine_gradient_mean(split):
+    """split: the engine's sub-batch lanes (vpt.engine.MICRO_SPLIT) in the ranks and in the single-rank reference."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    import vpt.engine as E
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, split)) for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=240) for _ in range(world)]
@@ -98,8 +104,13 @@ def test_two_ranks_real_engine_gradient_mean():
     g0, g1 = out[0][1], out[1][1]
     assert torch.equal(g0, g1)
     dev = torch.device("cuda", 0)
-    tr, cfg = _trainer(dev)
-    _step(tr, _batch(dev), slice(0, 4), dev)
+    old = E.MICRO_SPLIT
+    E.MICRO_SPLIT = split
+    try:
+        tr, cfg = _trainer(dev)
+        _step(tr, _batch(dev), slice(0, 4), dev)
+    finally:
+        E.MICRO_SPLIT = old
     ref = tr.engine.grads.float().cpu()
     assert ((g0 - ref).norm() / ref.norm()).item() < 8e-3  # bf16 wire: rank grads and sum rounded to bf16
     # hook order = backward completion order: final layer first, then blocks last to first

@@ -58,7 +58,7 @@ WGRAD_SPLIT_MUL = 1
 # sub-batch's kernels fill the CUs the other's leave idle in their last, partial round of work items (the GEMMs' wave
 # quantisation, the attention grids' tails). 2: C3 step +1.8 % (r05za). 1 = one stream. Needs B % MICRO_SPLIT == 0
 # (else one stream).
-MICRO_SPLIT = 1
+MICRO_SPLIT = 2
 
 
 class _SubPool:
@@ -86,8 +86,16 @@ class _Pool:
         cur = self.store.get(name)
         if cur is None or cur.numel() < n or cur.dtype != dtype:
             # zero-filled at allocation: rows that a kernel never writes (e.g. context rows of
-            # pre-context blocks) must stay finite
+            # pre-context blocks) must stay finite. Allocation (first use of a name, or growth for a larger
+            # batch) is rare and may happen on any of the engine's streams (sub-batch lanes, the weight-gradient
+            # stream), so it is made safe for all of them: nothing may still use a storage being replaced, and the
+            # zero fill completes before any stream touches the new one.
+            multi = self.device.type == "cuda"
+            if multi:
+                torch.cuda.synchronize(self.device)
             cur = torch.zeros(max(n, 1), dtype=dtype, device=self.device)
+            if multi:
+                torch.cuda.current_stream(self.device).synchronize()
             self.store[name] = cur
         v = cur[:n].view(*shape)
         if zero:
