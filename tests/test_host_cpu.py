@@ -147,3 +147,23 @@ def test_capi_reports_errors_without_gpu_work():
     rc = _lib.lib.vpt_gemm_bf16(None, 0, 1, None, 0, 1, None, 0, 0, 0, 0, None, None, 0, 0, 0, 1, None, 1.0, None)
     assert rc == 1
     assert b"null operand" in _lib.lib.vpt_last_error_string()
+
+
+def test_sub_pool_slices_one_storage():
+    """engine._SubPool (the sub-batch lanes' view of the buffer pool): lane h of n gets rows [h*r, (h+1)*r) of ONE
+    pooled buffer of n*r rows, whatever the trailing shape, so the lanes write disjoint halves the one-lane backward
+    then reads whole."""
+    import torch
+
+    from vpt.engine import _Pool, _SubPool
+    pool = _Pool(torch.device("cpu"))
+    a, b = _SubPool(pool, 0, 2).get("x", (3, 4)), _SubPool(pool, 1, 2).get("x", (3, 4))
+    full = pool.get("x", (6, 4))
+    a.fill_(1.0)
+    b.fill_(2.0)
+    assert full[:3].eq(1.0).all() and full[3:].eq(2.0).all()
+    lse0 = _SubPool(pool, 0, 2).get("lse", (2, 5, 7), torch.float32)
+    lse1 = _SubPool(pool, 1, 2).get("lse", (2, 5, 7), torch.float32)
+    whole = pool.get("lse", (4, 5, 7), torch.float32)
+    assert lse0.data_ptr() == whole.data_ptr() and lse1.data_ptr() == whole[2:].data_ptr()
+    assert lse1.shape == (2, 5, 7)
