@@ -186,8 +186,9 @@ def main():
     ap.add_argument("--grad-ckpt", action="store_true",
                     help="gradient checkpointing on (denoiser.py:945-967): keep block inputs, recompute in backward")
     ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
-                    help="optimizer per gradient bucket on a side stream as each all-reduce lands (auto: N > 1; "
-                         "at N = 1 one launch after the backward measured faster: 166.9 vs 166.0 img/s, r03d)")
+                    help="optimizer per gradient bucket on a side stream as each all-reduce lands (auto: off -- "
+                         "beside the engine's concurrent streams it costs 6 %% at N = 1, 163.5 vs 174.1 img/s, r05ze; "
+                         "the all-reduces themselves still run under the backward at any setting)")
     ap.add_argument("--hw-queues", type=int, default=8, help="GPU_MAX_HW_QUEUES for this process (applied at import)")
     ap.add_argument("--streams", default="multi", choices=["multi", "single"],
                     help="multi: the engine's concurrent streams (the backward's weight-gradient GEMMs beside the "
@@ -238,7 +239,7 @@ def main():
     opt.train()
     # per-block buckets: all-reduced (bf16 wire, as the reference's DDP reduces its bf16 .grad tensors) the
     # moment the backward completes them and stepped by the optimizer on a side stream as each reduction lands
-    overlap = args.overlap == "on" or (args.overlap == "auto" and world > 1)
+    overlap = args.overlap == "on"
     sync = GradSync(trainer.engine.grads, grad_buckets(trainer.engine.layout, cfg.depth), wire="bf16",
                     overlap=overlap)
     losslog = LossLog(device)
