@@ -27,11 +27,12 @@ def main():
     ap.add_argument("--setter", default="vpt_attn_set_xcd_order")
     ap.add_argument("--value", type=int, default=1, help="the B value")
     ap.add_argument("--base", type=int, default=0, help="the A value")
+    ap.add_argument("--shape", default="c3", choices=["c3", "c2"], help="c3: B=8, n=4170 (1024^2); c2: B=16, n=1098 (512^2)")
     args = ap.parse_args()
     _lib.use_diag()
     setter = getattr(_lib.lib, args.setter)
     dev = torch.device("cuda", 0)
-    B, H, n, nd = 8, 12, 4170, 4106
+    B, H, n, nd = (8, 12, 4170, 4106) if args.shape == "c3" else (16, 12, 1098, 1034)
     D = 64 * H
     M = B * n
     g = torch.Generator(device=dev).manual_seed(0)
