@@ -29,6 +29,7 @@ def main():
     ap.add_argument("knobs", help="comma-separated vpt.engine globals switched together")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--grad-ckpt", action="store_true", help="gradient checkpointing on")
     args = ap.parse_args()
     knobs = args.knobs.split(",")
     # diagnostic-library switches (loads the diagnostic library): name -> setter(on)
@@ -75,6 +76,7 @@ def main():
     torch.cuda.set_device(dev)
     tr = JiTTrainer(JiT_B_16_Config(), bench.N_CLASSES, JiTTrainingConfig(loss_target="image"), device=dev, seed=1)
     tr.engine.init_weights(seed=0)
+    tr.engine.set_gradient_checkpointing(args.grad_ckpt)
     opt = RAdamScheduleFreeFlat(tr.engine.params, tr.engine.grads, lr=1e-4)
     opt.train()
     batches = bench.make_batches(8, dev, seed=100)
