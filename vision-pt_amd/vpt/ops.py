@@ -1056,12 +1056,13 @@ class _LoraBatch:
     vpt_lora_wgrad_reduce_batch launch per 32 jobs (2 per LoRA target) -- instead of two launches per target.
     The operand tensors are held until the flush (their memory is not reused before the slab launch)."""
 
-    def __init__(self):
+    def __init__(self, side=None):
         self.jobs: list = []
         self.pjobs: list = []  # deferred slab jobs
         self.keep: list = []   # their operand tensors
         self.key = None  # (alpha, accumulate) of the pending jobs
         self.nws = 0     # workspaces handed out since the last flush
+        self.side = side  # a stream the flushes run on (beside the caller's), or None
 
     def reserve(self, key, njobs):
         """Called BEFORE a target takes its workspaces: flushes first when its jobs would not fit, so the
@@ -1083,15 +1084,27 @@ class _LoraBatch:
         self.keep.extend(tensors)
 
     def flush(self):
-        for i in range(0, len(self.pjobs), 24):
-            chunk = self.pjobs[i:i + 24]
-            arr = (_LoraWgradJob * len(chunk))(*chunk)
-            call("vpt_lora_wgrad_partial_batch", ctypes.addressof(arr), len(chunk), stream())
+        if not self.pjobs and not self.jobs:
+            return
+        ctx = contextlib.nullcontext()
+        if self.side is not None:
+            # the slab and reduce launches on the side stream, behind everything the caller's stream enqueued
+            # (the operands); the operand tensors are marked as used there so the allocator does not hand their
+            # memory out again before these launches ran; the workspaces are touched by the side stream alone
+            self.side.wait_stream(torch.cuda.current_stream())
+            for t in self.keep:
+                t.record_stream(self.side)
+            ctx = torch.cuda.stream(self.side)
+        with ctx:
+            for i in range(0, len(self.pjobs), 24):
+                chunk = self.pjobs[i:i + 24]
+                arr = (_LoraWgradJob * len(chunk))(*chunk)
+                call("vpt_lora_wgrad_partial_batch", ctypes.addressof(arr), len(chunk), stream())
+            if self.jobs:
+                arr = (_LoraReduceJob * len(self.jobs))(*self.jobs)
+                call("vpt_lora_wgrad_reduce_batch", ctypes.addressof(arr), len(self.jobs), float(self.key[0]),
+                     int(self.key[1]), stream())
         self.pjobs, self.keep = [], []
-        if self.jobs:
-            arr = (_LoraReduceJob * len(self.jobs))(*self.jobs)
-            call("vpt_lora_wgrad_reduce_batch", ctypes.addressof(arr), len(self.jobs), float(self.key[0]),
-                 int(self.key[1]), stream())
         self.jobs, self.nws = [], 0
 
 
@@ -1103,15 +1116,16 @@ _LORA_BATCHED = True
 
 
 @contextlib.contextmanager
-def lora_wgrad_batch():
+def lora_wgrad_batch(side=None):
     """Within the block, lora_wgrad2 only writes its split-M slabs (each target into its own workspace) and the
-    reduces run batched at exit (or every 32 jobs): same results, ~1/16 of the reduce launches."""
+    reduces run batched at exit (or every 32 jobs): same results, ~1/16 of the reduce launches. side: a stream the
+    batched launches run on beside the caller's (the caller joins it before reading the adapter gradients)."""
     global _LORA_BATCH
     if not _LORA_BATCHED:  # per-target reduces (A/B: tools/c5_knob_ab.py)
         yield
         return
     outer = _LORA_BATCH
-    _LORA_BATCH = _LoraBatch()
+    _LORA_BATCH = _LoraBatch(side)
     try:
         yield
         _LORA_BATCH.flush()
@@ -1146,6 +1160,8 @@ def lora_wgrad2(dy, ds, g_up, x, vs, g_down, accumulate=True, alpha=1.0):
                  _LoraWgradJob(x.data_ptr(), x.stride(0), vs.data_ptr(), vs.stride(0), ws_dn.data_ptr(), n_in, M)],
                 (dy, ds, x, vs))
     else:
+        if b.side is not None:  # the slabs may still be read by a side-stream reduce of an earlier flush
+            torch.cuda.current_stream().wait_stream(b.side)
         call("vpt_lora_wgrad2_partial", dy.data_ptr(), dy.stride(0), ds.data_ptr(), ds.stride(0), n_out,
              x.data_ptr(), x.stride(0), vs.data_ptr(), vs.stride(0), n_in, M, ws_up.data_ptr(), ws_dn.data_ptr(),
              stream())

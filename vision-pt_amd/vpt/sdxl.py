@@ -15,6 +15,8 @@ a30  SDXLTransformerBlock: TransformerBlock.forward (src/models/sdxl/denoiser.py
 from __future__ import annotations
 
 
+import contextlib
+
 import torch
 
 from . import ops
@@ -272,6 +274,36 @@ FUSED_LN_BWD_LORA = True  # the backward half alone
 FOLD_Q_SCALE = True
 # True = the GeGLU backward also emits ff.net.0.proj's input-gradient LoRA operand (ops.geglu_bwd_lora)
 FUSED_GEGLU_LORA = True
+# True = inside a training step's backward (lora_side_scope), each block's batched adapter-gradient launches
+# (ops.lora_wgrad_batch) run on a side stream beside the input-gradient chain (nothing in the chain reads an adapter
+# gradient); the scope's exit joins the side stream, before anything reads the adapter gradients
+LORA_WGRAD_SIDE = True
+_SIDE: dict = {}
+_SIDE_SCOPE = [0]
+
+
+def lora_side(device) -> torch.cuda.Stream | None:
+    """The adapter-gradient side stream of a device while a lora_side_scope is open (else None: same stream)."""
+    if not (LORA_WGRAD_SIDE and _SIDE_SCOPE[0]) or torch.device(device).type != "cuda":
+        return None
+    key = str(torch.device(device))
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=device)
+    return _SIDE[key]
+
+
+@contextlib.contextmanager
+def lora_side_scope(device):
+    """A training step's backward: adapter-gradient batches on the side stream; on exit the caller's stream waits
+    for all of them (the adapter gradients are then complete in its order)."""
+    _SIDE_SCOPE[0] += 1
+    try:
+        yield
+    finally:
+        _SIDE_SCOPE[0] -= 1
+        st = _SIDE.get(str(torch.device(device)))
+        if st is not None:
+            torch.cuda.current_stream(device).wait_stream(st)
 
 
 def _ctx_key(ctx: torch.Tensor) -> tuple:
@@ -469,7 +501,7 @@ class SDXLTransformerBlock:
         targets' adapter-gradient reduces run as one batched launch at the end (ops.lora_wgrad_batch).
         need_dctx=False: the context needs no gradient (the reference's text-encoder states are produced under
         no_grad, train/sdxl/flow_match.py:115-124), so the to_k / to_v input-gradient GEMMs are skipped."""
-        with ops.lora_wgrad_batch():
+        with ops.lora_wgrad_batch(side=lora_side(self.device)):
             return self._backward(dy, need_dctx)
 
     def _backward(self, dy: torch.Tensor, need_dctx: bool = True):

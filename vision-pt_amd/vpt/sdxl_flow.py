@@ -29,6 +29,7 @@ import math
 import torch
 
 from . import ops
+from .sdxl import lora_side_scope
 from .sdxl_train import CONTEXT_DIM, CONTEXT_TOKENS, SDXL_1024_STACKS, SDXLStacksQLoRA
 from .timestep import sample_timestep
 
@@ -261,7 +262,8 @@ class SDXLFlowMatchQLoRA:
         dv = torch.empty_like(v) if backward else None
         ops.velocity_loss(v, latents, eps, self.loss, dv)
         if backward:
-            self.backward(dv)
+            with lora_side_scope(self.device):  # adapter gradients beside the chain, joined before anything reads them
+                self.backward(dv)
             if optimizer_step:
                 self.opt.step()
         self._last = dict(t=t, z=z, eps=eps)

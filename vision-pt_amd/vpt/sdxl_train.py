@@ -33,7 +33,7 @@ import torch
 
 from . import ops
 from .optim import RAdamScheduleFreeFlat
-from .sdxl import TARGETS, SDXLSpatialTransformer, dynamic_map
+from .sdxl import TARGETS, SDXLSpatialTransformer, dynamic_map, lora_side_scope
 
 BF16, F32 = torch.bfloat16, torch.float32
 
@@ -229,9 +229,10 @@ class SDXLStacksQLoRA:
         for x, (_, C, _, st) in zip(xs, self.stacks):
             st.forward(x, ctx, self.B, x.shape[2], self.n_ctx)
         dctx = None
-        for gout, (_, C, _, st) in zip(reversed(gs), reversed(self.stacks)):
-            _dx, dc = st.backward(gout)
-            dctx = dc if dctx is None else ops.add_bf16(dctx, dc)
+        with lora_side_scope(self.device):  # adapter gradients beside the chain, joined before the optimizer
+            for gout, (_, C, _, st) in zip(reversed(gs), reversed(self.stacks)):
+                _dx, dc = st.backward(gout)
+                dctx = dc if dctx is None else ops.add_bf16(dctx, dc)
         self.opt.step()
         return dctx
 
