@@ -276,8 +276,9 @@ FOLD_Q_SCALE = True
 FUSED_GEGLU_LORA = True
 # True = inside a training step's backward (lora_side_scope), each block's batched adapter-gradient launches
 # (ops.lora_wgrad_batch) run on a side stream beside the input-gradient chain (nothing in the chain reads an adapter
-# gradient); the scope's exit joins the side stream, before anything reads the adapter gradients
-LORA_WGRAD_SIDE = True
+# gradient); the scope's exit joins the side stream, before anything reads the adapter gradients. Measured -1.5 % per
+# C5 step (r05zm: the batched slab / reduce launches are short and their join points close), so off.
+LORA_WGRAD_SIDE = False
 _SIDE: dict = {}
 _SIDE_SCOPE = [0]
 
