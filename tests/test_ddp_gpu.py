@@ -67,6 +67,7 @@ def _worker(rank, world, port, q, split=None):
     if split is not None:
         import vpt.engine as E
         E.MICRO_SPLIT = split
+        E.MICRO_SPLIT_MIN_ROWS = 0  # lanes at the micro size too
     tr, cfg = _trainer(dev)
     b = _batch(dev)
     sync = GradSync(tr.engine.grads, grad_buckets(tr.engine.layout, cfg.depth), wire="bf16")
@@ -104,13 +105,13 @@ def test_two_ranks_real_engine_gradient_mean(split):
     g0, g1 = out[0][1], out[1][1]
     assert torch.equal(g0, g1)
     dev = torch.device("cuda", 0)
-    old = E.MICRO_SPLIT
-    E.MICRO_SPLIT = split
+    old, old_min = E.MICRO_SPLIT, E.MICRO_SPLIT_MIN_ROWS
+    E.MICRO_SPLIT, E.MICRO_SPLIT_MIN_ROWS = split, 0
     try:
         tr, cfg = _trainer(dev)
         _step(tr, _batch(dev), slice(0, 4), dev)
     finally:
-        E.MICRO_SPLIT = old
+        E.MICRO_SPLIT, E.MICRO_SPLIT_MIN_ROWS = old, old_min
     ref = tr.engine.grads.float().cpu()
     assert ((g0 - ref).norm() / ref.norm()).item() < 8e-3  # bf16 wire: rank grads and sum rounded to bf16
     # hook order = backward completion order: final layer first, then blocks last to first

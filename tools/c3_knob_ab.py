@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--grad-ckpt", action="store_true", help="gradient checkpointing on")
+    ap.add_argument("--workload", default="c3", choices=["c3", "c2"], help="c2: 512^2 buckets, B=16")
     args = ap.parse_args()
     knobs = args.knobs.split(",")
     # diagnostic-library switches (loads the diagnostic library): name -> setter(on)
@@ -79,7 +80,8 @@ def main():
     tr.engine.set_gradient_checkpointing(args.grad_ckpt)
     opt = RAdamScheduleFreeFlat(tr.engine.params, tr.engine.grads, lr=1e-4)
     opt.train()
-    batches = bench.make_batches(8, dev, seed=100)
+    batches = (bench.make_batches(8, dev, seed=100) if args.workload == "c3"
+               else bench.make_batches(16, dev, seed=100, buckets=bench.BUCKETS_C2))
     it = [0]
 
     def step():
@@ -117,7 +119,7 @@ def main():
     med = {k: sorted(v)[len(v) // 2] for k, v in res.items()}
     print(json.dumps({"knobs": knobs, "ms_per_step": {k: [round(x, 3) for x in v] for k, v in res.items()},
                       "median_ms": {k: round(v, 3) for k, v in med.items()},
-                      "img_s_median": {k: round(8e3 / v, 3) for k, v in med.items()},
+                      "img_s_median": {k: round((8e3 if args.workload == "c3" else 16e3) / v, 3) for k, v in med.items()},
                       "gain": round(med["0"] / med["1"] - 1, 4)}))
 
 

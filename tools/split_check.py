@@ -19,7 +19,7 @@ from tests.test_ddp_gpu import _batch, _step, _trainer  # noqa: E402
 
 
 def run(split, conc, B):
-    E.MICRO_SPLIT, E.CONCURRENT_WGRAD = split, conc
+    E.MICRO_SPLIT, E.CONCURRENT_WGRAD, E.MICRO_SPLIT_MIN_ROWS = split, conc, 0
     dev = torch.device("cuda", 0)
     tr, cfg = _trainer(dev)
     _step(tr, _batch(dev), slice(0, B), dev)
@@ -31,7 +31,7 @@ def hook_check(split, B):
     """Copies every bucket's gradient slice at its on_ready call (on the caller's stream, as GradSync's wire cast does)
     and compares the copies with the final gradients."""
     from vpt.ddp import grad_buckets
-    E.MICRO_SPLIT, E.CONCURRENT_WGRAD = split, True
+    E.MICRO_SPLIT, E.CONCURRENT_WGRAD, E.MICRO_SPLIT_MIN_ROWS = split, True, 0
     dev = torch.device("cuda", 0)
     tr, cfg = _trainer(dev)
     buckets = {n: (lo, hi) for n, lo, hi in grad_buckets(tr.engine.layout, cfg.depth)}

@@ -56,9 +56,19 @@ WGRAD_SPLIT_MUL = 1
 # forward and input-gradient chain: every op there is row- or sequence-local, so the sub-batches need no exchange (the
 # forward is bitwise the one-batch forward; the backward's weight gradients still cover the whole batch); one
 # sub-batch's kernels fill the CUs the other's leave idle in their last, partial round of work items (the GEMMs' wave
-# quantisation, the attention grids' tails). 2: C3 step +1.8 % (r05za). 1 = one stream. Needs B % MICRO_SPLIT == 0
-# (else one stream).
+# quantisation, the attention grids' tails). 2: C3 step +1.8 % (r05za), +2.5 % with checkpointing (r05zi); at C2
+# (512^2, B=16: 8.8k rows per lane) -3.6 % (r05zo) -- the lanes' halved grids then underfill the chip -- so lanes are
+# used only when each keeps at least MICRO_SPLIT_MIN_ROWS token rows. 1 = one stream. Needs B % MICRO_SPLIT == 0.
 MICRO_SPLIT = 2
+MICRO_SPLIT_MIN_ROWS = 12288
+
+
+def _lanes(B: int, rows: int, device) -> int:
+    """The number of sub-batch lanes for a batch of B sequences of `rows` token rows."""
+    S = MICRO_SPLIT
+    if S > 1 and B % S == 0 and (B // S) * rows >= MICRO_SPLIT_MIN_ROWS and torch.device(device).type == "cuda":
+        return S
+    return 1
 
 
 class _SubPool:
@@ -236,7 +246,7 @@ class JiTEngine:
         x = pool.get("x0", (M, D))
         ops.assemble_tokens(pe2, semb, temb, p["time_position_embeds"], ctx, n_ctx, B, np_, rows, x)
         # --- blocks (denoiser.py:1087-1113)
-        S = MICRO_SPLIT if (MICRO_SPLIT > 1 and B % MICRO_SPLIT == 0 and self.device.type == "cuda") else 1
+        S = _lanes(B, rows, self.device)
         if S > 1:
             main = torch.cuda.current_stream(self.device)
             while len(self._mstreams) < S:
@@ -412,8 +422,7 @@ class JiTEngine:
         # independent sub-batches on their own streams ("lanes"), like the forward; every weight gradient -- and
         # norm1's weight-gradient reduce -- covers the whole batch on the side stream once all lanes produced its
         # inputs. S = 1: one lane, the caller's stream.
-        S = MICRO_SPLIT if (MICRO_SPLIT > 1 and B % MICRO_SPLIT == 0 and side is not None
-                            and not FUSED_QKNORM_BWD) else 1
+        S = _lanes(B, rows, self.device) if (side is not None and not FUSED_QKNORM_BWD) else 1
         if S > 1:
             while len(self._mstreams) < S:
                 self._mstreams.append(torch.cuda.Stream(device=self.device))
