@@ -68,6 +68,7 @@ def _worker(rank, world, port, q, split=None):
         import vpt.engine as E
         E.MICRO_SPLIT = split
         E.MICRO_SPLIT_MIN_ROWS = 0  # lanes at the micro size too
+        E.MICRO_SPLIT_BWD = True    # and in the backward (the on_ready hand-offs across lanes)
     tr, cfg = _trainer(dev)
     b = _batch(dev)
     sync = GradSync(tr.engine.grads, grad_buckets(tr.engine.layout, cfg.depth), wire="bf16")
@@ -105,13 +106,13 @@ def test_two_ranks_real_engine_gradient_mean(split):
     g0, g1 = out[0][1], out[1][1]
     assert torch.equal(g0, g1)
     dev = torch.device("cuda", 0)
-    old, old_min = E.MICRO_SPLIT, E.MICRO_SPLIT_MIN_ROWS
-    E.MICRO_SPLIT, E.MICRO_SPLIT_MIN_ROWS = split, 0
+    old, old_min, old_bwd = E.MICRO_SPLIT, E.MICRO_SPLIT_MIN_ROWS, E.MICRO_SPLIT_BWD
+    E.MICRO_SPLIT, E.MICRO_SPLIT_MIN_ROWS, E.MICRO_SPLIT_BWD = split, 0, True
     try:
         tr, cfg = _trainer(dev)
         _step(tr, _batch(dev), slice(0, 4), dev)
     finally:
-        E.MICRO_SPLIT, E.MICRO_SPLIT_MIN_ROWS = old, old_min
+        E.MICRO_SPLIT, E.MICRO_SPLIT_MIN_ROWS, E.MICRO_SPLIT_BWD = old, old_min, old_bwd
     ref = tr.engine.grads.float().cpu()
     assert ((g0 - ref).norm() / ref.norm()).item() < 8e-3  # bf16 wire: rank grads and sum rounded to bf16
     # hook order = backward completion order: final layer first, then blocks last to first

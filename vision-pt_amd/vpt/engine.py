@@ -61,6 +61,11 @@ WGRAD_SPLIT_MUL = 1
 # used only when each keeps at least MICRO_SPLIT_MIN_ROWS token rows. 1 = one stream. Needs B % MICRO_SPLIT == 0.
 MICRO_SPLIT = 2
 MICRO_SPLIT_MIN_ROWS = 12288
+# Where the lanes run (r05zr, same-box A/Bs at C3 with the other half on): in the forward +2.5 %; in the backward's
+# input-gradient chain -1.2 % (there the side-stream weight gradients already fill the chain's partial rounds, and the
+# lanes' extra hand-offs cost more than they fill), so the backward runs one lane by default.
+MICRO_SPLIT_FWD = True
+MICRO_SPLIT_BWD = False
 
 
 def _lanes(B: int, rows: int, device) -> int:
@@ -246,7 +251,7 @@ class JiTEngine:
         x = pool.get("x0", (M, D))
         ops.assemble_tokens(pe2, semb, temb, p["time_position_embeds"], ctx, n_ctx, B, np_, rows, x)
         # --- blocks (denoiser.py:1087-1113)
-        S = _lanes(B, rows, self.device)
+        S = _lanes(B, rows, self.device) if MICRO_SPLIT_FWD else 1
         if S > 1:
             main = torch.cuda.current_stream(self.device)
             while len(self._mstreams) < S:
@@ -422,7 +427,7 @@ class JiTEngine:
         # independent sub-batches on their own streams ("lanes"), like the forward; every weight gradient -- and
         # norm1's weight-gradient reduce -- covers the whole batch on the side stream once all lanes produced its
         # inputs. S = 1: one lane, the caller's stream.
-        S = _lanes(B, rows, self.device) if (side is not None and not FUSED_QKNORM_BWD) else 1
+        S = _lanes(B, rows, self.device) if (side is not None and not FUSED_QKNORM_BWD and MICRO_SPLIT_BWD) else 1
         if S > 1:
             while len(self._mstreams) < S:
                 self._mstreams.append(torch.cuda.Stream(device=self.device))
