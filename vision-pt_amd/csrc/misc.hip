@@ -21,11 +21,13 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 // Counter-based standard normals, rounded to fp16 like randn_like(fp16 image): pixel pair j = idx / 2 is one
-// Box-Muller draw from two keyed 32-bit hashes of j (lowbias32: 2 multiplies, 3 xor-shifts), element 2j taking
+// Box-Muller draw from ONE keyed 32-bit hash of j (lowbias32: 2 multiplies, 3 xor-shifts; a bijection of j for a
+// fixed key, so no two pairs of an image share a hash), its high half the radius uniform u1 and its low half the
+// angle u2 (16 bits each: radii up to 4.85 sigma, 65536 angles -- finer than the fp16 result), element 2j taking
 // r cos(2 pi u2), element 2j+1 r sin(2 pi u2). On the transcendental units: v_log_f32 (log2; ln u1 = ln2 log2 u1),
-// v_cos_f32 / v_sin_f32 (argument in revolutions: no range reduction). 32-bit integer work only and both draws of
-// a pair used: the per-element cost is a quarter of a 64-bit splitmix per element, which kept the noising pass
-// VALU-bound. A pure function of (seed, idx): the loss regenerates the forward's noise.
+// v_sqrt_f32, v_cos_f32 / v_sin_f32 (argument in revolutions: no range reduction). The 32-bit multiplies are the
+// expensive integer ops here (two per pair; the two-hash form had seven with its counter mixing). A pure function
+// of (seed, idx): the loss regenerates the forward's noise.
 struct NoiseKey {
   uint32_t a, b;
 };
@@ -43,15 +45,14 @@ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
 }
 __device__ __forceinline__ uint32_t pair_counter(uint64_t idx) {
   const uint64_t j = idx >> 1;
-  return (uint32_t)j ^ ((uint32_t)(j >> 32) * 0x85ebca6bu);
+  return (uint32_t)j ^ (uint32_t)(j >> 32);  // pairs past 2^32 (batches > 8 G pixels) folded in without a multiply
 }
 // (radius, angle in revolutions) of pair j
 __device__ __forceinline__ float2 gauss_polar(NoiseKey k, uint32_t j) {
-  const uint32_t w = j * 0x9e3779b9u;
-  const uint32_t h1 = lowbias32(w + k.a), h2 = lowbias32(w ^ k.b);
-  const float u1 = ((float)(h1 >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0,1)
-  const float u2 = (float)(h2 >> 8) * (1.0f / 16777216.0f);            // [0,1)
-  return {sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1)), u2};
+  const uint32_t h = lowbias32((j ^ k.a) + k.b);
+  const float u1 = ((float)(h >> 16) + 0.5f) * (1.0f / 65536.0f);  // (0,1)
+  const float u2 = (float)(h & 0xffffu) * (1.0f / 65536.0f);       // [0,1)
+  return {__builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1)), u2};
 }
 // both elements of pair j (fp16-rounded)
 __device__ __forceinline__ void gauss_pair_fp16(NoiseKey k, uint32_t j, float& g0, float& g1) {
@@ -78,39 +79,22 @@ __device__ __forceinline__ Strip strip_of(long s, int hp, int wp) {
   r.np = min(kStripP, wp - r.px0);
   return r;
 }
-// Stage the strip's pixels (fp16 / bf16 bits) into px[c][ky][0, 16 np) and, with want_eps, its noise
-// eps = fp16(noise * noise_scale) (explicit fp16 `noise`, or generated) into eps[c][ky][...]: 16-B pieces of 8 pixels
-// of one image row. (Loading the next strip's pieces into registers one strip ahead was measured slower: the extra
-// registers cost more waves per CU than the overlap gained, r04p.)
-__device__ __forceinline__ void stage_strip(const Strip& st, const unsigned short* __restrict__ img,
-                                            const unsigned short* __restrict__ noise, bool want_eps, NoiseKey key,
-                                            float noise_scale, int H, int W,
-                                            unsigned short (&px)[3][16][16 * kStripP],
-                                            unsigned short (&eps)[3][16][16 * kStripP]) {
-  const int cpr = st.np * 2;  // 16-B pieces per image row of the strip
-  for (int i = threadIdx.x; i < 48 * cpr; i += blockDim.x) {
-    const int rr = i / cpr, cc = i - rr * cpr, c = rr >> 4, ky = rr & 15;
-    const long base = (((long)st.b * 3 + c) * H + st.py * 16 + ky) * W + st.px0 * 16 + cc * 8;
-    *reinterpret_cast<uint4*>(&px[c][ky][cc * 8]) = *reinterpret_cast<const uint4*>(img + base);
-    if (!want_eps) continue;
-    float nz[8];
-    if (noise) {
-      const uint4 nv = *reinterpret_cast<const uint4*>(noise + base);
-      const unsigned short* ns = reinterpret_cast<const unsigned short*>(&nv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) nz[e] = h2f(ns[e]);
-    } else {
-      const uint32_t j0 = pair_counter((uint64_t)base);  // base is even (W, x multiples of 8)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) gauss_pair_fp16(key, j0 + e, nz[2 * e], nz[2 * e + 1]);
-    }
-    unsigned short ev[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) ev[e] = f2h(nz[e] * noise_scale);
-    *reinterpret_cast<uint4*>(&eps[c][ky][cc * 8]) = *reinterpret_cast<const uint4*>(ev);
-  }
+// Image-row piece i (< 384) of a strip with cpr in {2, 4, 6, 8} 16-B pieces per row -> row rr = c * 16 + ky and
+// piece cc: rr = i / cpr as a 24-bit multiply by the block's rounded-up reciprocal (exact for i < 2^15), no division
+// or 32-bit multiply per piece; and the piece's element offset in the image, (c * H + ky) * W + 8 cc (< 2^31).
+struct PieceMap {
+  int cpr, magic, H, W;
+};
+__device__ __forceinline__ PieceMap piece_map(int np, int H, int W) {
+  return {2 * np, (65536 + 2 * np - 1) / (2 * np), H, W};
 }
-
+__device__ __forceinline__ void piece_of(const PieceMap& m, int i, int& c, int& ky, int& cc, int& off) {
+  const int rr = (int)(__umul24((unsigned)i, (unsigned)m.magic) >> 16);
+  cc = i - (int)__umul24((unsigned)rr, (unsigned)m.cpr);
+  c = rr >> 4;
+  ky = rr & 15;
+  off = (int)__umul24((unsigned)(__umul24((unsigned)c, (unsigned)m.H) + ky), (unsigned)m.W) + cc * 8;
+}
 // z = t*x + (1-t)*eps written in patch-major im2col layout (col = c*P*P + ky*P + kx).
 // in_kind 0: x fp16 + noise (generated or explicit fp16 `noise`), in_kind 1: x bf16 copied as is.
 // An output piece (8 kx of one (c, ky)) is one 16-B piece of an image row, so no transposition is needed -- only
@@ -128,29 +112,29 @@ __global__ __launch_bounds__(kPatchThreads) void patchify_kernel(const unsigned 
                                                                  bf16_t* __restrict__ out) {
   const int hp = H / 16, wp = W / 16;
   const Strip st = strip_of(blockIdx.x, hp, wp);
-  const int cpr = st.np * 2;  // 16-B pieces per image row of the strip (8 for a full strip)
+  const PieceMap pm = piece_map(st.np, H, W);
   const long img0 = ((long)st.b * 3 * H + st.py * 16) * W + st.px0 * 16;  // (c = 0, ky = 0, strip column 0)
-  const long row0 = ((long)st.b * hp + st.py) * wp + st.px0;
+  bf16_t* const out0 = out + (((long)st.b * hp + st.py) * wp + st.px0) * 768;
+  const unsigned short* const im = img + img0;
   uint4 v[kPatchPer], nv[kPatchPer];
-  long base[kPatchPer];
-  bool ok[kPatchPer];
 #pragma unroll
   for (int k = 0; k < kPatchPer; ++k) {
     const int i = threadIdx.x + k * kPatchThreads;
-    ok[k] = i < 48 * cpr;
-    const int rr = cpr == 8 ? i >> 3 : i / cpr, cc = i - rr * cpr, c = rr >> 4, ky = rr & 15;  // full strips: shifts
-    base[k] = img0 + ((long)c * H + ky) * W + cc * 8;
-    v[k] = ok[k] ? *reinterpret_cast<const uint4*>(img + base[k]) : make_uint4(0, 0, 0, 0);
-    nv[k] = ok[k] && in_kind == 0 && noise ? *reinterpret_cast<const uint4*>(noise + base[k]) : make_uint4(0, 0, 0, 0);
+    int c, ky, cc, off;
+    piece_of(pm, i, c, ky, cc, off);
+    const bool ok = i < 48 * pm.cpr;
+    v[k] = ok ? *reinterpret_cast<const uint4*>(im + off) : make_uint4(0, 0, 0, 0);
+    nv[k] = ok && in_kind == 0 && noise ? *reinterpret_cast<const uint4*>(noise + img0 + off) : make_uint4(0, 0, 0, 0);
   }
   const NoiseKey key = noise_key(seed);
   const float tb = in_kind == 1 ? 0.f : t[st.b];
 #pragma unroll
   for (int k = 0; k < kPatchPer; ++k) {
-    if (!ok[k]) continue;
     const int i = threadIdx.x + k * kPatchThreads;
-    const int rr = cpr == 8 ? i >> 3 : i / cpr, cc = i - rr * cpr, c = rr >> 4, ky = rr & 15, pl = cc >> 1,
-              kx0 = (cc & 1) * 8;
+    if (i >= 48 * pm.cpr) continue;
+    int c, ky, cc, off;
+    piece_of(pm, i, c, ky, cc, off);
+    const int pl = cc >> 1, kx0 = (cc & 1) * 8;
     const unsigned short* vs = reinterpret_cast<const unsigned short*>(&v[k]);
     float o[8];
     if (in_kind == 1) {
@@ -163,14 +147,14 @@ __global__ __launch_bounds__(kPatchThreads) void patchify_kernel(const unsigned 
 #pragma unroll
         for (int e = 0; e < 8; ++e) nz[e] = h2f(ns[e]);
       } else {
-        const uint32_t j0 = pair_counter((uint64_t)base[k]);  // base is even (W, x multiples of 8)
+        const uint32_t j0 = pair_counter((uint64_t)(img0 + off));  // even (W, x multiples of 8)
 #pragma unroll
         for (int e = 0; e < 4; ++e) gauss_pair_fp16(key, j0 + e, nz[2 * e], nz[2 * e + 1]);
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = tb * h2f(vs[e]) + (1.f - tb) * h2f(f2h(nz[e] * noise_scale));
     }
-    *reinterpret_cast<uint4*>(out + (row0 + pl) * 768 + c * 256 + ky * 16 + kx0) = pack8(o);
+    *reinterpret_cast<uint4*>(out0 + pl * 768 + c * 256 + ky * 16 + kx0) = pack8(o);
   }
 }
 
@@ -261,39 +245,78 @@ __global__ void scale_bf16_2d_kernel(const bf16_t* __restrict__ a, long lda, lon
 
 // Flow-matching MSE over patch-layout predictions; also writes d(loss)/d(pred) (bf16, patch layout).
 // target 0 ("image"): mse(pred, x); target 1 ("velocity"): mse((pred-z)/c, (x-z)/c), c = clamp(1-t, eps).
-// Per strip (grid-stride, fixed assignment): the thread's prediction pieces are loaded first (in flight while the
-// strip's pixels / noise are staged through LDS), then each 16-B piece (col = (ky*16 + kx)*3 + c) is mapped onto
-// the staged strip. Per-thread sums in a fixed order, one partial per block: deterministic.
-__global__ __launch_bounds__(256) void loss_kernel(const bf16_t* __restrict__ pred, const unsigned short* __restrict__ img,
-                                                   const unsigned short* __restrict__ noise, const float* __restrict__ t,
-                                                   float noise_scale, uint64_t seed, int target, float t_eps, int B,
-                                                   int H, int W, float inv_numel, bf16_t* __restrict__ dpred,
-                                                   float* __restrict__ part) {
-  __shared__ float red[256];
+// One 128-thread block per strip (grid-stride past the grid, fixed assignment), patchify's shape: a thread takes the
+// strip's prediction pieces i = tid + 128 k and its image-row pieces (k < 3 for a full strip), every load (and the
+// explicit noise's) issued before the strip is staged through LDS; then each 16-B prediction piece
+// (col = (ky*16 + kx)*3 + c) is mapped onto the staged strip. Per-thread sums in a fixed order, one partial per block:
+// deterministic. (The 256-thread form staged its image pieces only after its prediction loads and a barrier, two
+// strips per block in sequence.)
+#ifndef VPT_LOSS_BLOCKS
+#define VPT_LOSS_BLOCKS 4096  // grid cap = partials (4096: 30.5 us, 8192: 32.8, 2048: 30.8 at C3, r05zu)
+#endif
+constexpr int kLossThreads = 128, kLossPer = 96 * kStripP / kLossThreads, kLossBlocks = VPT_LOSS_BLOCKS;
+template <int TARGET>
+__global__ __launch_bounds__(kLossThreads) void loss_kernel(const bf16_t* __restrict__ pred,
+                                                            const unsigned short* __restrict__ img,
+                                                            const unsigned short* __restrict__ noise,
+                                                            const float* __restrict__ t, float noise_scale,
+                                                            uint64_t seed, float t_eps, int B, int H, int W,
+                                                            float inv_numel, bf16_t* __restrict__ dpred,
+                                                            float* __restrict__ part) {
+  __shared__ float red[kLossThreads];
   __shared__ __attribute__((aligned(16))) unsigned short px[3][16][16 * kStripP];
-  __shared__ __attribute__((aligned(16))) unsigned short eps[3][16][16 * kStripP];
+  __shared__ __attribute__((aligned(16))) unsigned short eps[TARGET ? 3 : 1][16][16 * kStripP];
   const int hp = H / 16, wp = W / 16;
   const long strips = (long)B * hp * ((wp + kStripP - 1) / kStripP);
   const NoiseKey key = noise_key(seed);
-  constexpr int kPer = (96 * kStripP + 255) / 256;  // prediction pieces per thread per strip
   float acc = 0.f;
   for (long s = blockIdx.x; s < strips; s += gridDim.x) {
     const Strip st = strip_of(s, hp, wp);
+    const PieceMap pm = piece_map(st.np, H, W);
+    const long img0 = ((long)st.b * 3 * H + st.py * 16) * W + st.px0 * 16;
     const long row0 = ((long)st.b * hp + st.py) * wp + st.px0;
-    uint4 pv[kPer];
+    const bf16_t* const pr0 = pred + row0 * 768;
+    uint4 pv[kLossPer], iv[kLossPer], nv[kLossPer];
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int i = threadIdx.x + k * 256;
-      pv[k] = i < st.np * 96 ? *reinterpret_cast<const uint4*>(pred + row0 * 768 + i * 8) : make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < kLossPer; ++k) {
+      const int i = threadIdx.x + k * kLossThreads;
+      pv[k] = i < st.np * 96 ? *reinterpret_cast<const uint4*>(pr0 + i * 8) : make_uint4(0, 0, 0, 0);
+      int c, ky, cc, off;
+      piece_of(pm, i, c, ky, cc, off);
+      const bool ok = i < 48 * pm.cpr;
+      iv[k] = ok ? *reinterpret_cast<const uint4*>(img + img0 + off) : make_uint4(0, 0, 0, 0);
+      nv[k] = TARGET && ok && noise ? *reinterpret_cast<const uint4*>(noise + img0 + off) : make_uint4(0, 0, 0, 0);
     }
     __syncthreads();  // the previous strip's LDS reads are done
-    stage_strip(st, img, noise, target == 1, key, noise_scale, H, W, px, eps);
+#pragma unroll
+    for (int k = 0; k < kLossPer; ++k) {
+      const int i = threadIdx.x + k * kLossThreads;
+      if (i >= 48 * pm.cpr) continue;
+      int c, ky, cc, off;
+      piece_of(pm, i, c, ky, cc, off);
+      *reinterpret_cast<uint4*>(&px[c][ky][cc * 8]) = iv[k];
+      if (!TARGET) continue;
+      float nz[8];
+      if (noise) {
+        const unsigned short* ns = reinterpret_cast<const unsigned short*>(&nv[k]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) nz[e] = h2f(ns[e]);
+      } else {
+        const uint32_t j0 = pair_counter((uint64_t)(img0 + off));  // even
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gauss_pair_fp16(key, j0 + e, nz[2 * e], nz[2 * e + 1]);
+      }
+      unsigned short ev[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ev[e] = f2h(nz[e] * noise_scale);
+      *reinterpret_cast<uint4*>(&eps[TARGET ? c : 0][ky][cc * 8]) = *reinterpret_cast<const uint4*>(ev);
+    }
     __syncthreads();
     const float tb = t[st.b];
     const float cl = fmaxf(1.f - tb, t_eps);
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int i = threadIdx.x + k * 256;
+    for (int k = 0; k < kLossPer; ++k) {
+      const int i = threadIdx.x + k * kLossThreads;
       if (i >= st.np * 96) continue;
       const int pl = i / 96, chunk = i - pl * 96;
       float pr[8], g[8];
@@ -304,35 +327,45 @@ __global__ __launch_bounds__(256) void loss_kernel(const bf16_t* __restrict__ pr
         const int ky = pix >> 4, kx = pl * 16 + (pix & 15);
         const float xv = h2f(px[c][ky][kx]);
         float diff;
-        if (target == 0) {
+        if (!TARGET) {
           diff = pr[e] - xv;
           g[e] = 2.f * diff * inv_numel;
         } else {
-          const float z = tb * xv + (1.f - tb) * h2f(eps[c][ky][kx]);
+          const float z = tb * xv + (1.f - tb) * h2f(eps[TARGET ? c : 0][ky][kx]);
           diff = (pr[e] - z) / cl - (xv - z) / cl;
           g[e] = 2.f * diff * inv_numel / cl;
         }
         acc += diff * diff;
       }
-      *reinterpret_cast<uint4*>(dpred + (row0 + pl) * 768 + chunk * 8) = pack8(g);
+      *reinterpret_cast<uint4*>(dpred + row0 * 768 + i * 8) = pack8(g);
     }
   }
   red[threadIdx.x] = acc;
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
+  for (int s = kLossThreads / 2; s > 0; s >>= 1) {
     if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
     __syncthreads();
   }
   if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
 
-__global__ void loss_finalize_kernel(const float* __restrict__ part, int n, float inv_numel, float* __restrict__ loss) {
-  __shared__ float red[256];
+// The block partials' sum, in a fixed order: a 1024-thread block, each thread's partials (k-strided by 1024) loaded
+// 8 at a time before any add (a load-add loop waits one L2 round trip per partial: ~0.35 us each), then a tree.
+constexpr int kFinThreads = 1024;
+__global__ __launch_bounds__(kFinThreads) void loss_finalize_kernel(const float* __restrict__ part, int n,
+                                                                    float inv_numel, float* __restrict__ loss) {
+  __shared__ float red[kFinThreads];
   float s = 0.f;
-  for (int i = threadIdx.x; i < n; i += 256) s += part[i];
+  for (int i0 = threadIdx.x; i0 < n; i0 += 8 * kFinThreads) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = i0 + k * kFinThreads < n ? part[i0 + k * kFinThreads] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += v[k];
+  }
   red[threadIdx.x] = s;
   __syncthreads();
-  for (int k = 128; k > 0; k >>= 1) {
+  for (int k = kFinThreads / 2; k > 0; k >>= 1) {
     if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
     __syncthreads();
   }
@@ -893,20 +926,24 @@ extern "C" int vpt_scale_bf16_2d(const void* a, long lda, long rows, int cols, f
   return VPT_OK;
 }
 
-extern "C" int vpt_loss_blocks(void) { return 4096; }
+extern "C" int vpt_loss_blocks(void) { return kLossBlocks; }
 
 extern "C" int vpt_flow_loss(const void* pred, const void* img, const void* noise, const float* t, float noise_scale,
                              unsigned long long seed, int target, float t_eps, int B, int H, int W, void* dpred,
                              float* part, float* loss, void* stream) {
   VPT_CHECK_ARG(pred && img && t && dpred && part && loss, "vpt_flow_loss: null pointer");
   VPT_CHECK_ARG(target == 0 || target == 1, "vpt_flow_loss: target must be 0 (image) or 1 (velocity)");
+  VPT_CHECK_ARG(B > 0 && H % 16 == 0 && W % 16 == 0, "vpt_flow_loss: H and W must be multiples of the 16-px patch");
   const float numel = (float)B * 3.f * H * W;
+  const long strips = (long)B * (H / 16) * ((W / 16 + kStripP - 1) / kStripP);
+  const int blocks = (int)(strips < kLossBlocks ? strips : kLossBlocks);  // partials part[0, blocks)
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(loss_kernel, dim3(vpt_loss_blocks()), dim3(256), 0, s, (const bf16_t*)pred,
-                     (const unsigned short*)img, (const unsigned short*)noise, t, noise_scale, (uint64_t)seed, target,
-                     t_eps, B, H, W, 1.f / numel, (bf16_t*)dpred, part);
+  auto kern = target == 0 ? loss_kernel<0> : loss_kernel<1>;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(kLossThreads), 0, s, (const bf16_t*)pred, (const unsigned short*)img,
+                     (const unsigned short*)noise, t, noise_scale, (uint64_t)seed, t_eps, B, H, W, 1.f / numel,
+                     (bf16_t*)dpred, part);
   VPT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, part, vpt_loss_blocks(), 1.f / numel, loss);
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(kFinThreads), 0, s, part, blocks, 1.f / numel, loss);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
