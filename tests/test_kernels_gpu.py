@@ -655,8 +655,9 @@ def test_bias_grad(ops, M, N):
     assert rel(out, 2 * ref) < 1e-5
 
 
-def test_patchify_unpatchify_roundtrip(ops):
-    B, H, W = 2, 64, 96
+@pytest.mark.parametrize("W", [96, 112, 80])  # strips of 4 + 2, 4 + 3 and 4 + 1 patches (every piece-decode width)
+def test_patchify_unpatchify_roundtrip(ops, W):
+    B, H = 2, 64
     img = rnd(B, 3, H, W, seed=53)
     p = torch.empty(B * (H // 16) * (W // 16), 768, dtype=torch.bfloat16, device=DEV)
     ops.patchify(img, B, H, W, p, noising=False)
@@ -734,12 +735,12 @@ def test_generated_noise_depends_on_seed_only(ops):
 
 
 @pytest.mark.parametrize("target", [0, 1])
-def test_flow_loss(ops, target):
-    B, H, W = 2, 64, 32
+@pytest.mark.parametrize("B,H,W", [(2, 64, 32), (2, 48, 112), (9, 512, 1024)])  # ragged strips; > 4096 strips
+def test_flow_loss(ops, target, B, H, W):
     np_ = (H // 16) * (W // 16)
     x = rnd(B, 3, H, W, dtype=torch.float16, seed=56)
     nz = rnd(B, 3, H, W, dtype=torch.float16, seed=57)
-    t = torch.tensor([0.2, 0.99], device=DEV)
+    t = torch.linspace(0.2, 0.99, B, device=DEV)
     pred_img = rnd(B, 3, H, W, seed=58)
     pred = torch.empty(B * np_, 768, dtype=torch.bfloat16, device=DEV)
     ops.unpatchify(pred, B, H, W, pred_img, reverse=True)

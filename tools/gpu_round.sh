@@ -12,7 +12,7 @@ timeout -k 10 900 python -u -m pytest $SEL -x -v --timeout 300 --timeout-method 
 tail -3 $O/gpu_tests.log
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "SMOKE FAILED"; tail -30 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
-timeout -k 10 400 python -u bench.py > $O/bench_c3.json 2> $O/bench_c3.err || { echo "C3 FAILED"; tail -30 $O/bench_c3.err; exit 1; }
+timeout -k 10 400 python -u bench.py --breakdown $O/gemm_breakdown.json > $O/bench_c3.json 2> $O/bench_c3.err || { echo "C3 FAILED"; tail -30 $O/bench_c3.err; exit 1; }
 timeout -k 10 300 python -u bench.py --grad-ckpt --no-cpu-baseline > $O/bench_c3_ckpt.json 2> $O/bench_c3_ckpt.err || { echo "C3 CKPT FAILED"; tail -30 $O/bench_c3_ckpt.err; exit 1; }
 timeout -k 10 300 python -u bench.py --workload c2 > $O/bench_c2.json 2> $O/bench_c2.err || { echo "C2 FAILED"; tail -30 $O/bench_c2.err; exit 1; }
 timeout -k 10 400 python -u bench.py --workload c5 > $O/bench_c5.json 2> $O/bench_c5.err || { echo "C5 FAILED"; tail -30 $O/bench_c5.err; exit 1; }
