@@ -56,11 +56,13 @@ WGRAD_SPLIT_MUL = 1
 # forward and input-gradient chain: every op there is row- or sequence-local, so the sub-batches need no exchange (the
 # forward is bitwise the one-batch forward; the backward's weight gradients still cover the whole batch); one
 # sub-batch's kernels fill the CUs the other's leave idle in their last, partial round of work items (the GEMMs' wave
-# quantisation, the attention grids' tails). 2: C3 step +1.8 % (r05za), +2.5 % with checkpointing (r05zi); at C2
-# (512^2, B=16: 8.8k rows per lane) -3.6 % (r05zo) -- the lanes' halved grids then underfill the chip -- so lanes are
-# used only when each keeps at least MICRO_SPLIT_MIN_ROWS token rows. 1 = one stream. Needs B % MICRO_SPLIT == 0.
+# quantisation, the attention grids' tails). 2: C3 step +1.8 % (r05za), +2.5 % with checkpointing (r05zi). Lanes are
+# used only when each keeps at least MICRO_SPLIT_MIN_ROWS token rows: at C2 (512^2, B=16: 8.7k rows per lane) lanes in
+# forward AND backward were -3.6 % (r05zo, threshold 12288 then), forward-only lanes are +2.3 % (r05zzc), so the
+# threshold now admits C2 and keeps small batches (C1: 0.6k rows per lane) on one stream. 1 = one stream. Needs
+# B % MICRO_SPLIT == 0.
 MICRO_SPLIT = 2
-MICRO_SPLIT_MIN_ROWS = 12288
+MICRO_SPLIT_MIN_ROWS = 8192
 # Where the lanes run (r05zr, same-box A/Bs at C3 with the other half on): in the forward +2.5 %; in the backward's
 # input-gradient chain -1.2 % (there the side-stream weight gradients already fill the chain's partial rounds, and the
 # lanes' extra hand-offs cost more than they fill), so the backward runs one lane by default.
