@@ -68,6 +68,9 @@ MICRO_SPLIT_MIN_ROWS = 8192
 # lanes' extra hand-offs cost more than they fill), so the backward runs one lane by default.
 MICRO_SPLIT_FWD = True
 MICRO_SPLIT_BWD = False
+# Gradient checkpointing's per-block recompute in the backward as forward lanes too (while the backward itself runs one
+# lane); A/B knob
+MICRO_SPLIT_RECOMPUTE = True
 
 
 def _lanes(B: int, rows: int, device) -> int:
@@ -503,10 +506,26 @@ class JiTEngine:
                 settle_qkv()  # the recompute below overwrites the ck.* activations the previous block's wgrads read
                 # recompute the block's intermediates from its saved input (x{i+1} is left untouched)
                 xo = pool.get("ck.xout", (M, D))
-                for hh in range(S):
-                    with on(hh):
-                        self._block_forward(i, rs(x_in, hh), rs(xo, hh), tag, spools[hh], Bh, rows, n_ctx, n_pre,
-                                            bs(kbias, hh), cos_t, sin_t)
+                Sr = _lanes(B, rows, self.device) if (S == 1 and MICRO_SPLIT_FWD and MICRO_SPLIT_RECOMPUTE) else 1
+                if Sr > 1:  # the recompute as forward lanes (bitwise the one-lane recompute), joined on main
+                    while len(self._mstreams) < Sr:
+                        self._mstreams.append(torch.cuda.Stream(device=self.device))
+                    subs, cur = self._mstreams[:Sr], torch.cuda.current_stream(self.device)
+                    for st_r in subs:
+                        st_r.wait_stream(cur)
+                    Bhr, Mhr = B // Sr, M // Sr
+                    for hh in range(Sr):
+                        with torch.cuda.stream(subs[hh]):
+                            self._block_forward(i, x_in[hh * Mhr:(hh + 1) * Mhr], xo[hh * Mhr:(hh + 1) * Mhr], tag,
+                                                _SubPool(pool, hh, Sr), Bhr, rows, n_ctx, n_pre,
+                                                None if kbias is None else kbias[hh * Bhr:(hh + 1) * Bhr], cos_t, sin_t)
+                    for st_r in subs:
+                        cur.wait_stream(st_r)
+                else:
+                    for hh in range(S):
+                        with on(hh):
+                            self._block_forward(i, rs(x_in, hh), rs(xo, hh), tag, spools[hh], Bh, rows, n_ctx, n_pre,
+                                                bs(kbias, hh), cos_t, sin_t)
             xn1, qkv, qk, o = (pool.get(tag + n, s) for n, s in (("xn1", (M, D)), ("qkv", (M, 3 * D)),
                                                                  ("qk", (M, 2 * D)), ("o", (M, D))))
             xm, xn2, x12, h = (pool.get(tag + n, s) for n, s in (("xm", (M, D)), ("xn2", (M, D)),
