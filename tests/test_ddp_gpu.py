@@ -58,7 +58,7 @@ def _step(tr, b, sl, dev, on_ready=None):
                    noise=b["noise"][sl].to(dev), drop_context=False, on_ready=on_ready)
 
 
-def _worker(rank, world, port, q, split=None):
+def _worker(rank, world, port, q, split=None, bwd=True, ck=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -68,8 +68,9 @@ def _worker(rank, world, port, q, split=None):
         import vpt.engine as E
         E.MICRO_SPLIT = split
         E.MICRO_SPLIT_MIN_ROWS = 0  # lanes at the micro size too
-        E.MICRO_SPLIT_BWD = True    # and in the backward (the on_ready hand-offs across lanes)
+        E.MICRO_SPLIT_BWD = bwd     # and in the backward (the on_ready hand-offs across lanes)
     tr, cfg = _trainer(dev)
+    tr.engine.set_gradient_checkpointing(ck)
     b = _batch(dev)
     sync = GradSync(tr.engine.grads, grad_buckets(tr.engine.layout, cfg.depth), wire="bf16")
     launched = []
@@ -85,9 +86,10 @@ def _worker(rank, world, port, q, split=None):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("split", [1, 2])
-def test_two_ranks_real_engine_gradient_mean(split):
-    """split: the engine's sub-batch lanes (vpt.engine.MICRO_SPLIT) in the ranks and in the single-rank reference."""
+@pytest.mark.parametrize("split,bwd,ck", [(1, True, False), (2, True, False), (2, False, True)])
+def test_two_ranks_real_engine_gradient_mean(split, bwd, ck):
+    """split: the engine's sub-batch lanes (vpt.engine.MICRO_SPLIT) in the ranks and in the single-rank reference;
+    bwd: lanes in the backward too; ck: gradient checkpointing (with forward-only lanes: the recompute as lanes)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import vpt.engine as E
@@ -95,7 +97,7 @@ def test_two_ranks_real_engine_gradient_mean(split):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, split)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, split, bwd, ck)) for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=240) for _ in range(world)]
@@ -107,9 +109,10 @@ def test_two_ranks_real_engine_gradient_mean(split):
     assert torch.equal(g0, g1)
     dev = torch.device("cuda", 0)
     old, old_min, old_bwd = E.MICRO_SPLIT, E.MICRO_SPLIT_MIN_ROWS, E.MICRO_SPLIT_BWD
-    E.MICRO_SPLIT, E.MICRO_SPLIT_MIN_ROWS, E.MICRO_SPLIT_BWD = split, 0, True
+    E.MICRO_SPLIT, E.MICRO_SPLIT_MIN_ROWS, E.MICRO_SPLIT_BWD = split, 0, bwd
     try:
         tr, cfg = _trainer(dev)
+        tr.engine.set_gradient_checkpointing(ck)
         _step(tr, _batch(dev), slice(0, 4), dev)
     finally:
         E.MICRO_SPLIT, E.MICRO_SPLIT_MIN_ROWS, E.MICRO_SPLIT_BWD = old, old_min, old_bwd
