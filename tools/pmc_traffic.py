@@ -18,19 +18,20 @@ import json
 import sys
 
 # op -> (kernel-name substrings that belong to it, the substring counted as one launch of the op)
+# A kernel counts toward every op whose members it matches (the R2 ring, gemm_r2.hip, is both a GEMM-family launch and,
+# in production, only the fused SwiGLU-backward dgrad: its own entry).
 OPS = {
-    "gemm": (("gemm_ring_kernel", "gemm_bf16_kernel", "splitk_reduce_kernel"), ("gemm_ring_kernel", "gemm_bf16_kernel")),
+    "gemm": (("gemm_ring_kernel", "gemm_bf16_kernel", "gemm_r2_kernel", "splitk_reduce_kernel"),
+             ("gemm_ring_kernel", "gemm_bf16_kernel", "gemm_r2_kernel")),
+    "swb_dgrad_r2": (("gemm_r2_kernel",), ("gemm_r2_kernel",)),
     "attn_fwd": (("attn_fwd_kernel",), ("attn_fwd_kernel",)),
     "attn_bwd": (("attn_bwd_pre_kernel", "attn_bwd_kernel", "attn_bwd_dkdv_kernel", "attn_bwd_dq_kernel"),
                  ("attn_bwd_kernel", "attn_bwd_dkdv_kernel")),
 }
 
 
-def _op_of(name):
-    for op, (members, _) in OPS.items():
-        if any(m in name for m in members):
-            return op
-    return None
+def _ops_of(name):
+    return [op for op, (members, _) in OPS.items() if any(m in name for m in members)]
 
 
 def _counter(dirname, counter):
@@ -40,12 +41,10 @@ def _counter(dirname, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        op = _op_of(r["Kernel_Name"])
-        if op is None:
-            continue
-        tot[op] += float(r["Counter_Value"])
-        if any(m in r["Kernel_Name"] for m in OPS[op][1]):
-            launches[op] += 1
+        for op in _ops_of(r["Kernel_Name"]):
+            tot[op] += float(r["Counter_Value"])
+            if any(m in r["Kernel_Name"] for m in OPS[op][1]):
+                launches[op] += 1
     return tot, launches
 
 
@@ -57,12 +56,10 @@ def _counters(dirname, names):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] not in names:
             continue
-        op = _op_of(r["Kernel_Name"])
-        if op is None:
-            continue
-        tot[op][r["Counter_Name"]] += float(r["Counter_Value"])
-        if any(m in r["Kernel_Name"] for m in OPS[op][1]):
-            seen[op].add(r.get("Dispatch_Id", r.get("Correlation_Id", len(seen[op]))))
+        for op in _ops_of(r["Kernel_Name"]):
+            tot[op][r["Counter_Name"]] += float(r["Counter_Value"])
+            if any(m in r["Kernel_Name"] for m in OPS[op][1]):
+                seen[op].add(r.get("Dispatch_Id", r.get("Correlation_Id", len(seen[op]))))
     return tot, {op: len(v) for op, v in seen.items()}
 
 
@@ -84,12 +81,10 @@ def main():
     dur = collections.defaultdict(float)
     calls = collections.Counter()
     for r in csv.DictReader(open(stats)):
-        op = _op_of(r["Name"])
-        if op is None:
-            continue
-        dur[op] += float(r["TotalDurationNs"])
-        if any(m in r["Name"] for m in OPS[op][1]):
-            calls[op] += int(r["Calls"])
+        for op in _ops_of(r["Name"]):
+            dur[op] += float(r["TotalDurationNs"])
+            if any(m in r["Name"] for m in OPS[op][1]):
+                calls[op] += int(r["Calls"])
     res = {}
     for op in OPS:
         if not nf[op] or not nw[op]:
