@@ -30,11 +30,16 @@ sys.path.insert(0, ROOT)
 
 # HIP hardware queues per process (read at HIP's initialisation, so set before torch loads): at N > 1 the step runs six
 # streams -- the step's own, two sub-batch lanes, the weight-gradient stream, the optimizer's bucket stream and RCCL's
-# -- and with HIP's 4 queues some would share one and run behind each other. --hw-queues N (default 8, <= 32).
-_hwq = int(sys.argv[sys.argv.index("--hw-queues") + 1]) if "--hw-queues" in sys.argv else 8
-if not 1 <= _hwq <= 32:
-    raise SystemExit("--hw-queues: 1..32")
-os.environ["GPU_MAX_HW_QUEUES"] = str(_hwq)
+# -- and with HIP's 4 queues some would share one and run behind each other. --hw-queues N sets it (<= 32); without the
+# flag an exported GPU_MAX_HW_QUEUES is kept, else 8. The bench line records the REQUESTED value (`hw_queues_requested`):
+# under a profiler that initialises the HIP runtime first, the runtime may have read the variable before this line.
+if "--hw-queues" in sys.argv:
+    _hwq = int(sys.argv[sys.argv.index("--hw-queues") + 1])
+    if not 1 <= _hwq <= 32:
+        raise SystemExit("--hw-queues: 1..32")
+    os.environ["GPU_MAX_HW_QUEUES"] = str(_hwq)
+else:
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -189,7 +194,13 @@ def main():
                     help="optimizer per gradient bucket on a side stream as each all-reduce lands (auto: off -- "
                          "beside the engine's concurrent streams it costs 6 %% at N = 1, 163.5 vs 174.1 img/s, r05ze; "
                          "the all-reduces themselves still run under the backward at any setting)")
-    ap.add_argument("--hw-queues", type=int, default=8, help="GPU_MAX_HW_QUEUES for this process (applied at import)")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="GPU_MAX_HW_QUEUES for this process (applied at import; default: the exported value, else 8)")
+    ap.add_argument("--force-collective", action="store_true",
+                    help="world 1 only: initialise a one-rank nccl (RCCL) group and run every gradient bucket's "
+                         "all-reduce (bf16 wire cast included) and the loss all-reduce inside the timed step, as at "
+                         "N > 1 -- to measure the N > 1 schedule (overlap, HW queues) with the collectives really "
+                         "running on one GPU")
     ap.add_argument("--streams", default="multi", choices=["multi", "single"],
                     help="multi: the engine's concurrent streams (the backward's weight-gradient GEMMs beside the "
                          "input-gradient chain, vpt.engine.CONCURRENT_WGRAD: +2.2 %% per C3 step, r05v; the blocks as "
@@ -216,7 +227,15 @@ def main():
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    if world > 1:
+    force = bool(args.force_collective)
+    if force and world > 1:
+        raise SystemExit("--force-collective is the world-1 stand-in for N > 1")
+    if world > 1 or force:
+        if force:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
 
     from vpt import engine as vpt_engine
@@ -230,7 +249,7 @@ def main():
         vpt_engine.CONCURRENT_WGRAD = False
         vpt_engine.MICRO_SPLIT = 1
     timed_streams = dict(wgrad_stream="side" if vpt_engine.CONCURRENT_WGRAD else "step",
-                         sub_batches=vpt_engine.MICRO_SPLIT, hw_queues=int(os.environ["GPU_MAX_HW_QUEUES"]))
+                         sub_batches=vpt_engine.MICRO_SPLIT, hw_queues_requested=int(os.environ["GPU_MAX_HW_QUEUES"]))
     cfg = JiT_B_16_Config()
     trainer = JiTTrainer(cfg, N_CLASSES, JiTTrainingConfig(loss_target="image"), device=device, seed=1234 + rank)
     trainer.engine.init_weights(seed=0)  # identical on every rank (replaces DDP's broadcast)
@@ -241,8 +260,8 @@ def main():
     # moment the backward completes them and stepped by the optimizer on a side stream as each reduction lands
     overlap = args.overlap == "on"
     sync = GradSync(trainer.engine.grads, grad_buckets(trainer.engine.layout, cfg.depth), wire="bf16",
-                    overlap=overlap)
-    losslog = LossLog(device)
+                    overlap=overlap, force_collective=force)
+    losslog = LossLog(device, force_collective=force)
     batches = make_batches(args.batch, device, seed=100 + rank, buckets=buckets)
     n_probe = len(buckets)
     order = shared_order(len(buckets), args.warmup + args.steps + n_probe, world, rank)
@@ -336,7 +355,8 @@ def main():
                    "parallelism": f"dp{world}", "loss_target": "image", "optimizer": "RAdamScheduleFree (fused HIP)",
                    "optimizer_overlap": "per bucket on a side stream during backward" if overlap else
                    "one launch after the backward",
-                   "grad_allreduce": "bf16 wire, per-block buckets overlapped with backward" if world > 1 else None,
+                   "grad_allreduce": ("bf16 wire, per-block buckets overlapped with backward" if world > 1 else
+                                      "forced at world 1 (RCCL all-reduces in the step)" if force else None),
                    "grad_checkpointing": bool(args.grad_ckpt),
                    "streams": timed_streams},
         "roofline": roofline_entry(dom, stats[dom], args.workload),
@@ -353,7 +373,7 @@ def main():
         result["cpu_baseline"] = cpu_baseline(args.workload)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if world > 1 or force:
         dist.barrier()
         dist.destroy_process_group()
 

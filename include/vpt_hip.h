@@ -210,7 +210,8 @@ int vpt_reduce_rows(const float* in, int R, int C, float* out, int accumulate, v
  * patchify: z = t*x + (1-t)*eps (eps from `noise` fp16 or the counter RNG `seed`), written in the
  * Conv2d(k=16,s=16) im2col order; in_kind 1 copies a bf16 image. Replaces
  * prepare_scaled_noised_latents src/modules/loss/flow_match.py:60-74 + the proj_1 im2col.
- * flow_loss: mse(pred, x) (target 0) or mse(v(pred), v(x)) (target 1) with v = (. - z)/max(1-t, eps),
+ * flow_loss: mse(pred, x) (target 0) or mse(v(pred), v(x)) (target 1) with v = (. - z)/max(1-t, eps), or for a
+ * velocity prediction mse(pred, fp16(x - eps)) (target 2; class_to_image.py:146-156, no timestep clamp),
  * writes d loss/d pred. Replaces treat_loss train/jit/arb_class_to_image.py:108-151,
  * JiTModel.image_to_velocity src/models/jit/pipeline.py:253-260, JiT._unpatchify denoiser.py:828-860. */
 int vpt_patchify(const void* img, int in_kind, const void* noise, const float* t, float noise_scale,
@@ -224,6 +225,15 @@ int vpt_unpatchify(const void* patches, int B, int H, int W, void* img, int reve
 int vpt_euler_cfg_step(void* z, const void* pred, int B, int H, int W, int cfg, float cfg_scale, int mode, float t,
                        float dt, void* stream);
 int vpt_loss_blocks(void);
+/* lowres_loss inputs (train/jit/arb_class_to_image.py:228-264): F.interpolate(mode="area", scale_factor=1/k), k even,
+ * of the fp16 image -> img_lr fp16, of the fp16 noise (`noise`, or NULL = the counter RNG `seed` as patchify) ->
+ * noise_lr fp16, and of the noisy image t x + (1-t) eps -> z_lr bf16 (the lowres model input); all [B][3][H/k][W/k]. */
+/* The in-kernel noise as an fp16 tensor: element i of a flat [B][3][H][W] image (n = B*3*H*W, even) is exactly the
+ * draw patchify / flow_loss / area_lowres generate at that index for `seed` -- torch.randn_like(latents) * noise_scale
+ * of prepare_scaled_noised_latents (src/modules/loss/flow_match.py:60-74). */
+int vpt_gauss_noise(long n, unsigned long long seed, float noise_scale, void* out, void* stream);
+int vpt_area_lowres(const void* img, const void* noise, const float* t, float noise_scale, unsigned long long seed,
+                    int B, int H, int W, int k, void* img_lr, void* noise_lr, void* z_lr, void* stream);
 int vpt_flow_loss(const void* pred, const void* img, const void* noise, const float* t, float noise_scale,
                   unsigned long long seed, int target, float t_eps, int B, int H, int W, void* dpred, float* part,
                   float* loss, void* stream);
@@ -250,11 +260,13 @@ int vpt_copy_rows(void* seq, long ld_seq, int rows, int row0, int cnt, void* den
 int vpt_embed_gather(const void* table, const long long* ids, long R, int D, void* out, void* stream);
 int vpt_embed_scatter_add(const void* drows, const long long* ids, long R, int D, long long pad_id, float* dtable,
                           void* stream);
-/* The same gradient with overwrite semantics (the whole [V][D] table written: zeros where no id points, the padding
- * row zero), each row summed in position order -- deterministic; R <= 8192. Replaces the zero_() of the class-embedding
- * gradient + the scatter of arb_class_to_image.py's nn.Embedding backward (class_encoder.py:16-90). */
-int vpt_embed_grad_set(const void* drows, const long long* ids, long R, int D, long long pad_id, long V, float* dtable,
-                       void* stream);
+/* The same gradient written in one deterministic pass, each row summed in position order (O(R) position lists per
+ * 8-row block; R <= 16384): accumulate = 0 overwrites the whole [V][D] table (zeros where no id points, the padding
+ * row zero), accumulate = 1 adds the sum to the rows the ids name (torch's .grad += under gradient accumulation).
+ * Replaces the zero_() of the class-embedding gradient + the scatter of arb_class_to_image.py's nn.Embedding backward
+ * (class_encoder.py:16-90, :127-144). */
+int vpt_embed_grad_set(const void* drows, const long long* ids, long R, int D, long long pad_id, long V, int accumulate,
+                       float* dtable, void* stream);
 /* The JiT step's per-batch inputs in one launch: t_vals = bf16(bf16(t) * tscale) as f32 (arb_class_to_image.py:207),
  * size_vals [B][6] f32 = original_size | target_size | crop_coords (int64 [B][2] each; denoiser.py's size embedder
  * input), and key-bias rows kbias[b][0, n_pre + n_ctx) (row stride rows): 0, then 0 / -inf by mask [B][n_ctx] int64

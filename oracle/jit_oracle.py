@@ -323,8 +323,14 @@ def image_to_velocity(img, z, t, eps: float):
     return (img - z) / (1 - t.view(-1, 1, 1, 1)).clamp_min(eps)
 
 
-def treat_loss(pred, z, x, t, loss_target: str = "image", t_eps: float = 0.05):
-    """JiTForClassToImageTraining.treat_loss (train/jit/arb_class_to_image.py:108-151), model_pred=image."""
+def treat_loss(pred, z, x, t, loss_target: str = "image", t_eps: float = 0.05, model_pred: str = "image",
+               noise=None):
+    """JiTForClassToImageTraining.treat_loss: model_pred "image" (train/jit/arb_class_to_image.py:108-147) and
+    model_pred "velocity" (train/jit/class_to_image.py:146-156: target clean - noise, no timestep clamp)."""
+    if model_pred == "velocity":
+        if loss_target != "velocity":
+            raise NotImplementedError("Velocity prediction with image loss is not implemented yet.")
+        return F.mse_loss(pred.float(), x.float() - noise.float())
     if loss_target == "image":
         return F.mse_loss(pred.float(), x.float())
     if loss_target == "velocity":
@@ -350,19 +356,34 @@ def class_tokenize(captions: list[str], label2id: dict[str, int], max_len: int, 
 
 
 def train_step_loss(model: OracleJiT, emb: torch.Tensor, batch: dict, loss_target: str = "image",
-                    t_eps: float = 0.05, drop_context: bool = False):
-    """Forward half of train_step (train/jit/arb_class_to_image.py:153-224) with the random draws
-    (t, noise) taken from `batch` and context ids already tokenised. Returns (loss, pred)."""
+                    t_eps: float = 0.05, drop_context: bool = False, model_pred: str = "image", lowres_loss=()):
+    """Forward half of train_step (train/jit/arb_class_to_image.py:153-276) with the random draws
+    (t, noise) taken from `batch` and context ids already tokenised. lowres_loss: one more denoiser pass per
+    scale on F.interpolate(mode="area") resized image / noisy image / noise, its loss added (arb:228-272).
+    Returns (total loss, full-resolution pred)."""
     x = batch["image"].float()
     t = batch["t"]
-    z = noised(x, t, batch["noise"].float())
+    noise = batch["noise"].float()
+    z = noised(x, t, noise)
     ids, mask = batch["ids"], batch["mask"]
     if drop_context:  # captions -> "" (all pad ids), mask -> ones (arb_class_to_image.py:162-189)
         ids = torch.full_like(ids, emb.shape[0] - 1)
         mask = torch.ones_like(mask)
     ctx = F.embedding(ids, emb, padding_idx=emb.shape[0] - 1)
     pred = model(z, t, ctx, batch["original_size"], batch["target_size"], batch["crop_coords"], mask)
-    return treat_loss(pred, z, x, t, loss_target, t_eps), pred
+    loss = treat_loss(pred, z, x, t, loss_target, t_eps, model_pred, noise)
+    for s in lowres_loss:
+        if s <= 0.0:  # arb:230-231
+            continue
+
+        def resize(v):  # arb:233-238
+            return F.interpolate(v, scale_factor=s, mode="area")
+        rx, rz = resize(x), resize(z)
+        B, _, lh, lw = rx.shape
+        size_lr = torch.tensor([[lh, lw]]).repeat(B, 1)
+        pred_lr = model(rz, t, ctx, batch["original_size"] * s, size_lr, batch["crop_coords"] * s, mask)
+        loss = loss + treat_loss(pred_lr, rz, rx, t, loss_target, t_eps, model_pred, resize(noise))
+    return loss, pred
 
 
 # ------------------------------------------------------------------------------- buckets

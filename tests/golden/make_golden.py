@@ -520,6 +520,91 @@ def micro_fixture(R, meta, oc: OracleConfig, name: str):
               metadata=dict(meta, do_context_fuse=str(oc.do_context_fuse)))
 
 
+def objectives_fixture(R, meta):
+    """jit_objectives: the reference's OWN train_step functions, run with a stand-in `self` (the trainer's
+    accelerator / logging plumbing replaced; t and the noise draw taken from the batch):
+      vpred    -- train/jit/class_to_image.py:166-243 with model_pred="velocity" (treat_loss :146-156: target
+                  clean - noise, no clamp), the micro batch of jit_micro;
+      lowres_x -- train/jit/arb_class_to_image.py:153-276 with loss_target "image" and lowres_loss [0.5, 0.25]
+                  (two extra passes on F.interpolate(mode="area") inputs, arb:228-272), a 2 x 128 x 64 batch;
+      lowres_v -- the same with loss_target "velocity" and lowres_loss [0.5]."""
+    import functools
+    cti = importlib.import_module("class_to_image")
+    oc = micro_config()
+    V = 20
+    w = make_weights(oc, seed=1, n_classes=V)
+    out = {}
+    cases = {"vpred": (cti, "velocity", "velocity", [], make_batch(oc, 2, 64, 48, 8, V, seed=2)),
+             "lowres_x": (R.arb, "image", "image", [0.5, 0.25], make_batch(oc, 2, 128, 64, 8, V, seed=5)),
+             "lowres_v": (R.arb, "image", "velocity", [0.5], make_batch(oc, 2, 128, 64, 8, V, seed=5))}
+    def run(mod, model_pred, loss_target, lowres, batch, bf16):
+        """The reference's train_step on `batch`: fp32, or as its trainer runs it (bf16 weights, forward and
+        backward under bf16 autocast, fp16 images; run_reference_bf16's convention)."""
+        dt = torch.bfloat16 if bf16 else torch.float32
+        den = R.den.Denoiser(ref_config(R, oc))
+        den.load_state_dict({k: v for k, v in w.items() if not k.startswith("class_encoder.")}, strict=True)
+        den = den.to(dt)
+        den.train()
+        emb = w["class_encoder.embedding.weight"].clone().to(dt).requires_grad_(True)
+        preds = []
+
+        def denoiser(**kw):
+            o = den(**kw)
+            preds.append(o.detach().float().clone())
+            return o
+
+        class ClassEnc:
+            @staticmethod
+            def encode_prompts(caption, max_token_length):
+                return F.embedding(batch["ids"], emb, padding_idx=emb.shape[0] - 1), batch["mask"]
+
+        mcfg = types.SimpleNamespace(torch_dtype=dt, drop_context_rate=0.0, train_class_encoder=True,
+                                     max_token_length=batch["ids"].shape[1], timestep_sampling="scale_shift_sigmoid",
+                                     noise_scale=1.0, timestep_eps=0.05, model_pred=model_pred,
+                                     loss_target=loss_target, lowres_loss=lowres)
+        model = types.SimpleNamespace(text_encoder=None, class_encoder=ClassEnc(), denoiser=denoiser,
+                                      image_to_velocity=functools.partial(mod.JiTModel.image_to_velocity, None))
+        me = types.SimpleNamespace(model_config=mcfg, model=model, accelerator=types.SimpleNamespace(device="cpu"),
+                                   log=lambda *a, **k: None)
+        me.treat_loss = functools.partial(mod.JiTForClassToImageTraining.treat_loss, me)
+        # the fp32 reference run (as every fixture here): the fp16 image / noise values as f32 tensors (with fp16 tensors
+        # the velocity target's mixed-dtype mse_loss has no CPU backward outside autocast); the bf16 run: fp16 images
+        rb = {"image": batch["image"] if bf16 else batch["image"].float(), "caption": [""] * batch["image"].shape[0],
+              "original_size": batch["original_size"], "target_size": batch["target_size"],
+              "crop_coords_top_left": batch["crop_coords"]}
+        old_st, old_rl = mod.sample_timestep, torch.randn_like
+        mod.sample_timestep = lambda **kw: batch["t"]
+        torch.randn_like = lambda ten, *a, **k: batch["noise"].to(ten.dtype)
+        try:
+            with torch.autocast("cpu", dtype=torch.bfloat16, enabled=bf16):
+                loss = mod.JiTForClassToImageTraining.train_step(me, rb)
+        finally:
+            mod.sample_timestep, torch.randn_like = old_st, old_rl
+        loss.backward()
+        assert len(preds) == 1 + len(lowres)
+        grads = {n: p.grad.detach().float().clone() for n, p in den.named_parameters()}
+        grads["class_encoder.embedding.weight"] = emb.grad.detach().float().clone()
+        return loss.detach().float(), preds[0], grads
+
+    names = {}
+    for case, (mod, model_pred, loss_target, lowres, batch) in cases.items():
+        loss, pred, grads = run(mod, model_pred, loss_target, lowres, batch, False)
+        _, _, g16 = run(mod, model_pred, loss_target, lowres, batch, True)
+        for k in ("image", "noise", "t", "ids", "mask", "original_size", "target_size", "crop_coords"):
+            out[f"{case}/in/{k}"] = batch[k]
+        out[f"{case}/loss"] = loss.reshape(1)
+        out[f"{case}/pred"] = pred
+        grad_summary(f"{case}/", grads, out)
+        # the reference's own bf16-vs-fp32 gradient error on this case (the parity bars' yardstick, as ref_bf16_error)
+        names[case] = sorted(grads)
+        out[f"{case}/bf16_grad_rel"] = torch.tensor(
+            [((g16[n] - grads[n]).norm() / grads[n].norm().clamp_min(1e-30)).item() for n in names[case]],
+            dtype=torch.float64)
+        print(case, loss.item(), "worst bf16 rel", out[f"{case}/bf16_grad_rel"].max().item(), flush=True)
+    save_file({k: v.contiguous() for k, v in out.items()}, os.path.join(HERE, "jit_objectives.safetensors"),
+              metadata=dict(meta, lowres=json.dumps({c: v[3] for c, v in cases.items()}), names=json.dumps(names)))
+
+
 def main():
     R = import_reference()
     meta = {"torch": torch.__version__, "threads": str(torch.get_num_threads()), "reference": REF}
@@ -545,6 +630,10 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "timestep":
         timestep_fixture(meta)
         print("timestep", os.path.getsize(os.path.join(HERE, "timestep.safetensors")))
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "objectives":
+        objectives_fixture(R, meta)
+        print("jit_objectives", os.path.getsize(os.path.join(HERE, "jit_objectives.safetensors")))
         return
     if len(sys.argv) > 1 and sys.argv[1] == "fuse":
         micro_fixture(R, meta, micro_fuse_config(), "jit_micro_fuse")

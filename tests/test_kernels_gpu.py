@@ -734,7 +734,7 @@ def test_generated_noise_depends_on_seed_only(ops):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
-@pytest.mark.parametrize("target", [0, 1])
+@pytest.mark.parametrize("target", [0, 1, 2])
 @pytest.mark.parametrize("B,H,W", [(2, 64, 32), (2, 48, 112), (9, 512, 1024)])  # ragged strips; > 4096 strips
 def test_flow_loss(ops, target, B, H, W):
     np_ = (H // 16) * (W // 16)
@@ -751,6 +751,8 @@ def test_flow_loss(ops, target, B, H, W):
     pf = pred_img.float().requires_grad_(True)
     if target == 0:
         ref = torch.nn.functional.mse_loss(pf, x.float())
+    elif target == 2:  # velocity prediction: target = clean - noise as the reference's fp16 tensors (class_to_image:151)
+        ref = torch.nn.functional.mse_loss(pf, (x - nz).float())
     else:
         tt = t.view(-1, 1, 1, 1)
         z = tt * x.float() + (1 - tt) * nz.float()
@@ -819,6 +821,80 @@ def test_embedding(ops):
     ref = torch.zeros(V + 1, D, device=DEV).index_add_(0, ids.view(-1), dr.float())
     ref[V] = 0
     assert rel(dt, ref) < 1e-6
+
+
+@pytest.mark.parametrize("case", ["mixed", "one_row_hot", "empty", "out_of_range", "large"])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_embed_grad_set(ops, case, accumulate):
+    """vpt_embed_grad_set against index_add (float64): duplicates, the padding id (no gradient), ids past the table
+    (ignored), R = 0, every id in one 8-row block (the per-block position lists are O(R), not a rank sort) and the
+    largest R; overwrite (the whole table written, zeros elsewhere) and accumulate (old + sum on the named rows, the
+    others untouched); bitwise reproducible."""
+    V, D = 45, 768  # table rows V + 1 (the padding row V), 6 blocks of 8 rows (the last one ragged)
+    g = torch.Generator().manual_seed(5)
+    R = {"mixed": 64, "one_row_hot": 4096, "empty": 0, "out_of_range": 32, "large": 16384}[case]
+    if case == "one_row_hot":
+        ids = torch.full((R,), 3)
+        ids[::7] = 4
+    else:
+        ids = torch.randint(0, V + 1, (R,), generator=g)
+    if case == "out_of_range":
+        ids[::5] = V + 3
+    ids = ids.to(DEV)
+    dr = rnd(max(R, 1), D, seed=72)[:R]
+    old = rnd(V + 1, D, dtype=torch.float32, seed=73)
+    outs = []
+    for _ in range(2):
+        dt = old.clone()
+        ops.embed_grad_set(dr, ids, V, dt, accumulate=accumulate)
+        outs.append(dt)
+    assert torch.equal(outs[0], outs[1])
+    keep = (ids >= 0) & (ids < V)
+    s = torch.zeros(V + 1, D, dtype=torch.float64, device=DEV).index_add_(0, ids[keep], dr[keep].double())
+    named = torch.zeros(V + 1, dtype=torch.bool, device=DEV)
+    named[ids[keep]] = True
+    ref = torch.where(named[:, None], old.double() + s, old.double()) if accumulate else s
+    err = (outs[0].double() - ref).abs().max().item()
+    assert err <= 1e-6 * max(1.0, ref.abs().max().item()) * max(1, R) ** 0.5, err
+    assert torch.equal(outs[0][V], old[V] if accumulate else torch.zeros_like(old[V]))
+
+
+def test_gauss_noise_is_the_in_kernel_draw(ops):
+    """vpt_gauss_noise writes exactly the noise patchify generates (patchify at t = 0 outputs bf16(eps))."""
+    B, H, W = 2, 64, 96
+    x = rnd(B, 3, H, W, dtype=torch.float16, seed=80)
+    nz = ops.gauss_noise(torch.empty(B, 3, H, W, dtype=torch.float16, device=DEV), 777)
+    a = torch.empty(B * (H // 16) * (W // 16), 768, dtype=torch.bfloat16, device=DEV)
+    b = torch.empty_like(a)
+    t = torch.tensor([0.0, 0.6], device=DEV)
+    ops.patchify(x, B, H, W, a, t=t, seed=777)
+    ops.patchify(x, B, H, W, b, t=t, noise=nz)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("k,H,W", [(2, 64, 96), (4, 128, 64), (2, 1088, 960)])
+@pytest.mark.parametrize("explicit", [False, True])
+def test_area_lowres(ops, k, H, W, explicit):
+    """vpt_area_lowres vs F.interpolate(mode="area", scale_factor=1/k) of the fp16 image, the fp16 noise and the f32
+    noisy image (arb_class_to_image.py:233-245): image / noise within one fp16 rounding, z within one bf16 rounding."""
+    import torch.nn.functional as F
+    B = 2
+    x = rnd(B, 3, H, W, dtype=torch.float16, seed=81)
+    t = torch.tensor([0.25, 0.9], device=DEV)
+    nz = rnd(B, 3, H, W, dtype=torch.float16, seed=82) if explicit else \
+        ops.gauss_noise(torch.empty(B, 3, H, W, dtype=torch.float16, device=DEV), 4321)
+    h, w = H // k, W // k
+    il = torch.empty(B, 3, h, w, dtype=torch.float16, device=DEV)
+    nl, zl = torch.empty_like(il), torch.empty(B, 3, h, w, dtype=torch.bfloat16, device=DEV)
+    ops.area_lowres(x, B, H, W, k, t, il, nl, zl, noise=nz if explicit else None, seed=4321)
+
+    def area(v):
+        return F.interpolate(v.float(), scale_factor=1.0 / k, mode="area")
+    tt = t.view(-1, 1, 1, 1)
+    assert (il.float() - area(x)).abs().max().item() <= 1e-3
+    assert (nl.float() - area(nz)).abs().max().item() <= 2e-3
+    zr = area(tt * x.float() + (1 - tt) * nz.float())
+    assert ((zl.float() - zr).abs() <= zr.abs() * 2 ** -8 + 1e-6).all()
 
 
 # ------------------------------------------------------------------------------------ RAdamScheduleFree

@@ -63,6 +63,43 @@ def test_oracle_matches_reference_micro(micro, micro_fuse, target, fuse):
             assert rel(g.reshape(-1), micro[f"{target}/gfull/{n}"]) < 1e-4, n
 
 
+OBJECTIVES = {"vpred": ("velocity", "velocity", ()), "lowres_x": ("image", "image", (0.5, 0.25)),
+              "lowres_v": ("image", "velocity", (0.5,))}
+
+
+@pytest.mark.parametrize("case", list(OBJECTIVES))
+def test_oracle_matches_reference_objectives(case):
+    """jit_objectives: the reference's own train_step (class_to_image.py with model_pred="velocity";
+    arb_class_to_image.py with lowres_loss passes) vs the oracle's train_step_loss on the same batch."""
+    fx = load_file(os.path.join(GOLD, "jit_objectives.safetensors"))
+    model_pred, loss_target, lowres = OBJECTIVES[case]
+    oc = GC.micro_config()
+    w = O.make_weights(oc, seed=1, n_classes=20)
+    model = O.load_weights(O.OracleJiT(oc), w)
+    emb = w["class_encoder.embedding.weight"].clone().requires_grad_(True)
+    batch = {k: fx[f"{case}/in/{k}"] for k in ("image", "noise", "t", "ids", "mask", "original_size", "target_size",
+                                               "crop_coords")}
+    loss, pred = O.train_step_loss(model, emb, batch, loss_target, model_pred=model_pred, lowres_loss=lowres)
+    loss.backward()
+    grads = {n: p.grad for n, p in model.named_parameters()}
+    grads["class_encoder.embedding.weight"] = emb.grad
+    assert rel(pred.detach(), fx[f"{case}/pred"]) < 1e-5
+    assert abs(loss.item() - fx[f"{case}/loss"].item()) <= 1e-5 * fx[f"{case}/loss"].item()
+    for n, g in grads.items():
+        gn = fx[f"{case}/gnorm/{n}"].item()
+        assert abs(g.norm().item() - gn) <= 1e-4 * gn + 1e-12, n
+        if f"{case}/gfull/{n}" in fx and gn > 1e-9:
+            assert rel(g.reshape(-1), fx[f"{case}/gfull/{n}"]) < 1e-4, n
+
+
+def test_objectives_fixture_branches_differ():
+    """The velocity-prediction objective and the lowres passes change the loss (the branches are exercised)."""
+    fx = load_file(os.path.join(GOLD, "jit_objectives.safetensors"))
+    micro = load_file(os.path.join(GOLD, "jit_micro.safetensors"))
+    assert abs(fx["vpred/loss"].item() - micro["velocity/loss"].item()) > 1e-2 * micro["velocity/loss"].item()
+    assert abs(fx["lowres_x/loss"].item() - fx["lowres_v/loss"].item()) > 1e-3
+
+
 def test_fuse_fixture_differs_from_strip(micro, micro_fuse):
     """The two context modes give different outputs on the same weights and batch (the branch is exercised)."""
     assert rel(micro_fuse["image/pred"], micro["image/pred"]) > 1e-3

@@ -54,12 +54,12 @@ def main():
             sp = ops.wgrad_splits(N, K, M)
             t = {}
             for geo in (0, 128, 256, 2561, 2562):
-                ops.lib.vpt_gemm_set_geometry(geo)
+                _lib.lib.vpt_gemm_set_geometry(geo)
                 sfx = {0: "", 128: "@128", 256: "@256pp", 2561: "@256ring", 2562: "@256_2stage"}[geo]
                 t["fwd" + sfx] = timeit(lambda: ops.linear(x, w, out=y))
                 t["dgrad" + sfx] = timeit(lambda: ops.linear_dgrad(dy, w, out=dx))
                 t["wgrad" + sfx] = timeit(lambda: ops.linear_wgrad(dy, x, dw, splits=sp, workspace=ws))
-            ops.lib.vpt_gemm_set_geometry(0)
+            _lib.lib.vpt_gemm_set_geometry(0)
             t.update({
                 "torch_fwd": timeit(lambda: torch.matmul(x, w.t())),
                 "torch_dgrad": timeit(lambda: torch.matmul(dy, w)),
@@ -84,19 +84,19 @@ def main():
                                          ops._t4(dq, B, rows, H), ops._t4(dk, B, rows, H), ops._t4(dv, B, rows, H),
                                          B, H, rows, n, n))
         for var in (1, 2, 4, 5, 6, 7, 8):  # timing-only ablations of the backward (wrong results)
-            ops.lib.vpt_attn_set_variant(var)
+            _lib.lib.vpt_attn_set_variant(var)
             tv = timeit(lambda: ops.attn_bwd(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, None,
                                              ops._t4(dq, B, rows, H), ops._t4(dk, B, rows, H),
                                              ops._t4(dv, B, rows, H), B, H, rows, n, n))
-            ops.lib.vpt_attn_set_variant(0)
+            _lib.lib.vpt_attn_set_variant(0)
             res.setdefault(f"attn.bwd_alg_abl{var}", []).append(2 * fl / (tv * 1e-3) / 1e12)
             res.setdefault(f"attn.bwd_ms_abl{var}", []).append(tv)
-        ops.lib.vpt_attn_set_variant(3)  # 8-wave blocks (A/B)
+        _lib.lib.vpt_attn_set_variant(3)  # 8-wave blocks (A/B)
         tf4 = timeit(lambda: ops.attn_fwd(q4, k4, v4, o4, lse, None, B, H, rows, n, n))
         tb4 = timeit(lambda: ops.attn_bwd(q4, k4, v4, o4, ops._t4(do, B, rows, H), lse, delta, None,
                                           ops._t4(dq, B, rows, H), ops._t4(dk, B, rows, H), ops._t4(dv, B, rows, H),
                                           B, H, rows, n, n))
-        ops.lib.vpt_attn_set_variant(0)
+        _lib.lib.vpt_attn_set_variant(0)
         res.setdefault("attn.fwd_8wave", []).append(fl / (tf4 * 1e-3) / 1e12)
         res.setdefault("attn.bwd_alg_8wave", []).append(2 * fl / (tb4 * 1e-3) / 1e12)
         res.setdefault("attn.fwd", []).append(fl / (tf * 1e-3) / 1e12)

@@ -158,6 +158,63 @@ __global__ __launch_bounds__(kPatchThreads) void patchify_kernel(const unsigned 
   }
 }
 
+// lowres_loss inputs (train/jit/arb_class_to_image.py:228-264): F.interpolate(mode="area", scale_factor=1/k) of the
+// fp16 image, of the fp16 noise and of the f32 noisy image z = t x + (1-t) eps, for an integer factor k (even: whole
+// pixel pairs of the counter-based noise) -- adaptive average pooling over k x k windows, f32 sums. Writes the
+// resized image and noise as fp16 (the reference's fp16 tensors) and the resized noisy image as bf16 (the model input,
+// lowres_noisy_image.to(bf16)). noise = NULL: the full-resolution noise regenerated from `seed` exactly as patchify
+// and the loss generate it. One thread per output pixel, one 4-B image (and noise) load per pixel pair.
+__global__ void area_lowres_kernel(const unsigned short* __restrict__ img, const unsigned short* __restrict__ noise,
+                                   const float* __restrict__ t, float noise_scale, uint64_t seed, int B, int H, int W,
+                                   int k, unsigned short* __restrict__ img_lr, unsigned short* __restrict__ noise_lr,
+                                   bf16_t* __restrict__ z_lr) {
+  const int h = H / k, w = W / k;
+  const long total = (long)B * 3 * h * w;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int X = i % w, Y = (i / w) % h;
+  const long bc = i / ((long)w * h);  // b * 3 + c
+  const float tb = t[bc / 3];
+  const NoiseKey key = noise_key(seed);
+  float sx = 0.f, se = 0.f, sz = 0.f;
+  for (int dy = 0; dy < k; ++dy) {
+    const long row = (bc * H + (long)Y * k + dy) * W + (long)X * k;
+    for (int dx = 0; dx < k; dx += 2) {
+      const long idx = row + dx;  // even
+      const uint32_t xv = *reinterpret_cast<const uint32_t*>(img + idx);
+      float n0, n1;
+      if (noise) {
+        const uint32_t nv = *reinterpret_cast<const uint32_t*>(noise + idx);
+        n0 = h2f((unsigned short)(nv & 0xffffu));
+        n1 = h2f((unsigned short)(nv >> 16));
+      } else {
+        gauss_pair_fp16(key, pair_counter((uint64_t)idx), n0, n1);
+      }
+      const float x0 = h2f((unsigned short)(xv & 0xffffu)), x1 = h2f((unsigned short)(xv >> 16));
+      const float e0 = h2f(f2h(n0 * noise_scale)), e1 = h2f(f2h(n1 * noise_scale));
+      sx += x0 + x1;
+      se += e0 + e1;
+      sz += (tb * x0 + (1.f - tb) * e0) + (tb * x1 + (1.f - tb) * e1);
+    }
+  }
+  const float inv = 1.f / (float)(k * k);
+  img_lr[i] = f2h(sx * inv);
+  noise_lr[i] = f2h(se * inv);
+  z_lr[i] = f2bf(sz * inv);
+}
+
+// The counter-based noise itself as an fp16 tensor (element idx of a flat [B][3][H][W] image = exactly the draw
+// patchify, the loss and the lowres resize regenerate in-kernel at that index): randn_like(latents) * noise_scale of
+// prepare_scaled_noised_latents (flow_match.py:60-74), for callers that need the tensor (explicit-noise paths, tests).
+__global__ void gauss_noise_kernel(long n2, uint64_t seed, float noise_scale, unsigned short* __restrict__ out) {
+  const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;  // pixel pair
+  if (j >= n2) return;
+  float g0, g1;
+  gauss_pair_fp16(noise_key(seed), pair_counter((uint64_t)(2 * j)), g0, g1);
+  const uint32_t v = (uint32_t)f2h(g0 * noise_scale) | ((uint32_t)f2h(g1 * noise_scale) << 16);
+  reinterpret_cast<uint32_t*>(out)[j] = v;
+}
+
 // Patch rows [B*np][P*P*3] (col = (ky*P + kx)*3 + c) <-> image [B][3][H][W] (bf16), P = 16.
 __global__ void unpatchify_kernel(const bf16_t* __restrict__ patches, int B, int H, int W, bf16_t* __restrict__ img,
                                   int reverse) {
@@ -244,7 +301,9 @@ __global__ void scale_bf16_2d_kernel(const bf16_t* __restrict__ a, long lda, lon
 }
 
 // Flow-matching MSE over patch-layout predictions; also writes d(loss)/d(pred) (bf16, patch layout).
-// target 0 ("image"): mse(pred, x); target 1 ("velocity"): mse((pred-z)/c, (x-z)/c), c = clamp(1-t, eps).
+// target 0 ("image"): mse(pred, x); target 1 ("velocity"): mse((pred-z)/c, (x-z)/c), c = clamp(1-t, eps);
+// target 2 (model_pred="velocity", class_to_image.py:146-156): mse(pred, fp16(x - eps)) -- the fp16 image minus the
+// fp16 noise rounded to fp16 as the reference's fp16 tensor subtraction, no timestep clamp.
 // One 128-thread block per strip (grid-stride past the grid, fixed assignment), patchify's shape: a thread takes the
 // strip's prediction pieces i = tid + 128 k and its image-row pieces (k < 3 for a full strip), every load (and the
 // explicit noise's) issued before the strip is staged through LDS; then each 16-B prediction piece
@@ -329,6 +388,9 @@ __global__ __launch_bounds__(kLossThreads) void loss_kernel(const bf16_t* __rest
         float diff;
         if (!TARGET) {
           diff = pr[e] - xv;
+          g[e] = 2.f * diff * inv_numel;
+        } else if (TARGET == 2) {
+          diff = pr[e] - h2f(f2h(xv - h2f(eps[TARGET ? c : 0][ky][kx])));
           g[e] = 2.f * diff * inv_numel;
         } else {
           const float z = tb * xv + (1.f - tb) * h2f(eps[TARGET ? c : 0][ky][kx]);
@@ -589,50 +651,86 @@ __global__ void embed_scatter_kernel(const bf16_t* __restrict__ drows, const int
   atomicAdd(dtable + id * D + d, bf2f(drows[gid]));
 }
 
-// The class-embedding gradient with overwrite semantics in one pass (replaces a fill of the whole table + the
-// atomic scatter): each block owns kEmbRows table rows, collects the positions p whose id falls in them (LDS list),
-// orders each row's positions ascending (rank sort of the few entries) and writes every row as the sum of its drows
-// rows in position order -- zeros for rows no id names and for the padding row (nn.Embedding padding_idx, as the
-// scatter skips it). Deterministic, unlike the atomics. Dynamic LDS: R ints (the list) + R ints (sorted), R <= 8192.
-constexpr int kEmbRows = 8;
-__global__ void embed_grad_set_kernel(const bf16_t* __restrict__ drows, const int64_t* __restrict__ ids, int R, int D,
-                                      long pad_id, long V, float* __restrict__ dtable) {
-  extern __shared__ int elist[];  // [R] unsorted keys, then [R] sorted
-  __shared__ int cnt, start[kEmbRows + 1];
-  int* sorted = elist + R;
+// The class-embedding gradient in one deterministic pass (replaces a fill of the whole table + the atomic scatter):
+// each block owns kEmbRows table rows and builds, per row, the list of positions p whose id names it, in ascending p
+// without a sort: thread t scans the contiguous position chunk [t*ch, (t+1)*ch), counts its hits per row, an exclusive
+// scan over the threads (per row) gives each thread its offsets, and a second scan of the chunk writes the positions
+// there -- O(R) per block however many ids share a row. Every row is then the sum of its drows rows in position order
+// -- zeros for rows no id names and for the padding row (nn.Embedding padding_idx, as the scatter skips it). accumulate:
+// the old value plus that sum (torch's .grad += of the dense embedding gradient); rows no id names are left as they
+// are. Dynamic LDS: R ints (the lists), R <= 16384.
+constexpr int kEmbRows = 8, kEmbThreads = 256;
+__global__ __launch_bounds__(kEmbThreads) void embed_grad_set_kernel(const bf16_t* __restrict__ drows,
+                                                                     const int64_t* __restrict__ ids, int R, int D,
+                                                                     long pad_id, long V, int accumulate,
+                                                                     float* __restrict__ dtable) {
+  extern __shared__ int elist[];  // [R] positions, grouped by row, ascending within a row
+  __shared__ int cnt[kEmbRows][kEmbThreads + 1];
+  __shared__ int start[kEmbRows + 1];
   const long r0 = (long)blockIdx.x * kEmbRows;
-  if (threadIdx.x == 0) cnt = 0;
-  __syncthreads();
-  for (int p = threadIdx.x; p < R; p += blockDim.x) {
+  const int ch = (R + kEmbThreads - 1) / kEmbThreads;
+  const int lo = min(R, (int)threadIdx.x * ch), hi = min(R, lo + ch);
+  int c[kEmbRows];
+#pragma unroll
+  for (int ro = 0; ro < kEmbRows; ++ro) c[ro] = 0;
+  for (int p = lo; p < hi; ++p) {
     const long id = ids[p];
-    if (id >= r0 && id < r0 + kEmbRows && id != pad_id) elist[atomicAdd(&cnt, 1)] = (int)(id - r0) * R + p;
+    if (id >= r0 && id < r0 + kEmbRows && id != pad_id) {
+#pragma unroll
+      for (int ro = 0; ro < kEmbRows; ++ro) c[ro] += (id - r0) == ro;
+    }
+  }
+#pragma unroll
+  for (int ro = 0; ro < kEmbRows; ++ro) cnt[ro][threadIdx.x] = c[ro];
+  __syncthreads();
+  if (threadIdx.x < kEmbRows) {  // row ro: exclusive scan over the threads; the total in cnt[ro][kEmbThreads]
+    int run = 0;
+    for (int t = 0; t < kEmbThreads; ++t) {
+      const int v = cnt[threadIdx.x][t];
+      cnt[threadIdx.x][t] = run;
+      run += v;
+    }
+    cnt[threadIdx.x][kEmbThreads] = run;
   }
   __syncthreads();
-  const int m = cnt;
-  for (int i = threadIdx.x; i < m; i += blockDim.x) {  // keys are distinct: rank = number of smaller keys
-    const int k = elist[i];
-    int rank = 0;
-    for (int j = 0; j < m; ++j) rank += elist[j] < k;
-    sorted[rank] = k;
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int ro = 0; ro < kEmbRows; ++ro) {
+      start[ro] = run;
+      run += cnt[ro][kEmbThreads];
+    }
+    start[kEmbRows] = run;
   }
-  if (threadIdx.x <= kEmbRows) {  // first sorted entry of row offset threadIdx.x
-    int c = 0;
-    for (int j = 0; j < m; ++j) c += elist[j] < (int)threadIdx.x * R;
-    start[threadIdx.x] = c;
+  __syncthreads();
+  {
+    int o[kEmbRows];
+#pragma unroll
+    for (int ro = 0; ro < kEmbRows; ++ro) o[ro] = start[ro] + cnt[ro][threadIdx.x];
+    for (int p = lo; p < hi; ++p) {
+      const long id = ids[p];
+      if (id >= r0 && id < r0 + kEmbRows && id != pad_id) {
+#pragma unroll
+        for (int ro = 0; ro < kEmbRows; ++ro)
+          if ((id - r0) == ro) elist[o[ro]++] = p;
+      }
+    }
   }
   __syncthreads();
   const int nc = D >> 2;
   for (int idx = threadIdx.x; idx < kEmbRows * nc; idx += blockDim.x) {
-    const int ro = idx / nc, c = idx % nc;
+    const int ro = idx / nc, c4 = idx % nc;
     if (r0 + ro >= V) break;
+    const int e0 = start[ro], e1 = start[ro + 1];
+    if (accumulate && e0 == e1) continue;
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int e = start[ro]; e < start[ro + 1]; ++e) {
-      const int pos = sorted[e] - ro * R;
-      const uint2 w = *reinterpret_cast<const uint2*>(drows + (long)pos * D + 4 * c);
+    for (int e = e0; e < e1; ++e) {
+      const uint2 w = *reinterpret_cast<const uint2*>(drows + (long)elist[e] * D + 4 * c4);
       acc += floatx4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u), __uint_as_float(w.y << 16),
                      __uint_as_float(w.y & 0xffff0000u)};
     }
-    *reinterpret_cast<floatx4*>(dtable + (r0 + ro) * D + 4 * c) = acc;
+    floatx4* dst = reinterpret_cast<floatx4*>(dtable + (r0 + ro) * D + 4 * c4);
+    if (accumulate) acc = *dst + acc;
+    *dst = acc;
   }
 }
 
@@ -926,19 +1024,43 @@ extern "C" int vpt_scale_bf16_2d(const void* a, long lda, long rows, int cols, f
   return VPT_OK;
 }
 
+extern "C" int vpt_area_lowres(const void* img, const void* noise, const float* t, float noise_scale,
+                               unsigned long long seed, int B, int H, int W, int k, void* img_lr, void* noise_lr,
+                               void* z_lr, void* stream) {
+  VPT_CHECK_ARG(img && t && img_lr && noise_lr && z_lr && B > 0, "vpt_area_lowres: null pointer");
+  VPT_CHECK_ARG(k >= 2 && k % 2 == 0 && H % k == 0 && W % k == 0,
+                "vpt_area_lowres: the factor must be even and divide H and W");
+  const long n = (long)B * 3 * (H / k) * (W / k);
+  hipLaunchKernelGGL(area_lowres_kernel, grid1(n), dim3(256), 0, (hipStream_t)stream, (const unsigned short*)img,
+                     (const unsigned short*)noise, t, noise_scale, (uint64_t)seed, B, H, W, k,
+                     (unsigned short*)img_lr, (unsigned short*)noise_lr, (bf16_t*)z_lr);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+extern "C" int vpt_gauss_noise(long n, unsigned long long seed, float noise_scale, void* out, void* stream) {
+  VPT_CHECK_ARG(out && n >= 0 && n % 2 == 0, "vpt_gauss_noise: n must be even");
+  if (n == 0) return VPT_OK;
+  hipLaunchKernelGGL(gauss_noise_kernel, grid1(n / 2), dim3(256), 0, (hipStream_t)stream, n / 2, (uint64_t)seed,
+                     noise_scale, (unsigned short*)out);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
 extern "C" int vpt_loss_blocks(void) { return kLossBlocks; }
 
 extern "C" int vpt_flow_loss(const void* pred, const void* img, const void* noise, const float* t, float noise_scale,
                              unsigned long long seed, int target, float t_eps, int B, int H, int W, void* dpred,
                              float* part, float* loss, void* stream) {
   VPT_CHECK_ARG(pred && img && t && dpred && part && loss, "vpt_flow_loss: null pointer");
-  VPT_CHECK_ARG(target == 0 || target == 1, "vpt_flow_loss: target must be 0 (image) or 1 (velocity)");
+  VPT_CHECK_ARG(target >= 0 && target <= 2,
+                "vpt_flow_loss: target must be 0 (image), 1 (velocity of an image prediction) or 2 (velocity prediction)");
   VPT_CHECK_ARG(B > 0 && H % 16 == 0 && W % 16 == 0, "vpt_flow_loss: H and W must be multiples of the 16-px patch");
   const float numel = (float)B * 3.f * H * W;
   const long strips = (long)B * (H / 16) * ((W / 16 + kStripP - 1) / kStripP);
   const int blocks = (int)(strips < kLossBlocks ? strips : kLossBlocks);  // partials part[0, blocks)
   hipStream_t s = (hipStream_t)stream;
-  auto kern = target == 0 ? loss_kernel<0> : loss_kernel<1>;
+  auto kern = target == 0 ? loss_kernel<0> : target == 1 ? loss_kernel<1> : loss_kernel<2>;
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(kLossThreads), 0, s, (const bf16_t*)pred, (const unsigned short*)img,
                      (const unsigned short*)noise, t, noise_scale, (uint64_t)seed, t_eps, B, H, W, 1.f / numel,
                      (bf16_t*)dpred, part);
@@ -1041,13 +1163,12 @@ extern "C" int vpt_embed_scatter_add(const void* drows, const long long* ids, lo
 }
 
 extern "C" int vpt_embed_grad_set(const void* drows, const long long* ids, long R, int D, long long pad_id, long V,
-                                  float* dtable, void* stream) {
+                                  int accumulate, float* dtable, void* stream) {
   VPT_CHECK_ARG((drows || R == 0) && (ids || R == 0) && dtable && D % 4 == 0 && V > 0, "vpt_embed_grad_set: bad args");
-  VPT_CHECK_ARG(R >= 0 && R <= 8192, "vpt_embed_grad_set: R <= 8192 ids (LDS position lists)");
-  VPT_CHECK_ARG((long)kEmbRows * R < (1L << 31), "vpt_embed_grad_set: key range");
-  hipLaunchKernelGGL(embed_grad_set_kernel, dim3((unsigned)((V + kEmbRows - 1) / kEmbRows)), dim3(256),
-                     (size_t)(2 * R) * sizeof(int), (hipStream_t)stream, (const bf16_t*)drows, (const int64_t*)ids,
-                     (int)R, D, (long)pad_id, V, dtable);
+  VPT_CHECK_ARG(R >= 0 && R <= 16384, "vpt_embed_grad_set: R <= 16384 ids (LDS position lists)");
+  hipLaunchKernelGGL(embed_grad_set_kernel, dim3((unsigned)((V + kEmbRows - 1) / kEmbRows)), dim3(kEmbThreads),
+                     (size_t)(R > 0 ? R : 1) * sizeof(int), (hipStream_t)stream, (const bf16_t*)drows,
+                     (const int64_t*)ids, (int)R, D, (long)pad_id, V, accumulate, dtable);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

@@ -51,6 +51,8 @@ SIGNATURES: dict[str, list] = {
     "vpt_patchify": [P, I, P, P, F, U64, I, I, I, P, P],
     "vpt_unpatchify": [P, I, I, I, P, I, P],
     "vpt_loss_blocks": [],
+    "vpt_gauss_noise": [L, U64, F, P, P],
+    "vpt_area_lowres": [P, P, P, F, U64, I, I, I, I, P, P, P, P],
     "vpt_euler_cfg_step": [P, P, I, I, I, I, F, I, F, F, P],
     "vpt_flow_loss": [P, P, P, P, F, U64, I, F, I, I, I, P, P, P, P],
     "vpt_timestep_embed": [P, I, P, P],
@@ -63,7 +65,7 @@ SIGNATURES: dict[str, list] = {
     "vpt_bias_grad": [P, L, L, I, P, P, I, P],
     "vpt_embed_gather": [P, P, L, I, P, P],
     "vpt_embed_scatter_add": [P, P, L, I, LL, P, P],
-    "vpt_embed_grad_set": [P, P, L, I, LL, L, P, P],
+    "vpt_embed_grad_set": [P, P, L, I, LL, L, I, P, P],
     "vpt_step_inputs": [P, I, F, P, P, P, P, P, P, I, I, I, P, P],
     "vpt_cast_f32_bf16": [P, L, P, P],
     "vpt_radam_sf_step": [P, P, I, P, P, L, F, F, F, F, F, F, F, F, I, P, F, P],
@@ -171,7 +173,7 @@ def _load(path: Path, diag: bool = False) -> C.CDLL:
     return lib
 
 
-ABI_VERSION = 3  # the signatures in SIGNATURES / include/vpt_hip.h
+ABI_VERSION = 4  # the signatures in SIGNATURES / include/vpt_hip.h
 
 
 def load_library(path: Path | str, diag: bool = False) -> C.CDLL:

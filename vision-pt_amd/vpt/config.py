@@ -3,15 +3,17 @@ YAML `model.denoiser:` dicts validate unchanged).
 
   DenoiserConfig      <- src/models/jit/config.py:16-46
   JiT_B_16_Config     <- src/models/jit/config.py:49-65
-  JiTTrainingConfig   <- train/jit/arb_class_to_image.py:26-44 (JiTConfigForTraining fields that
-                         the training step reads)
+  JiTTrainingConfig   <- train/jit/arb_class_to_image.py:26-44 (JiTConfigForTraining, every field, including the
+                         inherited JiTConfig ones of src/models/jit/config.py:95-102); unknown keys are refused
+                         (extra="forbid") instead of silently dropped, and the reference's known values this path
+                         does not build raise NotImplementedError as the reference's own treat_loss does
 """
 
 from __future__ import annotations
 
 from typing import Literal
 
-from pydantic import BaseModel
+from pydantic import BaseModel, ConfigDict, field_validator, model_validator
 
 NormType = Literal["layer", "rms", "dyt", "derf"]
 PositionalEncoding = Literal["rope", "pope", "n-pope"]
@@ -77,6 +79,20 @@ class JiT_B_16_Config(DenoiserConfig):
 
 
 class JiTTrainingConfig(BaseModel):
+    """The `model:` section of a JiT training YAML (configs/jit/x-loss/config.yml). Objectives: model_pred "image"
+    with loss_target "image" | "velocity" (arb_class_to_image.py:108-147), model_pred "velocity" with loss_target
+    "velocity" (class_to_image.py:146-156: target clean - noise, no timestep clamp); lowres_loss adds one pass per
+    scale on area-resized inputs (arb_class_to_image.py:228-272)."""
+
+    model_config = ConfigDict(extra="forbid")
+
+    # JiTConfig (src/models/jit/config.py:95-102)
+    dtype: str = "float32"
+    context_encoder: dict | None = None
+    denoiser: DenoiserConfig = JiT_B_16_Config()
+    model_pred: Literal["image", "velocity", "noise"] = "image"
+    # JiTConfigForTraining (train/jit/arb_class_to_image.py:26-40)
+    checkpoint_path: str | None = None
     max_token_length: int = 64
     noise_scale: float = 1.0
     timestep_eps: float = 0.05
@@ -84,6 +100,41 @@ class JiTTrainingConfig(BaseModel):
     timestep_sampling: str = "scale_shift_sigmoid"
     train_class_encoder: bool = True
     drop_context_rate: float = 0.1
+    lowres_loss: list[float] = []
+
+    @field_validator("context_encoder")
+    @classmethod
+    def _class_context(cls, v):
+        if v is not None and v.get("type", "class") != "class":
+            raise NotImplementedError("HIP JiT: only the class context encoder (text encoders are out of scope)")
+        return v
+
+    @model_validator(mode="after")
+    def _objective(self):
+        if self.model_pred == "noise":  # class_to_image.py:161-162
+            raise NotImplementedError("Noise prediction is not implemented yet.")
+        if self.model_pred == "velocity" and self.loss_target != "velocity":  # class_to_image.py:157-160
+            raise NotImplementedError("Velocity prediction with image loss is not implemented yet.")
+        for s in self.lowres_loss:
+            if s > 0.0:
+                lowres_factor(s)
+        return self
+
+    @property
+    def loss_kind(self) -> int:
+        """vpt_flow_loss target: 0 image loss, 1 velocity loss of an image prediction, 2 velocity prediction."""
+        if self.model_pred == "velocity":
+            return 2
+        return 0 if self.loss_target == "image" else 1
+
+
+def lowres_factor(scale: float) -> int:
+    """The integer area-pooling factor k of a lowres_loss scale (F.interpolate(scale_factor=scale, mode="area") with
+    scale = 1/k): the HIP path builds even k (2, 4, 6, ...: whole pixel pairs of the noise generator)."""
+    k = round(1.0 / scale)
+    if k < 2 or k % 2 or abs(k * scale - 1.0) > 1e-9:
+        raise NotImplementedError(f"HIP JiT: lowres_loss scale {scale} must be 1/k for an even integer k")
+    return k
 
 
 def check_supported(cfg: DenoiserConfig) -> None:

@@ -88,39 +88,74 @@ class _SubPool:
         self.pool, self.h, self.n = pool, h, n
 
     def get(self, name: str, shape, dtype=BF16, zero: bool = False) -> torch.Tensor:
-        full = self.pool.get(name, (shape[0] * self.n,) + tuple(shape[1:]), dtype, zero)
-        return full[self.h * shape[0]:(self.h + 1) * shape[0]]
+        # the pooled buffer is shared by every lane: only this lane's slice may be zeroed, on this lane's stream
+        full = self.pool.get(name, (shape[0] * self.n,) + tuple(shape[1:]), dtype)
+        v = full[self.h * shape[0]:(self.h + 1) * shape[0]]
+        if zero:
+            v.zero_()
+        return v
 
 
 class _Pool:
-    """Named, growable device buffers (views into cached storages)."""
+    """Named, growable device buffers (views into cached storages).
 
-    def __init__(self, device):
+    A storage is allocated (zero-filled: rows a kernel never writes, e.g. a pre-context block's context rows, must stay
+    finite) on the first use of a name or when a larger bucket needs it to grow. That may happen on any of the engine's
+    streams (sub-batch lanes, the weight-gradient stream) and is made safe for all of them without a host sync:
+    - the zero fill runs on the allocating stream, and an event recorded after it is waited for (stream-ordered) by
+      every other stream's next get() of that name until the next point where all streams have joined (`joined()`);
+    - a replaced storage is marked used by every engine stream (record_stream), so the caching allocator does not hand
+      its memory out again before the work those streams have enqueued so far is done."""
+
+    def __init__(self, device, streams=None):
         self.device = device
         self.store: dict[str, torch.Tensor] = {}
+        self._ready: dict[str, tuple] = {}  # name -> (event after the zero fill, allocating stream)
+        self._streams = streams             # callable -> the engine's streams (record_stream on replacement)
 
     def get(self, name: str, shape, dtype=BF16, zero: bool = False) -> torch.Tensor:
         n = 1
         for s in shape:
             n *= s
         cur = self.store.get(name)
+        cuda = self.device.type == "cuda"
         if cur is None or cur.numel() < n or cur.dtype != dtype:
-            # zero-filled at allocation: rows that a kernel never writes (e.g. context rows of
-            # pre-context blocks) must stay finite. Allocation (first use of a name, or growth for a larger
-            # batch) is rare and may happen on any of the engine's streams (sub-batch lanes, the weight-gradient
-            # stream), so it is made safe for all of them: nothing may still use a storage being replaced, and the
-            # zero fill completes before any stream touches the new one.
-            multi = self.device.type == "cuda"
-            if multi:
-                torch.cuda.synchronize(self.device)
+            if cur is not None and cuda:
+                for st in self._engine_streams():
+                    cur.record_stream(st)
             cur = torch.zeros(max(n, 1), dtype=dtype, device=self.device)
-            if multi:
-                torch.cuda.current_stream(self.device).synchronize()
+            if cuda:
+                ev = torch.cuda.Event()
+                here = torch.cuda.current_stream(self.device)
+                ev.record(here)
+                self._ready[name] = (ev, here)
             self.store[name] = cur
+        elif cuda and name in self._ready:
+            ev, src = self._ready[name]
+            here = torch.cuda.current_stream(self.device)
+            if here != src:
+                here.wait_event(ev)
         v = cur[:n].view(*shape)
         if zero:
             v.zero_()
         return v
+
+    def joined(self, streams):
+        """`streams` (and the caller's stream) have just been joined into the caller's stream, and every stream forks
+        from the caller's stream (wait_stream) before it next uses a pooled buffer: the zero fills those streams
+        enqueued are ordered before any later use, so their pending events can go."""
+        keep = {}
+        joined = list(streams) + [torch.cuda.current_stream(self.device)]
+        for name, (ev, src) in self._ready.items():
+            if not any(src == st for st in joined):
+                keep[name] = (ev, src)
+        self._ready = keep
+
+    def _engine_streams(self):
+        out = [torch.cuda.current_stream(self.device), torch.cuda.default_stream(self.device)]
+        if self._streams is not None:
+            out += [s for s in self._streams() if s is not None]
+        return out
 
 
 class JiTEngine:
@@ -133,8 +168,8 @@ class JiTEngine:
         self.layout = ParamLayout(cfg, n_classes)
         self.params = params if params is not None else torch.zeros(self.layout.total, dtype=BF16, device=self.device)
         self.grads = grads if grads is not None else torch.zeros(self.layout.total, dtype=F32, device=self.device)
-        self.pool = _Pool(self.device)
-        self.pool_infer = _Pool(self.device)  # no-grad forwards never clobber saved activations
+        self.pool = _Pool(self.device, self._pool_streams)
+        self.pool_infer = _Pool(self.device, self._pool_streams)  # no-grad forwards never clobber saved activations
         self.rope = RopeCache(cfg, self.device)
         self.D = cfg.hidden_size
         self.F = cfg.mlp_hidden_padded  # zero-padded SwiGLU width (vpt.params.ParamSpec)
@@ -145,6 +180,9 @@ class JiTEngine:
         self._wstream = None  # the weight-gradient stream (CONCURRENT_WGRAD), created on first use
         self._mstreams = []   # the sub-batch streams (MICRO_SPLIT)
         self._bind()
+
+    def _pool_streams(self):
+        return list(self._mstreams) + ([self._wstream] if self._wstream is not None else [])
 
     # ------------------------------------------------------------------ parameter views
     def _bind(self):
@@ -287,6 +325,7 @@ class JiTEngine:
         if S > 1:
             for st in subs:
                 main.wait_stream(st)
+            pool.joined(subs)
         # --- final layer + (per-patch) output (denoiser.py:1115-1116, 535-543)
         f = self.fin
         M2 = B * np_
@@ -622,6 +661,7 @@ class JiTEngine:
             # run on the main stream, after every block's weight gradient
             main.wait_stream(side)
             on_side = False
+            pool.joined(list(self._mstreams) + [side])
         # --- embeddings backward
         dpe2 = pool.get("d_pe2", (M2, D))
         dsize = pool.get("d_size", (6 * B, D))

@@ -12,7 +12,8 @@ import ctypes
 
 import torch
 
-from ._lib import call, lib
+from . import _lib
+from ._lib import call  # the size helpers read _lib.lib per call: tools/ may switch builds (use_library)
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -430,7 +431,7 @@ def rmsnorm_fwd(x, w, out=None, rstd=None, eps=1e-6):
 
 
 def rmsnorm_bwd_blocks(M: int) -> int:
-    return lib.vpt_rmsnorm_bwd_blocks(M)
+    return _lib.lib.vpt_rmsnorm_bwd_blocks(M)
 
 
 def rmsnorm_bwd(dy, x, rstd, w, dres=None, dx=None, dw_part=None):
@@ -469,7 +470,7 @@ def qknorm_rope_fwd(qkv, wq, wk, cos_t, sin_t, rows_per_seq, out=None, eps=1e-6,
 
 
 def qknorm_rope_blocks(M: int) -> int:
-    return lib.vpt_qknorm_rope_blocks(M)
+    return _lib.lib.vpt_qknorm_rope_blocks(M)
 
 
 def qknorm_rope_bwd(dqk, qkv, wq, wk, cos_t, sin_t, rows_per_seq, dqkv, dw_part=None, eps=1e-6, n_valid=None):
@@ -543,7 +544,7 @@ def attn_bwd(q, k, v, o, do, lse, delta, kbias, dq, dk, dv, B, H, rows, n, n_den
 
 
 def attn_bwd_dw_rows(B: int, H: int, n: int) -> int:
-    return int(lib.vpt_attn_bwd_dw_rows(B, H, n))
+    return int(_lib.lib.vpt_attn_bwd_dw_rows(B, H, n))
 
 
 def attn_bwd_qknorm(q, k, v, o, do, lse, delta, kbias, xq, xk, wq, wk, cos_t, sin_t, dq, dk, dw_part, dv,
@@ -578,6 +579,21 @@ def patchify(img, B, H, W, out, t=None, noise=None, noise_scale=1.0, seed=0, noi
     return out
 
 
+def gauss_noise(out, seed, noise_scale=1.0):
+    """out (fp16, any shape, even numel) <- the in-kernel noise draw of `seed` at each flat element index."""
+    call("vpt_gauss_noise", out.numel(), seed, noise_scale, out.data_ptr(), stream())
+    return out
+
+
+def area_lowres(img, B, H, W, k, t, img_lr, noise_lr, z_lr, noise=None, noise_scale=1.0, seed=0):
+    """F.interpolate(mode="area", scale_factor=1/k) of the fp16 image, the fp16 noise (explicit or regenerated from
+    `seed`) and the noisy image (arb_class_to_image.py:233-245) -> img_lr / noise_lr fp16, z_lr bf16 [B,3,H/k,W/k]."""
+    _launch("area_lowres", B * 3 * H * W * (2 + (2 if noise is not None else 0)) + B * 3 * (H // k) * (W // k) * 6,
+            lambda: call("vpt_area_lowres", img.data_ptr(), _p(noise), t.data_ptr(), noise_scale, seed, B, H, W, k,
+                         img_lr.data_ptr(), noise_lr.data_ptr(), z_lr.data_ptr(), stream()))
+    return img_lr, noise_lr, z_lr
+
+
 def unpatchify(patches, B, H, W, img, reverse=False):
     call("vpt_unpatchify", patches.data_ptr(), B, H, W, img.data_ptr(), int(reverse), stream())
     return img
@@ -591,7 +607,7 @@ def euler_cfg_step(z, pred, B, H, W, cfg, cfg_scale, mode, t, dt):
 
 
 def loss_blocks() -> int:
-    return lib.vpt_loss_blocks()
+    return _lib.lib.vpt_loss_blocks()
 
 
 def flow_loss(pred, img, t, B, H, W, dpred, part, loss, target=0, t_eps=0.05, noise=None, noise_scale=1.0,
@@ -637,7 +653,7 @@ def swiglu_bwd(dh, x12, dx12):
 
 
 def colsum_blocks(M: int) -> int:
-    return lib.vpt_colsum_blocks(M)
+    return _lib.lib.vpt_colsum_blocks(M)
 
 
 def bias_grad(dy, out, part=None, accumulate=False):
@@ -669,16 +685,16 @@ def embed_scatter_add(drows, ids, pad_id, dtable):
          stream())
 
 
-def embed_grad_set(drows, ids, pad_id, dtable):
-    """dtable[V, D] f32 = the embedding gradient of drows [R, D] bf16 at ids [R] (overwrite; padding row and unnamed
-    rows zero; each row summed in position order)."""
+def embed_grad_set(drows, ids, pad_id, dtable, accumulate=False):
+    """dtable[V, D] f32 = (or += with accumulate) the embedding gradient of drows [R, D] bf16 at ids [R]; overwrite:
+    padding row and unnamed rows zero; each row summed in position order (deterministic on both paths)."""
     R = ids.numel()
     call("vpt_embed_grad_set", drows.data_ptr() if R else None, ids.data_ptr() if R else None, R, dtable.shape[1],
-         pad_id, dtable.shape[0], dtable.data_ptr(), stream())
+         pad_id, dtable.shape[0], int(bool(accumulate)), dtable.data_ptr(), stream())
     return dtable
 
 
-EMBED_GRAD_SET_MAX_IDS = 8192
+EMBED_GRAD_SET_MAX_IDS = 16384
 
 
 def step_inputs(t, tscale, orig, target, crop, t_vals, size_vals, mask, n_ctx, n_pre, rows, kbias):
@@ -825,7 +841,7 @@ def layernorm_bwd_lora(dy, x, mean, rstd, w, up, alpha: float, vs, dres=None):
 
 
 def layernorm_bwd_blocks(M: int) -> int:
-    return lib.vpt_layernorm_bwd_blocks(M)
+    return _lib.lib.vpt_layernorm_bwd_blocks(M)
 
 
 def geglu_fwd(x12, out=None):
@@ -1141,8 +1157,8 @@ def lora_wgrad2(dy, ds, g_up, x, vs, g_down, accumulate=True, alpha=1.0):
     n_in = x.shape[1]
     b = _LORA_BATCH
     if b is None:
-        ws_up = _lora_ws(dy.device, "up", int(lib.vpt_lora_wgrad_workspace(M, n_out)))
-        ws_dn = _lora_ws(dy.device, "down", int(lib.vpt_lora_wgrad_workspace(M, n_in)))
+        ws_up = _lora_ws(dy.device, "up", int(_lib.lib.vpt_lora_wgrad_workspace(M, n_out)))
+        ws_dn = _lora_ws(dy.device, "down", int(_lib.lib.vpt_lora_wgrad_workspace(M, n_in)))
         call("vpt_lora_wgrad2", dy.data_ptr(), dy.stride(0), ds.data_ptr(), ds.stride(0), g_up.data_ptr(), n_out,
              x.data_ptr(), x.stride(0), vs.data_ptr(), vs.stride(0), g_down.data_ptr(), n_in, M, int(accumulate),
              float(alpha), ws_up.data_ptr(), ws_dn.data_ptr(), stream())
@@ -1150,8 +1166,8 @@ def lora_wgrad2(dy, ds, g_up, x, vs, g_down, accumulate=True, alpha=1.0):
     for t, dt in ((g_up, F32), (g_down, F32)):
         _chk(t, dt, "adapter grad")
     b.reserve((float(alpha), int(accumulate)), 2)
-    ws_up = b.ws(dy.device, int(lib.vpt_lora_wgrad_workspace(M, n_out)))
-    ws_dn = b.ws(dy.device, int(lib.vpt_lora_wgrad_workspace(M, n_in)))
+    ws_up = b.ws(dy.device, int(_lib.lib.vpt_lora_wgrad_workspace(M, n_out)))
+    ws_dn = b.ws(dy.device, int(_lib.lib.vpt_lora_wgrad_workspace(M, n_in)))
     if _LORA_DEFER:
         for t in (dy, ds, x, vs):
             if t.stride(1) != 1 or t.stride(0) % 8:
