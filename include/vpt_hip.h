@@ -157,6 +157,17 @@ int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr, const void* k, 
                  long l_sh, const float* kbias, long kb_sb, void* dq, long dq_sb, long dq_sh, long dq_sr,
                  void* dk, long dk_sb, long dk_sh, long dk_sr, void* dv, long dv_sb, long dv_sh, long dv_sr,
                  int B, int H, int n, int nk, int n_dense, float scale, void* stream);
+/* vpt_attn_bwd on a persistent work-queue kernel: the same dK/dV and dQ items and products, bitwise the same results,
+ * run by two resident blocks per CU pulling items from per-XCD queues (dynamic fill; the next item's first tile staged
+ * under the current item's last). queue = vpt_attn_bwd_queue_bytes() (64) bytes of 64-byte-aligned device memory owned
+ * by the caller: zero before its first use, left zero by every launch; one per stream that may run it concurrently. */
+int vpt_attn_bwd_q(const void* q, long q_sb, long q_sh, long q_sr, const void* k, long k_sb, long k_sh, long k_sr,
+                   const void* v, long v_sb, long v_sh, long v_sr, const void* o, long o_sb, long o_sh, long o_sr,
+                   const void* dO, long do_sb, long do_sh, long do_sr, const float* lse, float* delta, long l_sb,
+                   long l_sh, const float* kbias, long kb_sb, void* dq, long dq_sb, long dq_sh, long dq_sr, void* dk,
+                   long dk_sb, long dk_sh, long dk_sr, void* dv, long dv_sb, long dv_sh, long dv_sr, int B, int H, int n,
+                   int nk, int n_dense, float scale, void* queue, void* stream);
+int vpt_attn_bwd_queue_bytes(void);
 /* The same backward with the per-head QK-RMSNorm + RoPE backward fused into its dQ / dK stores (JiT self-attention,
  * src/models/jit/denoiser.py:307-316, 98-111; replaces vpt_attn_bwd + vpt_qknorm_rope_bwd for that path): q, k are
  * the normed, roped (q pre-scaled) attention inputs as for vpt_attn_bwd; xq / xk the raw projections they came from

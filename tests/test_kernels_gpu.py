@@ -434,6 +434,53 @@ def test_attention_fwd_bwd(ops, n, n_dense, masked):
     assert rel(unh(dv), vf.grad) < 2e-2
 
 
+@pytest.mark.parametrize("B,H,n,nk,n_dense,masked", [(2, 3, 200, 200, 150, True), (2, 3, 40, 40, 20, True),
+                                                     (1, 2, 64, 64, 64, False), (2, 12, 4170, 4170, 4106, True),
+                                                     (3, 5, 1034, 1034, 1024, True), (2, 3, 300, 231, 231, False),
+                                                     (2, 3, 1000, 77, 38, True)])
+def test_attention_bwd_queue_bitwise(ops, B, H, n, nk, n_dense, masked):
+    """vpt_attn_bwd_q (resident blocks pulling the dK/dV and dQ items from per-XCD work queues, the next item's first
+    tile staged under the current item's last) is bitwise vpt_attn_bwd (one block per item): self- and cross-attention,
+    ragged and sub-tile lengths, masks, fewer items than resident blocks (40 rows) and the C3 shape; three launches in a
+    row on the same queue words (each launch resets them) and two streams with their own queues at once."""
+    D = H * 64
+    q = prescale_q(ops, rnd(B * n, D, seed=90), D)
+    kv = rnd(B * nk, 2 * D, seed=91)
+    kb = torch.zeros(B, nk, device=DEV)
+    if masked:
+        kb[0, n_dense + (nk - n_dense) // 2:] = float("-inf")
+    o = torch.zeros(B * n, D, dtype=torch.bfloat16, device=DEV)
+    lse = torch.zeros(B, H, n, device=DEV)
+    q4, k4, v4, o4 = (ops._t4(q, B, n, H, 0), ops._t4(kv, B, nk, H, 0), ops._t4(kv, B, nk, H, D),
+                      ops._t4(o, B, n, H, 0))
+    ops.attn_fwd(q4, k4, v4, o4, lse, kb, B, H, n, n, n_dense, nk=nk)
+    do = rnd(B * n, D, seed=92)
+
+    def run(queue):
+        dq = torch.full((B * n, D), 7.0, dtype=torch.bfloat16, device=DEV)
+        dkv = torch.full((B * nk, 2 * D), 7.0, dtype=torch.bfloat16, device=DEV)
+        delta = torch.zeros(B, H, n, device=DEV)
+        ops.attn_bwd(q4, k4, v4, o4, ops._t4(do, B, n, H, 0), lse, delta, kb, ops._t4(dq, B, n, H, 0),
+                     ops._t4(dkv, B, nk, H, 0), ops._t4(dkv, B, nk, H, D), B, H, n, n, n_dense, nk=nk, queue=queue)
+        return dq, dkv
+
+    ref = run(False)
+    for _ in range(3):
+        got = run(True)
+        torch.cuda.synchronize()
+        assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+    assert ops.attn_queue().abs().sum().item() == 0  # left reset
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for st in streams:
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            outs.append(run(True))
+    torch.cuda.synchronize()
+    for got in outs:
+        assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+
+
 @pytest.mark.parametrize("n,n_dense,masked", [(200, 150, True), (330, 330, False), (1034, 1024, True), (700, 520, True)])
 def test_attention_bwd_fused_qknorm_rope(ops, n, n_dense, masked):
     """vpt_attn_bwd_qknorm (the QK-RMSNorm + RoPE backward fused into the attention backward's dQ / dK stores) vs an

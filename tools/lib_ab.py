@@ -6,6 +6,8 @@ routed through each in turn (vpt._lib.use_library), interleaved over rounds, so 
          4106 always-valid keys, 12 heads, QK-normed inputs), HIP events on the launching stream, per-launch medians;
          outputs compared bitwise with "base".
   step : the C3 training step (B=8, the 5 buckets round-robin, fused optimizer), ms per step medians.
+  swb  : the SwiGLU-backward dgrad (dY . W3 with the SwiGLU backward in the epilogue) at the C3 shape (M = 33360,
+         F = 2048, D = 768), per-launch medians; dx12 compared bitwise with the first variant.
 
   python tools/lib_ab.py --variants base,noslp [--what attn,step] [--rounds 6]
 """
@@ -131,6 +133,49 @@ def main():
         out["attn"] = {"bitwise_equal_to_first": eq, "fwd_vs_fp32": err, "median_ms": med,
                        "ratio_to_first": {k: round(v / med[k.split("_")[0] + "_" + names[0]], 4) for k, v in med.items()}}
         print(json.dumps(out["attn"]), flush=True)
+    if "swb" in what:
+        M, D, F = 8 * 4170, 768, 2048
+        g = torch.Generator(device=dev).manual_seed(1)
+        dy = torch.randn(M, D, device=dev, generator=g).bfloat16()
+        w3 = (torch.randn(D, F, device=dev, generator=g) * 0.05).bfloat16()
+        x12 = torch.randn(M, 2 * F, device=dev, generator=g).bfloat16()
+        dx12 = torch.empty(M, 2 * F, dtype=torch.bfloat16, device=dev)
+        ws = torch.empty(M, F, dtype=torch.bfloat16, device=dev)
+        # a 512-MB sweep between launches evicts L2 / MALL as the step's other kernels do
+        flush = torch.empty(128 << 20, dtype=torch.float32, device=dev)
+
+        def swb():
+            flush.zero_()
+            ops.linear_dgrad_swiglu(dy, w3, x12, dx12, workspace=ws)
+
+        ref, eq = None, {}
+        for nm in names:
+            _lib.use_library(libs[nm])
+            swb()
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = dx12.clone()
+            eq[nm] = torch.equal(ref, dx12)
+        tm = {nm: [] for nm in names}
+        for r in range(args.rounds):
+            order = names if r % 2 == 0 else names[::-1]
+            for nm in order:
+                _lib.use_library(libs[nm])
+                st = torch.cuda.current_stream()
+                ts = []
+                for _ in range(args.iters):
+                    flush.zero_()
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record(st)
+                    ops.linear_dgrad_swiglu(dy, w3, x12, dx12, workspace=ws)
+                    b.record(st)
+                    ts.append((a, b))
+                torch.cuda.synchronize()
+                tm[nm].append(statistics.median(x.elapsed_time(y) for x, y in ts))
+        med = {nm: round(statistics.median(v) * 1e3, 2) for nm, v in tm.items()}
+        out["swb"] = {"bitwise_equal_to_first": eq, "median_us": med,
+                      "ratio_to_first": {nm: round(v / med[names[0]], 4) for nm, v in med.items()}}
+        print(json.dumps(out["swb"]), flush=True)
     if "step" in what:
         import bench
         from vpt.config import JiT_B_16_Config, JiTTrainingConfig

@@ -1531,6 +1531,376 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs g, int nkb, i
     else dq_body<DQ, 4, NST>(g, bx, r % g.H, r / g.H, lds, kbl, &lstat[0][0][0]);
   }
 }
+// ------------------------------------------------------------------ backward, persistent work queue
+// The same dK/dV and dQ items as attn_bwd_kernel<16, 17> (16x16x32 bodies, the dK/dV body explicitly ordered: the same
+// products in the same order, so the results are bitwise those of the one-launch grid), run by a resident grid (two
+// blocks per CU) that pulls items from per-XCD queues instead of one block per item:
+//  - queue x holds the items xcd_remap deals to XCD x (a contiguous range of dK/dV items, then one of dQ items), so a
+//    (batch, head)'s Q / dO (or K / V) stays in that XCD's L2 as before; a block reads its XCD from HW_REG_XCC_ID and
+//    pulls from its own queue with one returning atomic add per item (in the item's prologue, beside the fragment
+//    loads), taking from the other XCDs' queues only once its own is empty -- a dynamic fill, unlike the static
+//    persistent walk (r05zzi: +3.0 % at C3, +4.5 % at C2: the tail lost the dispatcher's fill);
+//  - the next item's first K / V (or Q / dO + LSE / delta) tile is DMA'd into the free LDS buffer during the current
+//    item's last tile, so an item starts on staged data; the key-bias array is refilled only when the batch changes;
+//    the per-block launch, first-tile round trip and retirement of the one-launch grid are gone.
+// Queue words (caller's workspace, zero before the first launch): [0, 8) per-XCD tickets, [8] finished blocks. The block
+// that finishes last resets them, so the next launch on the same workspace starts from zero (stream order). Every
+// block ends once all queues are drained: no block ever waits for another.
+constexpr int kPqWords = 16;
+__device__ __forceinline__ int xcc_id() { return (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u); }
+
+struct PqGeom {
+  int nkb, nqb, nkv, nq;  // blocks per head (dK/dV, dQ), items of each kind
+  __device__ __forceinline__ int kv_lo(int x) const { return x * (nkv >> 3) + min(x, nkv & 7); }
+  __device__ __forceinline__ int q_lo(int x) const { return x * (nq >> 3) + min(x, nq & 7); }
+  __device__ __forceinline__ int kv_len(int x) const { return (nkv >> 3) + (x < (nkv & 7)); }
+  __device__ __forceinline__ int q_len(int x) const { return (nq >> 3) + (x < (nq & 7)); }
+  // ticket t of queue x -> item id: [0, nkv) dK/dV logical ids, [nkv, nkv + nq) dQ logical ids + nkv; -1 past the end
+  __device__ __forceinline__ int item(int x, unsigned t) const {
+    const int lk = kv_len(x);
+    if (t < (unsigned)lk) return kv_lo(x) + (int)t;
+    if (t < (unsigned)(lk + q_len(x))) return nkv + q_lo(x) + ((int)t - lk);
+    return -1;
+  }
+};
+
+// One item from the block's own queue, else from the others in turn (-1: all drained). One lane.
+__device__ __forceinline__ int pq_pull(unsigned* qws, const PqGeom& q, int x) {
+#pragma unroll 1
+  for (int i = 0; i < 8; ++i) {
+    const int xq = (x + i) & 7;
+    const int it = q.item(xq, atomicAdd(qws + xq, 1u));
+    if (it >= 0) return it;
+  }
+  return -1;
+}
+
+// Tile 0 of item `it` into LDS buffer `buf` (dK/dV: Q / dO rows and the LSE / delta rows; dQ: K / V rows).
+// threadIdx.x hidden from the optimiser per call: the lane-dependent DMA offsets and fragment addresses of an item are
+// then recomputed in each item instead of being hoisted out of the item loop, kept live across every item (spilled)
+__device__ __forceinline__ int pq_opaque_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
+template <int NW>
+__device__ __forceinline__ void pq_stage0(const AttnArgs& g, const PqGeom& q, int it, uint32_t lb, int buf,
+                                          float (&lstat)[2][2][64], int wid, int lane) {
+  lane = pq_opaque_tid() & 63;
+  const bool kv = it < q.nkv;
+  const int id = kv ? it : it - q.nkv;
+  const int r = kv ? id / q.nkb : id / q.nqb, hd = r % g.H, b = r / g.H;
+  if (kv) {
+    dma_rows_at<NW, 1>(lb + buf * 16384, uniform_ptr(g.q.p + b * g.q.sb + hd * g.q.sh), g.q.sr, 0, g.n,
+                       row_plan<NW, 1>(g.q.sr, wid, lane), wid, lane);
+    dma_rows_at<NW, 1>(lb + buf * 16384 + 8192, uniform_ptr(g.dO.p + b * g.dO.sb + hd * g.dO.sh), g.dO.sr, 0, g.n,
+                       row_plan<NW, 1>(g.dO.sr, wid, lane), wid, lane);
+    if (wid == 0) dma_stat(lstat[buf][0], uniform_ptr(g.lse + b * g.l_sb + hd * g.l_sh), 0, g.n, lane);
+    else if (wid == 1) dma_stat(lstat[buf][1], uniform_ptr(g.delta_in + b * g.l_sb + hd * g.l_sh), 0, g.n, lane);
+  } else {
+    dma_rows_at<NW, 1>(lb + buf * 16384, uniform_ptr(g.k.p + b * g.k.sb + hd * g.k.sh), g.k.sr, 0, g.nk,
+                       row_plan<NW, 1>(g.k.sr, wid, lane), wid, lane);
+    dma_rows_at<NW, 1>(lb + buf * 16384 + 8192, uniform_ptr(g.v.p + b * g.v.sb + hd * g.v.sh), g.v.sr, 0, g.nk,
+                       row_plan<NW, 1>(g.v.sr, wid, lane), wid, lane);
+  }
+}
+
+// Prologue shared by both item kinds, after the item's fragment loads were issued: every wave waits for its loads and
+// tile-0 pieces; lane 0 publishes the next item into `slot` -- its ticket `pend` was taken one item earlier, so the
+// atomic's round trip ran under that item (own queue drained: the others are tried in turn, at the tail only) -- and
+// then takes the ticket after it, which returns while this item runs (only an explicit vmcnt(0) later waits for it,
+// at this item's first tile). The barrier publishes the slot. Returns the next item (-1: none).
+__device__ __forceinline__ int pq_prologue(unsigned* qws, const PqGeom& q, int x, volatile int* slot, unsigned& pend) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (threadIdx.x == 0) {
+    int it = q.item(x, pend);
+    if (it < 0) it = pq_pull(qws, q, x);
+    *slot = it;
+    pend = atomicAdd(qws + x, 1u);
+  }
+  __syncthreads();
+  return __builtin_amdgcn_readfirstlane(*slot);  // the same in every lane: uniform for the compiler too
+}
+
+// dkdv16_body<NW, true> as a queue item: tile 0 staged (possibly still in flight) in buffer p0; the next item's tile 0
+// is staged into the free buffer during this item's last tile. Returns the buffer of the next tile 0; *next = item.
+template <int NW>
+__device__ __forceinline__ int pq_dkdv(const AttnArgs& g, const PqGeom& q, int bx, int hd, int b, int p0,
+                                       char (&lds)[2][2][8192], float (&lstat)[2][2][64], unsigned* qws, int x,
+                                       volatile int* slot, unsigned& pend, int& next) {
+  const int tid = pq_opaque_tid(), lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6), G = lane >> 4;
+  const int k0 = bx * (32 * NW) + wid * 32;
+  bf16x8 kf[2][2], vf[2][2];
+  bool kmasked[2];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int key = k0 + 16 * kt + (lane & 15);
+    load_row_frags16(kf[kt], g.k.p + b * g.k.sb + hd * g.k.sh, g.k.sr, key, g.nk, lane);
+    load_row_frags16(vf[kt], g.v.p + b * g.v.sb + hd * g.v.sh, g.v.sr, key, g.nk, lane);
+    kmasked[kt] = key_bias(g, b, key) == kNegInf;
+  }
+  const int nxt = pq_prologue(qws, q, x, slot, pend);
+  next = nxt;
+  if (g.n < 64) {  // padding query rows of the (only) tile zeroed
+    zero_rows<NW>(lds[p0][0], g.n, tid);
+    zero_rows<NW>(lds[p0][1], g.n, tid);
+    __syncthreads();
+  }
+  floatx4 dv[2][4], dk[2][4];  // [kt][dt]
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { dv[kt][dt][e] = 0.f; dk[kt][dt][e] = 0.f; }
+  const int nt = (g.n + 63) / 64;
+  const void* Qu = uniform_ptr(g.q.p + b * g.q.sb + hd * g.q.sh);
+  const void* Du = uniform_ptr(g.dO.p + b * g.dO.sb + hd * g.dO.sh);
+  const void* Lu = uniform_ptr(g.lse + b * g.l_sb + hd * g.l_sh);
+  const void* Eu = uniform_ptr(g.delta_in + b * g.l_sb + hd * g.l_sh);
+  const uint32_t lb = lds_addr(&lds[0][0][0]);
+  const RowPlan<NW> pq = row_plan<NW, 1>(g.q.sr, wid, lane), pd0 = row_plan<NW, 1>(g.dO.sr, wid, lane);
+  for (int t = 0; t < nt; ++t) {
+    const int cur = (t + p0) & 1;
+    const bool more = t + 1 < nt;
+    if (more) {
+      dma_rows_at<NW, 1>(lb + (cur ^ 1) * 16384, Qu, g.q.sr, (t + 1) * 64, g.n, pq, wid, lane);
+      dma_rows_at<NW, 1>(lb + (cur ^ 1) * 16384 + 8192, Du, g.dO.sr, (t + 1) * 64, g.n, pd0, wid, lane);
+      if (wid == 0) dma_stat(lstat[cur ^ 1][0], Lu, (t + 1) * 64, g.n, lane);
+      else if (wid == 1) dma_stat(lstat[cur ^ 1][1], Eu, (t + 1) * 64, g.n, lane);
+    } else if (nxt >= 0) {
+      pq_stage0<NW>(g, q, nxt, lb, cur ^ 1, lstat, wid, lane);
+    }
+    const char* lq = lds[cur][0];
+    const char* ld = lds[cur][1];
+    bf16x8 qa[2][2], da[2][2], pp[2][2], pd[2][2];  // qa / da [u][ks]; pp / pd [m][kt]
+    auto rd = [&](int m) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          qa[u][ks] = frag16_rows(lq, 32 * m + 16 * u, ks, lane);
+          da[u][ks] = frag16_rows(ld, 32 * m + 16 * u, ks, lane);
+        }
+    };
+    rd(0);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      floatx4 s[2][2], dp[2][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const floatx4 cs = *reinterpret_cast<const floatx4*>(&lstat[cur][0][32 * m + 16 * u + 4 * G]);
+        const floatx4 cd = *reinterpret_cast<const floatx4*>(&lstat[cur][1][32 * m + 16 * u + 4 * G]);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) { s[u][kt] = cs; dp[u][kt] = cd; }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            s[u][kt] = mfma16(qa[u][ks], kf[kt][ks], s[u][kt]);
+            dp[u][kt] = mfma16(da[u][ks], vf[kt][ks], dp[u][kt]);
+          }
+      if (m == 0) rd(1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        floatx4 P[2], dS[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float p = __builtin_amdgcn_exp2f(s[u][kt][e]);
+            P[u][e] = p;
+            dS[u][e] = p * dp[u][kt][e];
+          }
+        pp[m][kt] = pack16(P[0], P[1]);
+        pd[m][kt] = pack16(dS[0], dS[1]);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 tv = frag16_tr(ld, dt, m, lane);
+        const bf16x8 tq = frag16_tr(lq, dt, m, lane);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          dv[kt][dt] = mfma16(tv, pp[m][kt], dv[kt][dt]);
+          dk[kt][dt] = mfma16(tq, pd[m][kt], dk[kt][dt]);
+        }
+      }
+    if (more) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int r1 = (t + 1) * 64;
+      if (g.n - r1 < 64) {  // padding query rows zeroed: no dK / dV contribution
+        zero_rows<NW>(lds[cur ^ 1][0], g.n - r1, tid);
+        zero_rows<NW>(lds[cur ^ 1][1], g.n - r1, tid);
+        __syncthreads();
+      }
+    }
+  }
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int key = k0 + 16 * kt + (lane & 15);
+    store16_T(g.dv, (long)b * g.dv.sb + hd * g.dv.sh, dv[kt], 1.f, key, g.nk, lane, kmasked[kt]);
+    store16_T(g.dk, (long)b * g.dk.sb + hd * g.dk.sh, dk[kt], 0.69314718055994531f, key, g.nk, lane, kmasked[kt]);
+  }
+  return (nt + p0) & 1;
+}
+
+// dq16_body<NW> as a queue item (see pq_dkdv); kbl_b = the batch whose key biases kbl holds (-1: none yet).
+template <int NW>
+__device__ __forceinline__ int pq_dq(const AttnArgs& g, const PqGeom& q, int bx, int hd, int b, int p0,
+                                     char (&lds)[2][2][8192], float (&lstat)[2][2][64], float* kbl, int& kbl_b,
+                                     unsigned* qws, int x, volatile int* slot, unsigned& pend, int& next) {
+  const int tid = pq_opaque_tid(), lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6), G = lane >> 4;
+  const int q0 = bx * (32 * NW) + wid * 32;
+  bf16x8 qf[2][2], df[2][2];
+  float nlse[2], ndel[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qrow = q0 + 16 * qt + (lane & 15);
+    load_row_frags16(qf[qt], g.q.p + b * g.q.sb + hd * g.q.sh, g.q.sr, qrow, g.n, lane);
+    load_row_frags16(df[qt], g.dO.p + b * g.dO.sb + hd * g.dO.sh, g.dO.sr, qrow, g.n, lane);
+    const long lo = b * g.l_sb + hd * g.l_sh + qrow;
+    nlse[qt] = qrow < g.n ? g.lse[lo] : -__builtin_huge_valf();
+    ndel[qt] = qrow < g.n ? g.delta_in[lo] : 0.f;
+  }
+  if (b != kbl_b) {  // the previous item's last reads of kbl were before its last barrier
+    fill_key_bias<NW>(kbl, g, b, tid);
+    kbl_b = b;
+  }
+  const int nxt = pq_prologue(qws, q, x, slot, pend);
+  next = nxt;
+  floatx4 dq[2][4];  // [qt][dt]
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dq[qt][dt][e] = 0.f;
+  const int nt = (g.nk + 63) / 64;
+  const void* Ku = uniform_ptr(g.k.p + b * g.k.sb + hd * g.k.sh);
+  const void* Vu = uniform_ptr(g.v.p + b * g.v.sb + hd * g.v.sh);
+  const uint32_t lb = lds_addr(&lds[0][0][0]);
+  const RowPlan<NW> pk = row_plan<NW, 1>(g.k.sr, wid, lane), pv = row_plan<NW, 1>(g.v.sr, wid, lane);
+  for (int t = 0; t < nt; ++t) {
+    const int kv0 = t * 64;
+    const int cur = (t + p0) & 1;
+    if (t + 1 < nt) {
+      dma_rows_at<NW, 1>(lb + (cur ^ 1) * 16384, Ku, g.k.sr, kv0 + 64, g.nk, pk, wid, lane);
+      dma_rows_at<NW, 1>(lb + (cur ^ 1) * 16384 + 8192, Vu, g.v.sr, kv0 + 64, g.nk, pv, wid, lane);
+    } else if (nxt >= 0) {
+      pq_stage0<NW>(g, q, nxt, lb, cur ^ 1, lstat, wid, lane);
+    }
+    const char* lk = lds[cur][0];
+    const char* lv = lds[cur][1];
+    const bool dense = kv0 + 64 <= g.n_dense;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      floatx4 s[2][2], dp[2][2];  // [u][qt]: key rows 32m + 16u + 4G + e, query 16qt + (lane & 15)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { s[u][qt][e] = nlse[qt]; dp[u][qt][e] = ndel[qt]; }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 ka = frag16_rows(lk, 32 * m + 16 * u, ks, lane);
+          const bf16x8 va = frag16_rows(lv, 32 * m + 16 * u, ks, lane);
+#pragma unroll
+          for (int qt = 0; qt < 2; ++qt) {
+            s[u][qt] = mfma16(ka, qf[qt][ks], s[u][qt]);
+            dp[u][qt] = mfma16(va, df[qt][ks], dp[u][qt]);
+          }
+        }
+        if (!dense) {  // scalar branch: only the context / padding key tiles carry a bias
+          const floatx4 bias = *reinterpret_cast<const floatx4*>(&kbl[kv0 - g.kb0 + 32 * m + 16 * u + 4 * G]);
+#pragma unroll
+          for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s[u][qt][e] += bias[e];
+        }
+      }
+      bf16x8 pd[2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        floatx4 dS[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dS[u][e] = __builtin_amdgcn_exp2f(s[u][qt][e]) * dp[u][qt][e];
+        pd[qt] = pack16(dS[0], dS[1]);
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 tk = frag16_tr(lk, dt, m, lane);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) dq[qt][dt] = mfma16(tk, pd[qt], dq[qt][dt]);
+      }
+    }
+    if (t + 1 < nt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+    store16_T(g.dq, (long)b * g.dq.sb + hd * g.dq.sh, dq[qt], g.scale, q0 + 16 * qt + (lane & 15), g.n, lane, false);
+  return (nt + p0) & 1;
+}
+
+__global__ __launch_bounds__(256, 2) void attn_bwd_pq_kernel(AttnArgs g, int nkb, int nqb, int B, unsigned* qws) {
+  constexpr int NW = 4;
+  __shared__ __attribute__((aligned(16))) char lds[2][2][8192];
+  __shared__ __attribute__((aligned(16))) float lstat[2][2][64];
+  __shared__ int s_item[2];
+  extern __shared__ __attribute__((aligned(16))) float kbl[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  PqGeom q;
+  q.nkb = nkb;
+  q.nqb = nqb;
+  q.nkv = nkb * g.H * B;
+  q.nq = nqb * g.H * B;
+  const int x = xcc_id();
+  volatile int* slots = s_item;
+  unsigned pend = 0;  // lane 0: the ticket of the item after the current one (pq_prologue)
+  if (tid == 0) {
+    slots[0] = pq_pull(qws, q, x);
+    pend = atomicAdd(qws + x, 1u);
+  }
+  __syncthreads();
+  int it = __builtin_amdgcn_readfirstlane(slots[0]);
+  int buf = 0, kbl_b = -1;
+  if (it >= 0) pq_stage0<NW>(g, q, it, lds_addr(&lds[0][0][0]), 0, lstat, wid, lane);
+  // item n's prologue writes slot (n + 1) & 1 (a wave can reach the next item's prologue before a slower wave has
+  // passed this one's barrier, never two items ahead: every item has a barrier)
+  for (int n = 0; it >= 0; ++n) {
+    const bool kv = it < q.nkv;
+    const int id = kv ? it : it - q.nkv;
+    const int r = kv ? id / nkb : id / nqb;
+    const int bx = kv ? id - r * nkb : id - r * nqb;
+    int next;
+    if (kv) buf = pq_dkdv<NW>(g, q, bx, r % g.H, r / g.H, buf, lds, lstat, qws, x, slots + ((n + 1) & 1), pend, next);
+    else buf = pq_dq<NW>(g, q, bx, r % g.H, r / g.H, buf, lds, lstat, kbl, kbl_b, qws, x, slots + ((n + 1) & 1), pend,
+                         next);
+    it = next;
+  }
+  // queue reset by the block that finishes last (every block has taken its last, failing tickets before it counts)
+  if (tid == 0 && atomicAdd(qws + 8, 1u) == gridDim.x - 1) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) atomicExch(qws + i, 0u);
+  }
+}
+
 constexpr int kDqBody = 0;  // production dQ body (0 = compiler-scheduled, 8 = explicitly ordered)
 // production dK/dV body: the explicitly ordered body without s_setprio around its MFMA groups (10); with them (8) the
 // other wave on the SIMD waits out each prioritised MFMA group before its exp / pack phase can issue: kernel -1.1 %,
@@ -1647,6 +2017,7 @@ extern "C" int vpt_attn_fwd_qknorm(const void* q, long q_sb, long q_sh, long q_s
 
 namespace {
 int attn_bwd_impl(AttnArgs& g, int B, int H, int n, int nk, hipStream_t s);
+int attn_bwd_pq_impl(AttnArgs& g, int B, int H, int n, int nk, unsigned* qws, hipStream_t s);
 }
 
 extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
@@ -1685,6 +2056,45 @@ extern "C" int vpt_attn_bwd(const void* q, long q_sb, long q_sh, long q_sr,
 #endif
   return attn_bwd_impl(g, B, H, n, nk, (hipStream_t)stream);
 }
+
+// vpt_attn_bwd on the persistent work-queue kernel (bitwise the same results): `queue` = 64 bytes of device memory owned
+// by the caller, zero before its first use and left zero by every launch; one per stream that may run this concurrently.
+extern "C" int vpt_attn_bwd_q(const void* q, long q_sb, long q_sh, long q_sr,
+                              const void* k, long k_sb, long k_sh, long k_sr,
+                              const void* v, long v_sb, long v_sh, long v_sr,
+                              const void* o, long o_sb, long o_sh, long o_sr,
+                              const void* dO, long do_sb, long do_sh, long do_sr,
+                              const float* lse, float* delta, long l_sb, long l_sh,
+                              const float* kbias, long kb_sb,
+                              void* dq, long dq_sb, long dq_sh, long dq_sr,
+                              void* dk, long dk_sb, long dk_sh, long dk_sr,
+                              void* dv, long dv_sb, long dv_sh, long dv_sr,
+                              int B, int H, int n, int nk, int n_dense, float scale, void* queue, void* stream) {
+  int rc = check_common(B, H, n, nk);
+  if (rc) return rc;
+  VPT_CHECK_ARG(q && k && v && o && dO && lse && delta && dq && dk && dv && queue, "vpt_attn_bwd_q: null pointer");
+  VPT_CHECK_ARG(((uintptr_t)queue & 63) == 0, "vpt_attn_bwd_q: queue must be 64-byte aligned");
+  AttnArgs g = {};
+  g.xcd = 1;
+  g.q = {(const bf16_t*)q, q_sb, q_sh, q_sr};
+  g.k = {(const bf16_t*)k, k_sb, k_sh, k_sr};
+  g.v = {(const bf16_t*)v, v_sb, v_sh, v_sr};
+  g.o = {(bf16_t*)o, o_sb, o_sh, o_sr};
+  g.dO = {(const bf16_t*)dO, do_sb, do_sh, do_sr};
+  g.dq = {(bf16_t*)dq, dq_sb, dq_sh, dq_sr};
+  g.dk = {(bf16_t*)dk, dk_sb, dk_sh, dk_sr};
+  g.dv = {(bf16_t*)dv, dv_sb, dv_sh, dv_sr};
+  g.lse = (float*)lse; g.delta_in = delta; g.delta_out = delta; g.l_sb = l_sb; g.l_sh = l_sh;
+  g.kbias = kbias; g.kb_sb = kb_sb;
+  g.n = n; g.nk = nk; g.n_dense = n_dense < nk ? n_dense : nk;
+  g.scale = scale; g.scale_log2 = scale * 1.4426950408889634f;
+  g.kb0 = g.n_dense / 64 * 64;
+  g.nq_pad = (n + 63) / 64 * 64;
+  g.H = H;
+  return attn_bwd_pq_impl(g, B, H, n, nk, (unsigned*)queue, (hipStream_t)stream);
+}
+
+extern "C" int vpt_attn_bwd_queue_bytes(void) { return kPqWords * 4; }
 
 // Rows of the per-workgroup weight-gradient partials vpt_attn_bwd_qknorm writes for n rows (q: n = query rows,
 // k: n = key rows): one 64-float row per 128-row block of every (batch, head).
@@ -1826,6 +2236,26 @@ int attn_bwd_impl(AttnArgs& g, int B, int H, int n, int nk, hipStream_t s) {
   else  // the fused QK-norm epilogue reads the 32x32x16 accumulator layout
     hipLaunchKernelGGL((attn_bwd_kernel<kDqBody, kDkdvBody>), dim3((nkb + nqb) * H * B), dim3(256), key_bias_lds_bytes(g),
                        s, g, nkb, nqb, B);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
+// The persistent-queue backward (attn_bwd_pq_kernel): delta pre-pass, then two resident blocks per CU.
+int attn_bwd_pq_impl(AttnArgs& g, int B, int H, int n, int nk, unsigned* qws, hipStream_t s) {
+  const long rows = (long)B * H * n;
+  g.dqacc = nullptr;
+  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, s, g, H, rows);
+  VPT_LAUNCH_CHECK();
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (cus[dev] == 0) {
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    cus[dev] = c;
+  }
+  const int nkb = (nk + 127) / 128, nqb = (n + 127) / 128;
+  hipLaunchKernelGGL(attn_bwd_pq_kernel, dim3(2 * cus[dev]), dim3(256), key_bias_lds_bytes(g), s, g, nkb, nqb, B, qws);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

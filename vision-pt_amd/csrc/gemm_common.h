@@ -452,6 +452,28 @@ __device__ __forceinline__ EpiAddr epi_addr(const GemmArgs& g, const RingItem& i
 // EPI_SWB1: the SwiGLU-backward epilogue with its x12 operands loaded one group at a time (the form before the
 // one-group-ahead preload; diagnostic build only, A/B)
 enum { EPI_PLAIN = 0, EPI_RESID = 1, EPI_SWB = 2, EPI_ACC = 3, EPI_QKN = 4, EPI_SWB1 = 5 };
+// Cache policy (buffer instruction aux bits) of the SwiGLU-backward epilogue's x12 loads and dx12 stores: both streams
+// are touched once (270 MB each at C3), while the GEMM's B operand (W3, 3 MB) is re-read by every row tile of an XCD.
+// nt (2) on the x12 loads, sc1 (16: the line leaves the XCD's L2) on the dx12 stores. In-process A/B at the C3 shape
+// (tools/lib_ab.py swb, r06b; L2 / MALL flushed between launches, bitwise equal): 218.4 us default policy, 196.0 nt
+// loads, 216.4 sc1 stores, 194.0 both. Compile-time knobs for such A/B builds.
+#ifndef VPT_SWB_LD_AUX
+#define VPT_SWB_LD_AUX 2
+#endif
+#ifndef VPT_SWB_ST_AUX
+#define VPT_SWB_ST_AUX 16
+#endif
+// The same knobs for the residual epilogue's loads, the SwiGLU forward's x12 / h stores and the plain bf16 stores
+// (A/B builds; default policy unless measured otherwise)
+#ifndef VPT_RESID_LD_AUX
+#define VPT_RESID_LD_AUX 0
+#endif
+#ifndef VPT_SWF_ST_AUX
+#define VPT_SWF_ST_AUX 0
+#endif
+#ifndef VPT_EPI_ST_AUX
+#define VPT_EPI_ST_AUX 0
+#endif
 __host__ __device__ constexpr bool epi_swb(int e) { return e == EPI_SWB || e == EPI_SWB1; }
 __host__ __device__ constexpr int epi_frags(int epi) {  // fragments per preload group (0: no loads)
   return epi == EPI_RESID ? 4 : (epi_swb(epi) || epi == EPI_ACC) ? 2 : 0;
@@ -470,9 +492,9 @@ __device__ __forceinline__ void epi_preload(const GemmArgs& g, const EpiAddr& e,
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         const int so = ((I0 + i) * 16 + p * 8) * e.rastride;
-        pre.v[4 * i + 2 * p] = __builtin_amdgcn_raw_buffer_load_b128(e.ra, (int)e.avoff, so, 0);
-        pre.v[4 * i + 2 * p + 1] =
-            __builtin_amdgcn_raw_buffer_load_b128(e.ra, (int)(e.col_ok ? e.avoff + g.N * 2 : e.avoff), so, 0);
+        pre.v[4 * i + 2 * p] = __builtin_amdgcn_raw_buffer_load_b128(e.ra, (int)e.avoff, so, VPT_SWB_LD_AUX);
+        pre.v[4 * i + 2 * p + 1] = __builtin_amdgcn_raw_buffer_load_b128(
+            e.ra, (int)(e.col_ok ? e.avoff + g.N * 2 : e.avoff), so, VPT_SWB_LD_AUX);
       }
   } else if (EPI == EPI_ACC) {
 #pragma unroll
@@ -489,7 +511,8 @@ __device__ __forceinline__ void epi_preload(const GemmArgs& g, const EpiAddr& e,
 #pragma unroll
       for (int p = 0; p < 2; ++p)
         pre.v[2 * i + p] =
-            __builtin_amdgcn_raw_buffer_load_b128(e.rr, (int)e.rvoff, ((I0 + i) * 16 + p * 8) * e.rrstride, 0);
+            __builtin_amdgcn_raw_buffer_load_b128(e.rr, (int)e.rvoff, ((I0 + i) * 16 + p * 8) * e.rrstride,
+                                                  VPT_RESID_LD_AUX);
   }
 }
 
@@ -514,8 +537,9 @@ __device__ __forceinline__ int stg_off(int row, int col) {
 // after issue, and hipcc (ROCm 7.2, gfx950) emitted the SwiGLU-backward epilogue's first store followed
 // directly by a VALU write of its data registers, with no wait state -- the stored dwords came out corrupted.
 // The scheduling barrier pins the pad right behind the store (tools/isa_store_hazard.py checks the .s).
+template <int AUX = 0>
 __device__ __forceinline__ void store_b128_padded(u32x4 v, __amdgpu_buffer_rsrc_t rs, int voff, int soff) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, AUX);
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 1");
   __builtin_amdgcn_sched_barrier(0);
@@ -558,8 +582,9 @@ __device__ __forceinline__ void epilogue_ring(const GemmArgs& g, const floatx4 (
 #pragma unroll
         for (int q = 0; q < 8; ++q) swiglu_bwd1(bf2f(f2bf(o[q])), a[q], b[q], d1[q], d2[q]);  // dh: a bf16 tensor
         const uint4 w1 = pack8(d1), w2 = pack8(d2);
-        store_b128_padded(u32x4{w1.x, w1.y, w1.z, w1.w}, e.rs, (int)e.voff, soff);
-        store_b128_padded(u32x4{w2.x, w2.y, w2.z, w2.w}, e.rs, (int)(e.col_ok ? e.voff + g.N * 2 : e.voff), soff);
+        store_b128_padded<VPT_SWB_ST_AUX>(u32x4{w1.x, w1.y, w1.z, w1.w}, e.rs, (int)e.voff, soff);
+        store_b128_padded<VPT_SWB_ST_AUX>(u32x4{w2.x, w2.y, w2.z, w2.w}, e.rs,
+                                          (int)(e.col_ok ? e.voff + g.N * 2 : e.voff), soff);
       } else if (g.out_mode == OUT_BF16) {
         if (EPI == EPI_RESID) {
           // reference semantics: residual + bf16(linear output), rounded again to bf16. Out-of-range rows /
@@ -572,7 +597,7 @@ __device__ __forceinline__ void epilogue_ring(const GemmArgs& g, const floatx4 (
         }
         const uint4 w = pack8(o);
         if (NOST) asm volatile("" :: "v"(w.x), "v"(w.y), "v"(w.z), "v"(w.w));  // timing ablation: no store
-        else store_b128_padded(u32x4{w.x, w.y, w.z, w.w}, e.rs, (int)e.voff, soff);
+        else store_b128_padded<VPT_EPI_ST_AUX>(u32x4{w.x, w.y, w.z, w.w}, e.rs, (int)e.voff, soff);
       } else {
         if (EPI == EPI_ACC) {
           const u32x4 a0 = pre.v[4 * il + 2 * p], a1 = pre.v[4 * il + 2 * p + 1];
@@ -714,9 +739,9 @@ __device__ __forceinline__ void epilogue_ring_swf(const GemmArgs& g, const float
     }
     const int soff = i * 16 * (int)g.ldc * 2, soffh = i * 16 * (int)g.ldc2 * 2;
     const uint4 w1 = pack8(x1), w2 = pack8(x2), wh = pack8(hv);
-    store_b128_padded(u32x4{w1.x, w1.y, w1.z, w1.w}, rs, (int)vx, soff);
-    store_b128_padded(u32x4{w2.x, w2.y, w2.z, w2.w}, rs, (int)(vx + F * 2), soff);
-    store_b128_padded(u32x4{wh.x, wh.y, wh.z, wh.w}, rh, (int)vh, soffh);
+    store_b128_padded<VPT_SWF_ST_AUX>(u32x4{w1.x, w1.y, w1.z, w1.w}, rs, (int)vx, soff);
+    store_b128_padded<VPT_SWF_ST_AUX>(u32x4{w2.x, w2.y, w2.z, w2.w}, rs, (int)(vx + F * 2), soff);
+    store_b128_padded<VPT_SWF_ST_AUX>(u32x4{wh.x, wh.y, wh.z, wh.w}, rh, (int)vh, soffh);
   }
 }
 

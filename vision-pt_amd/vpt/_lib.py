@@ -34,6 +34,9 @@ SIGNATURES: dict[str, list] = {
     "vpt_attn_fwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, P, L, I, I, I, I, I, F, P],
     "vpt_attn_bwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, P, L, L, P, L,
                      P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, I, F, P],
+    "vpt_attn_bwd_q": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, P, L, L, P, L,
+                       P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, I, F, P, P],
+    "vpt_attn_bwd_queue_bytes": [],
     "vpt_attn_bwd_qknorm": [P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, P, L, L, P, L,
                             P, P, L, L, L, P, P, P, P, F, P, P, L, L, L, P, P, L, P, L, L, L, I, I, I, I, I, F, P],
     "vpt_attn_bwd_dw_rows": [I, I, I],
@@ -156,7 +159,7 @@ _RESTYPES = {
     "vpt_build_info": C.c_char_p,
 }
 # Entry points that return a value (size / count / string) rather than a status code.
-_VALUE_FNS = {"vpt_grad_norm_blocks", "vpt_velocity_loss_blocks", "vpt_lora_wgrad_workspace", "vpt_lora_wgrad_splits", "vpt_gemm_workspace_bytes", "vpt_linear_wgrad_workspace_bytes", "vpt_attn_fused_workspace_bytes", "vpt_cover_resize_crop_workspace", "vpt_gemm_swiglu_bwd_workspace", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
+_VALUE_FNS = {"vpt_attn_bwd_queue_bytes", "vpt_grad_norm_blocks", "vpt_velocity_loss_blocks", "vpt_lora_wgrad_workspace", "vpt_lora_wgrad_splits", "vpt_gemm_workspace_bytes", "vpt_linear_wgrad_workspace_bytes", "vpt_attn_fused_workspace_bytes", "vpt_cover_resize_crop_workspace", "vpt_gemm_swiglu_bwd_workspace", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
               "vpt_colsum_blocks", "vpt_attn_q_scale", "vpt_attn_bwd_dw_rows", "vpt_last_error_string", "vpt_abi_version", "vpt_build_info"}
 
 

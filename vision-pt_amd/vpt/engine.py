@@ -68,6 +68,14 @@ MICRO_SPLIT_MIN_ROWS = 8192
 # lanes' extra hand-offs cost more than they fill), so the backward runs one lane by default.
 MICRO_SPLIT_FWD = True
 MICRO_SPLIT_BWD = False
+# The attention backward on the persistent work-queue kernel (vpt_attn_bwd_q: resident blocks pulling dK/dV and dQ items
+# from per-XCD queues, the next item's first tile staged under the current item's last; bitwise the one-launch grid).
+# Measured slower (tools/attn_queue_ab.py, r06b / r06c, same box, interleaved): C3 1.371 vs 1.348 ms (+1.7 %), C2 0.267 vs
+# 0.232 ms (+15 %) with the ticket pulled in the item's prologue; +3.9 % / +20 % with it taken one item ahead (its return
+# then waited at the first tile's vmcnt(0)); C3 step -0.54 % (r06b). Each item still pays a vmcnt(0) on the previous
+# item's epilogue stores (vector-memory counters retire in issue order) and the atomic's round trip, which the
+# dispatcher's block launch does not. Off.
+ATTN_BWD_QUEUE = False
 # Gradient checkpointing's per-block recompute in the backward as forward lanes too (while the backward itself runs one
 # lane); A/B knob
 MICRO_SPLIT_RECOMPUTE = True
@@ -616,7 +624,8 @@ class JiTEngine:
                                      ops._t4(qkvh, Bh, rows, Hh, 2 * D), ops._t4(rs(o, hh), Bh, rows, Hh, 0),
                                      ops._t4(rs(d_o, hh), Bh, rows, Hh, 0), bs(lse, hh), bs(delta, hh), bs(kbias, hh),
                                      ops._t4(dqkh, Bh, rows, Hh, 0), ops._t4(dqkh, Bh, rows, Hh, D),
-                                     ops._t4(dqkvh, Bh, rows, Hh, 2 * D), Bh, Hh, rows, n_i, n_pre, scale)
+                                     ops._t4(dqkvh, Bh, rows, Hh, 2 * D), Bh, Hh, rows, n_i, n_pre, scale,
+                                     queue=ATTN_BWD_QUEUE)
                         # rows >= n_i (a pre-context block's context rows): zero q | k | v gradients, dqk not read there
                         ops.qknorm_rope_bwd(dqkh, qkvh, w["pqk_norm"][:64], w["pqk_norm"][64:], cos_t, sin_t, rows,
                                             dqkvh, dw_part=qkp[hh * nq_h:(hh + 1) * nq_h], n_valid=n_i)

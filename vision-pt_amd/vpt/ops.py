@@ -529,10 +529,34 @@ def attn_fwd_qknorm(q, k, v, o, lse, kbias, wq, wk, B, H, rows, n, n_dense, scal
     return pr.record(4.0 * B * H * n * n * 64, run, nbytes=B * H * (2.0 * 64 * 2 * (2 * n) + 4.0 * n))
 
 
-def attn_bwd(q, k, v, o, do, lse, delta, kbias, dq, dk, dv, B, H, rows, n, n_dense, scale=0.125, nk=None):
+_ATTN_QUEUES: dict = {}
+
+
+def attn_queue(device=None) -> torch.Tensor:
+    """The persistent backward's 64-byte work-queue words for the current stream (zeroed once; every launch leaves
+    them zero): one set per stream, since launches on different streams may overlap."""
+    st = torch.cuda.current_stream(device)
+    key = (st.device.index, st.cuda_stream)
+    ws = _ATTN_QUEUES.get(key)
+    if ws is None:
+        ws = torch.zeros(int(_lib.lib.vpt_attn_bwd_queue_bytes()) // 4, dtype=torch.int32, device=st.device)
+        _ATTN_QUEUES[key] = ws
+    return ws
+
+
+def attn_bwd(q, k, v, o, do, lse, delta, kbias, dq, dk, dv, B, H, rows, n, n_dense, scale=0.125, nk=None,
+             queue=False):
+    """queue: the persistent work-queue kernel (vpt_attn_bwd_q, bitwise the same results) instead of one block per
+    item (vpt_attn_bwd)."""
     nk = n if nk is None else nk
+    ws = attn_queue() if queue else None
 
     def run():
+        if ws is not None:
+            call("vpt_attn_bwd_q", *q, *k, *v, *o, *do, lse.data_ptr(), delta.data_ptr(), lse.stride(0),
+                 lse.stride(1), _p(kbias), 0 if kbias is None else kbias.stride(0), *dq, *dk, *dv, B, H, n, nk,
+                 n_dense, scale, ws.data_ptr(), stream())
+            return
         call("vpt_attn_bwd", *q, *k, *v, *o, *do, lse.data_ptr(), delta.data_ptr(), lse.stride(0), lse.stride(1),
              _p(kbias), 0 if kbias is None else kbias.stride(0), *dq, *dk, *dv, B, H, n, nk, n_dense, scale,
              stream())
