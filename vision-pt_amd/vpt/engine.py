@@ -109,55 +109,43 @@ class _Pool:
 
     A storage is allocated (zero-filled: rows a kernel never writes, e.g. a pre-context block's context rows, must stay
     finite) on the first use of a name or when a larger bucket needs it to grow. That may happen on any of the engine's
-    streams (sub-batch lanes, the weight-gradient stream) and is made safe for all of them without a host sync:
-    - the zero fill runs on the allocating stream, and an event recorded after it is waited for (stream-ordered) by
-      every other stream's next get() of that name until the next point where all streams have joined (`joined()`);
+    streams (sub-batch lanes, the weight-gradient stream), and the view it returns may then be handed to kernels on any
+    other of them (a buffer got on the step's stream is written by the lanes), so an allocation is made safe for all of
+    them without a host sync:
+    - the zero fill runs on the allocating stream, and every other engine stream waits (stream-ordered) for an event
+      recorded after it before anything enqueued on it later -- no kernel on any stream can touch the new storage
+      before its fill is complete;
     - a replaced storage is marked used by every engine stream (record_stream), so the caching allocator does not hand
       its memory out again before the work those streams have enqueued so far is done."""
 
     def __init__(self, device, streams=None):
         self.device = device
         self.store: dict[str, torch.Tensor] = {}
-        self._ready: dict[str, tuple] = {}  # name -> (event after the zero fill, allocating stream)
-        self._streams = streams             # callable -> the engine's streams (record_stream on replacement)
+        self._streams = streams  # callable -> the engine's streams
 
     def get(self, name: str, shape, dtype=BF16, zero: bool = False) -> torch.Tensor:
         n = 1
         for s in shape:
             n *= s
         cur = self.store.get(name)
-        cuda = self.device.type == "cuda"
         if cur is None or cur.numel() < n or cur.dtype != dtype:
+            cuda = self.device.type == "cuda"
             if cur is not None and cuda:
                 for st in self._engine_streams():
                     cur.record_stream(st)
             cur = torch.zeros(max(n, 1), dtype=dtype, device=self.device)
             if cuda:
-                ev = torch.cuda.Event()
                 here = torch.cuda.current_stream(self.device)
+                ev = torch.cuda.Event()
                 ev.record(here)
-                self._ready[name] = (ev, here)
+                for st in self._engine_streams():
+                    if st != here:
+                        st.wait_event(ev)
             self.store[name] = cur
-        elif cuda and name in self._ready:
-            ev, src = self._ready[name]
-            here = torch.cuda.current_stream(self.device)
-            if here != src:
-                here.wait_event(ev)
         v = cur[:n].view(*shape)
         if zero:
             v.zero_()
         return v
-
-    def joined(self, streams):
-        """`streams` (and the caller's stream) have just been joined into the caller's stream, and every stream forks
-        from the caller's stream (wait_stream) before it next uses a pooled buffer: the zero fills those streams
-        enqueued are ordered before any later use, so their pending events can go."""
-        keep = {}
-        joined = list(streams) + [torch.cuda.current_stream(self.device)]
-        for name, (ev, src) in self._ready.items():
-            if not any(src == st for st in joined):
-                keep[name] = (ev, src)
-        self._ready = keep
 
     def _engine_streams(self):
         out = [torch.cuda.current_stream(self.device), torch.cuda.default_stream(self.device)]
@@ -333,7 +321,6 @@ class JiTEngine:
         if S > 1:
             for st in subs:
                 main.wait_stream(st)
-            pool.joined(subs)
         # --- final layer + (per-patch) output (denoiser.py:1115-1116, 535-543)
         f = self.fin
         M2 = B * np_
@@ -670,7 +657,6 @@ class JiTEngine:
             # run on the main stream, after every block's weight gradient
             main.wait_stream(side)
             on_side = False
-            pool.joined(list(self._mstreams) + [side])
         # --- embeddings backward
         dpe2 = pool.get("d_pe2", (M2, D))
         dsize = pool.get("d_size", (6 * B, D))
