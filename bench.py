@@ -28,18 +28,19 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "vision-pt_amd"))
 sys.path.insert(0, ROOT)
 
-# HIP hardware queues per process (read at HIP's initialisation, so set before torch loads): at N > 1 the step runs six
-# streams -- the step's own, two sub-batch lanes, the weight-gradient stream, the optimizer's bucket stream and RCCL's
-# -- and with HIP's 4 queues some would share one and run behind each other. --hw-queues N sets it (<= 32); without the
-# flag an exported GPU_MAX_HW_QUEUES is kept, else 8. The bench line records the REQUESTED value (`hw_queues_requested`):
-# under a profiler that initialises the HIP runtime first, the runtime may have read the variable before this line.
+# HIP hardware queues per process (read at HIP's initialisation, so set before torch loads). 4 (HIP's own default): with
+# the collectives really running in the step (--force-collective, r06g, one box, 3 interleaved repeats) 8 queues cost
+# 16 % (152.8-153.8 vs 179.3-181.5 img/s at 4; 2 queues 181.0-181.2), while without them 4 and 8 are level (182.2-183.0)
+# and 2 lose 8.5 %. --hw-queues N sets it (<= 32); without the flag an exported GPU_MAX_HW_QUEUES is kept, else 4. The
+# bench line records the REQUESTED value (`hw_queues_requested`): under a profiler that initialises the HIP runtime
+# first, the runtime may have read the variable before this line.
 if "--hw-queues" in sys.argv:
     _hwq = int(sys.argv[sys.argv.index("--hw-queues") + 1])
     if not 1 <= _hwq <= 32:
         raise SystemExit("--hw-queues: 1..32")
     os.environ["GPU_MAX_HW_QUEUES"] = str(_hwq)
 else:
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "4")
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -192,10 +193,11 @@ def main():
                     help="gradient checkpointing on (denoiser.py:945-967): keep block inputs, recompute in backward")
     ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
                     help="optimizer per gradient bucket on a side stream as each all-reduce lands (auto: off -- "
-                         "beside the engine's concurrent streams it costs 6 %% at N = 1, 163.5 vs 174.1 img/s, r05ze; "
-                         "the all-reduces themselves still run under the backward at any setting)")
+                         "with the RCCL all-reduces really in the step (--force-collective, r06f, 4 HW queues) on "
+                         "177.2 / 177.5 vs off 177.8 / 177.7 img/s; the all-reduces themselves run under the backward "
+                         "at any setting)")
     ap.add_argument("--hw-queues", type=int, default=None,
-                    help="GPU_MAX_HW_QUEUES for this process (applied at import; default: the exported value, else 8)")
+                    help="GPU_MAX_HW_QUEUES for this process (applied at import; default: the exported value, else 4)")
     ap.add_argument("--force-collective", action="store_true",
                     help="world 1 only: initialise a one-rank nccl (RCCL) group and run every gradient bucket's "
                          "all-reduce (bf16 wire cast included) and the loss all-reduce inside the timed step, as at "
@@ -236,7 +238,18 @@ def main():
             os.environ.setdefault("MASTER_PORT", "29533")
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
+        # RCCL prints its version banner on stdout when it creates the communicator; the driver reads rank 0's stdout as
+        # ONE JSON line, so stdout goes to stderr while the group (and its communicator, by the barrier) is created
+        saved = os.dup(1)
+        sys.stdout.flush()
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
 
     from vpt import engine as vpt_engine
     from vpt import ops
