@@ -27,6 +27,10 @@ OPS = {
     "attn_fwd": (("attn_fwd_kernel",), ("attn_fwd_kernel",)),
     "attn_bwd": (("attn_bwd_pre_kernel", "attn_bwd_kernel", "attn_bwd_dkdv_kernel", "attn_bwd_dq_kernel"),
                  ("attn_bwd_kernel", "attn_bwd_dkdv_kernel")),
+    # the GEMM family by kernel geometry: the 128 x 128 tile kernel and the 256 x 256 ring (each with its split-K
+    # reduces counted in the family entry above only)
+    "gemm_t128": (("gemm_bf16_kernel",), ("gemm_bf16_kernel",)),
+    "gemm_ring256": (("gemm_ring_kernel",), ("gemm_ring_kernel",)),
 }
 
 

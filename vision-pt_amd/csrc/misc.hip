@@ -57,8 +57,13 @@ __device__ __forceinline__ float2 gauss_polar(NoiseKey k, uint32_t j) {
 // both elements of pair j (fp16-rounded)
 __device__ __forceinline__ void gauss_pair_fp16(NoiseKey k, uint32_t j, float& g0, float& g1) {
   const float2 ra = gauss_polar(k, j);
-  g0 = h2f(f2h(ra.x * __builtin_amdgcn_cosf(ra.y)));
-  g1 = h2f(f2h(ra.x * __builtin_amdgcn_sinf(ra.y)));
+  // both fp16 roundings (RNE) in one v_cvt_pk_f16_f32
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+  const f2v g = {ra.x * __builtin_amdgcn_cosf(ra.y), ra.x * __builtin_amdgcn_sinf(ra.y)};
+  const h2v h = __builtin_convertvector(g, h2v);
+  g0 = (float)h[0];
+  g1 = (float)h[1];
 }
 // Strips: up to kStripP horizontally adjacent 16x16 patches of one patch row, i.e. 3 x 16 image rows of up to
 // 64 pixels (128 B per row piece: whole cache lines). patchify and the loss stage a strip's pixels through LDS by
@@ -105,7 +110,11 @@ __device__ __forceinline__ void piece_of(const PieceMap& m, int i, int& c, int& 
 // before any arithmetic. (The earlier grid-stride form decoded every piece's strip with 64-bit divisions by runtime
 // values and held one load in flight per thread: its integer index math and latency, not HBM, set its time.)
 constexpr int kPatchThreads = 128, kPatchPer = 96 * kStripP / kPatchThreads;
-__global__ __launch_bounds__(kPatchThreads) void patchify_kernel(const unsigned short* __restrict__ img, int in_kind,
+// MODE (compile time, so the element loop carries no source branches): 0 = generated noise at noise_scale 1 (the
+// draw is already fp16-rounded, so the reference's second rounding of randn * 1.0 is the identity and is skipped),
+// 1 = generated noise at another scale, 2 = explicit fp16 noise, 3 = a bf16 image copied as is (in_kind 1).
+template <int MODE>
+__global__ __launch_bounds__(kPatchThreads) void patchify_kernel(const unsigned short* __restrict__ img,
                                                                  const unsigned short* __restrict__ noise,
                                                                  const float* __restrict__ t, float noise_scale,
                                                                  uint64_t seed, int B, int H, int W,
@@ -124,10 +133,10 @@ __global__ __launch_bounds__(kPatchThreads) void patchify_kernel(const unsigned 
     piece_of(pm, i, c, ky, cc, off);
     const bool ok = i < 48 * pm.cpr;
     v[k] = ok ? *reinterpret_cast<const uint4*>(im + off) : make_uint4(0, 0, 0, 0);
-    nv[k] = ok && in_kind == 0 && noise ? *reinterpret_cast<const uint4*>(noise + img0 + off) : make_uint4(0, 0, 0, 0);
+    if (MODE == 2) nv[k] = ok ? *reinterpret_cast<const uint4*>(noise + img0 + off) : make_uint4(0, 0, 0, 0);
   }
   const NoiseKey key = noise_key(seed);
-  const float tb = in_kind == 1 ? 0.f : t[st.b];
+  const float tb = MODE == 3 ? 0.f : t[st.b];
 #pragma unroll
   for (int k = 0; k < kPatchPer; ++k) {
     const int i = threadIdx.x + k * kPatchThreads;
@@ -137,22 +146,27 @@ __global__ __launch_bounds__(kPatchThreads) void patchify_kernel(const unsigned 
     const int pl = cc >> 1, kx0 = (cc & 1) * 8;
     const unsigned short* vs = reinterpret_cast<const unsigned short*>(&v[k]);
     float o[8];
-    if (in_kind == 1) {
+    if (MODE == 3) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = bf2f(vs[e]);
     } else {
       float nz[8];
-      if (noise) {
+      if (MODE == 2) {
         const unsigned short* ns = reinterpret_cast<const unsigned short*>(&nv[k]);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) nz[e] = h2f(ns[e]);
+        for (int e = 0; e < 8; ++e) nz[e] = h2f(f2h(h2f(ns[e]) * noise_scale));
       } else {
         const uint32_t j0 = pair_counter((uint64_t)(img0 + off));  // even (W, x multiples of 8)
 #pragma unroll
         for (int e = 0; e < 4; ++e) gauss_pair_fp16(key, j0 + e, nz[2 * e], nz[2 * e + 1]);
-      }
+        if (MODE == 1) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = tb * h2f(vs[e]) + (1.f - tb) * h2f(f2h(nz[e] * noise_scale));
+          for (int e = 0; e < 8; ++e) nz[e] = h2f(f2h(nz[e] * noise_scale));
+        }
+      }
+      const float ct = 1.f - tb;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = tb * h2f(vs[e]) + ct * nz[e];
     }
     *reinterpret_cast<uint4*>(out0 + pl * 768 + c * 256 + ky * 16 + kx0) = pack8(o);
   }
@@ -970,9 +984,11 @@ extern "C" int vpt_patchify(const void* img, int in_kind, const void* noise, con
   VPT_CHECK_ARG(in_kind == 1 || t, "vpt_patchify: noising needs t");
   const long strips = (long)B * (H / 16) * ((W / 16 + kStripP - 1) / kStripP);
   VPT_CHECK_ARG(strips < (1L << 31), "vpt_patchify: too many strips");
-  hipLaunchKernelGGL(patchify_kernel, dim3((unsigned)strips), dim3(kPatchThreads), 0, (hipStream_t)stream,
-                     (const unsigned short*)img,
-                     in_kind, (const unsigned short*)noise, t, noise_scale, (uint64_t)seed, B, H, W, (bf16_t*)out);
+  auto kern = in_kind == 1 ? patchify_kernel<3> : noise ? patchify_kernel<2> : noise_scale == 1.f ? patchify_kernel<0>
+                                                                                                  : patchify_kernel<1>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)strips), dim3(kPatchThreads), 0, (hipStream_t)stream,
+                     (const unsigned short*)img, (const unsigned short*)noise, t, noise_scale, (uint64_t)seed, B, H, W,
+                     (bf16_t*)out);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
