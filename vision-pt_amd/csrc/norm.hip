@@ -64,10 +64,12 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd32_kernel(const bf16_t* __rest
   const int lane = threadIdx.x & 63, hl = lane & 31;
   const long row = (long)blockIdx.x * 8 + (threadIdx.x >> 6) * 2 + (lane >> 5);
   const bool ok = row < M;
-  uint4 v[NC];
+  uint4 v[NC], wv[NC];  // the weight pieces loaded up front too: no load follows a store (tools/isa_store_hazard.py)
 #pragma unroll
-  for (int i = 0; i < NC; ++i)
+  for (int i = 0; i < NC; ++i) {
     v[i] = ok ? *reinterpret_cast<const uint4*>(x + row * ldx + (hl + 32 * i) * 8) : make_uint4(0, 0, 0, 0);
+    wv[i] = *reinterpret_cast<const uint4*>(w + (hl + 32 * i) * 8);
+  }
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < NC; ++i) {
@@ -85,7 +87,7 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd32_kernel(const bf16_t* __rest
     const int c = hl + 32 * i;
     float f[8], wf[8];
     unpack8(v[i], f);
-    unpack8(*reinterpret_cast<const uint4*>(w + c * 8), wf);
+    unpack8(wv[i], wf);
 #pragma unroll
     for (int e = 0; e < 8; ++e) f[e] = (f[e] * r) * wf[e];
     *reinterpret_cast<uint4*>(y + row * ldy + c * 8) = pack8(f);
