@@ -1,6 +1,6 @@
 """In-process A/B of config-5 module-level knobs: one SDXLFlowMatchQLoRA built once, then rounds of K timed steps
 alternating the knob(s) on / off (vpt.sdxl globals read at call time, e.g. FOLD_Q_SCALE, FUSED_LN_LORA,
-FUSED_LN_BWD_LORA), so allocation, clocks and box are shared; medians of ms per step. The step and the optimizer
+FUSED_LN_BWD_LORA; "ops.NAME" for a vpt.ops global, e.g. ops.LORA_SERIAL_SPLIT), so allocation, clocks and box are shared; medians of ms per step. The step and the optimizer
 keep running across rounds (the values drift; the timing does not depend on them).
 
   python tools/c5_knob_ab.py FOLD_Q_SCALE [--rounds 6] [--steps 4]
@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "vision-pt_amd"))
 
 import torch  # noqa: E402
 
-from vpt import sdxl  # noqa: E402
+from vpt import ops, sdxl  # noqa: E402
 from vpt.sdxl_flow import SDXLFlowMatchQLoRA  # noqa: E402
 
 
@@ -27,15 +27,19 @@ def main():
     ap.add_argument("--steps", type=int, default=4)
     args = ap.parse_args()
     knobs = args.knobs.split(",")
+
+    def where(k):  # "NAME" = vpt.sdxl.NAME, "ops.NAME" = vpt.ops.NAME
+        return (ops, k[4:]) if k.startswith("ops.") else (sdxl, k)
     for k in knobs:
-        if not isinstance(getattr(sdxl, k), bool):
-            raise SystemExit(f"{k}: not a boolean knob of vpt.sdxl")
+        mod, name = where(k)
+        if not isinstance(getattr(mod, name), bool):
+            raise SystemExit(f"{k}: not a boolean knob of {mod.__name__}")
     m = SDXLFlowMatchQLoRA(B=4, device="cuda", seed=0)
     lat, ctx, pooled, sizes = m.make_inputs(seed=1)
 
     def setk(v):
         for k in knobs:
-            setattr(sdxl, k, v)
+            setattr(*where(k), v)
 
     for v in (True, False):
         setk(v)
