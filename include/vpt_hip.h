@@ -45,6 +45,9 @@ long vpt_gemm_workspace_bytes(int M, int N, int K, int splits);
 /* vpt_gemm_bf16 with an explicit tile geometry (stateless; same results contract): geometry 0 =
  * automatic, 128 = 128x128 2-stage, 256 = the persistent 256x256 ping-pong ring, whose
  * min(work items, ring_grid) blocks walk (tile, split-K slice) items (ring_grid 0 = one block per item).
+ * 1281 = 128x128 tiles on the pipeline of the 256x128 ring (3-stage LDS-DMA ring, counted waits; bf16 / f32 /
+ * f32-accumulate output with bias / residual, split-K; no fused bias gradient, SwiGLU or QK-norm epilogue): the
+ * same K order as geometry 128, equal results. The LoRA entry points below take it as well.
  * Used by tests to cover both geometries and multi-item ring walks at small shapes. */
 int vpt_gemm_bf16_tiled(const void* A, long lda, int a_kmajor, const void* B, long ldb, int b_kmajor, void* C,
                         long ldc, int M, int N, int K, const void* bias, const void* resid, long ldr, int out_mode,

@@ -270,6 +270,31 @@ def test_swiglu_fused_epilogues_match_unfused(ops, M):
     assert rel(dx12[:, :F], a.grad) < 1e-2 and rel(dx12[:, F:], b.grad) < 1e-2
 
 
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("splits", [1, 2])
+def test_gemm_r2_128_equals_t128(ops, ak, bk, splits):
+    """Geometry 1281 (128x128 tiles on the R2 ring's 3-stage LDS-DMA pipeline) == geometry 128 (the two-stage 128x128
+    kernel): the same 32-deep K chunks in the same order, so equal outputs -- bf16 with bias + residual, f32 and f32
+    accumulate, ragged M / N / K, split-K."""
+    M, N, K = 1000, 1280, 1216
+    a = rnd(M, K, seed=90) if ak else rnd(K, M, seed=90)
+    b = rnd(N, K, scale=0.05, seed=91) if bk else rnd(K, N, scale=0.05, seed=91)
+    bias, resid = rnd(N, scale=0.1, seed=92), rnd(M, N, seed=93)
+    for out_mode, kw in ((ops.OUT_BF16, dict(bias=bias, resid=resid)), (ops.OUT_F32, {}), (ops.OUT_F32_ACC, {})):
+        dt = torch.bfloat16 if out_mode == ops.OUT_BF16 else torch.float32
+        if out_mode == ops.OUT_F32_ACC:
+            if splits > 1:
+                continue
+            base = rnd(M, N, dtype=torch.float32, seed=94)
+            ref, out = base.clone(), base.clone()
+        else:
+            ref, out = torch.empty(M, N, dtype=dt, device=DEV), torch.full((M, N), float("nan"), dtype=dt, device=DEV)
+        ops.gemm(a, ak, b, bk, M, N, K, ref, out_mode=out_mode, splits=splits, geometry=128, **kw)
+        ops.gemm(a, ak, b, bk, M, N, K, out, out_mode=out_mode, splits=splits, geometry=1281, **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), (out_mode, (out.float() - ref.float()).abs().max().item())
+
+
 def test_gemm_split_matches_unsplit(ops):
     M, N, K = 2048, 384, 256
     dy, x = rnd(M, N, seed=12), rnd(M, K, seed=13)

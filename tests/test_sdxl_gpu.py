@@ -211,6 +211,37 @@ def test_gemm_lora_bit_exact_vs_concatenated_gemm(ops, geometry, splits, forward
     assert rel(out.float() - resid.float(), y) < 1e-2
 
 
+@pytest.mark.parametrize("forward", [True, False])
+@pytest.mark.parametrize("M,Nw,Kw", [(4224, 1280, 1280), (600, 1280, 640), (1000, 640, 1280)])
+def test_gemm_lora_r2_128_equals_t128(ops, forward, M, Nw, Kw):
+    """The config-5 LoRA GEMMs on geometry 1281 (128x128 tiles, R2 pipeline, the K-extension padded to 32) == geometry
+    128 (the extension padded to 64 with zeros): equal outputs, bias and residual epilogues, forward and input gradient;
+    the grouped form (q | k | v) as well."""
+    N, K = (Nw, Kw) if forward else (Kw, Nw)
+    W = rnd(Nw, Kw, scale=0.05, seed=60)
+    a = rnd(M, K, seed=61)
+    a2 = rnd(M, 16, scale=0.5, seed=62)
+    b2 = rnd(N, 16, scale=0.1, seed=63) if forward else rnd(16, N, scale=0.1, seed=63)
+    bias = rnd(N, scale=0.1, seed=64) if forward else None
+    resid = rnd(M, N, seed=65)
+    ref = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+    ops.gemm_lora(a, W, forward, a2, b2, M, N, K, ref, bias=bias, resid=resid, geometry=128, splits=1)
+    ops.gemm_lora(a, W, forward, a2, b2, M, N, K, out, bias=bias, resid=resid, geometry=1281, splits=1)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref), (out.float() - ref.float()).abs().max().item()
+    if forward:
+        Ws = [rnd(Nw, Kw, scale=0.03, seed=66 + g) for g in range(3)]
+        ups = [rnd(Nw, 16, scale=0.1, seed=70 + g) for g in range(3)]
+        ds = rnd(M, 48, scale=0.5, seed=73)
+        o1 = torch.empty(M, 3 * Nw, dtype=torch.bfloat16, device=DEV)
+        o2 = torch.full((M, 3 * Nw), float("nan"), dtype=torch.bfloat16, device=DEV)
+        ops.gemm_lora_grouped(a, torch.cat(Ws, 0), ds, ups, o1, geometry=128, splits=1)
+        ops.gemm_lora_grouped(a, torch.cat(Ws, 0), ds, ups, o2, geometry=1281, splits=1)
+        torch.cuda.synchronize()
+        assert torch.equal(o1, o2)
+
+
 @pytest.mark.parametrize("gn,geometry", [(1280, 128), (1280, 256), (640, 128)])
 def test_gemm_lora_grouped_bit_exact_vs_per_target(ops, gn, geometry):
     """vpt_gemm_bf16_lora_grouped (q | k | v of one input as one GEMM, each column block with its own LoRA term)

@@ -29,6 +29,9 @@ using namespace vptg;
 
 namespace vptg {
 int launch_r2(const GemmArgs& g, bool ak, bool bk, hipStream_t s);  // gemm_r2.hip: the 256x128 two-blocks-per-CU ring
+int launch_r2_128(const GemmArgs& g, bool ak, bool bk, hipStream_t s);  // gemm_r2.hip: its 128x128 form
+// geometry 1281 of the C-ABI: the 128x128 tiles on the R2 ring's pipeline (3-stage LDS-DMA ring, counted waits)
+constexpr int kGeoR2x128 = 1281;
 }
 
 namespace {
@@ -572,6 +575,7 @@ template <bool AK, bool BK_>
 int launch_geo(const GemmArgs& g, int splits, int geo, hipStream_t s) {
   if (geo != 128 && geo != 2562 && g.N % 8 != 0) geo = 128;  // ring epilogue stores 8-column chunks
   if (geo == 256) return use_r2(g, AK) ? launch_r2_st(g, AK, BK_, s) : launch_ring<AK, BK_, true>(g, splits, s);
+  if (geo == kGeoR2x128) return launch_r2_128(g, AK, BK_, s);
 #ifdef VPT_DIAG
   // diagnostic build only (libvpt_hip_diag.so): A/B geometries, timing ablations with WRONG results
   // (2563, 2564), stamped / timeline builds
@@ -703,7 +707,8 @@ extern "C" int vpt_gemm_bf16_lora(const void* A, long lda, const void* B, long l
   VPT_CHECK_ARG(K % 64 == 0 && K2 > 0 && K2 <= 256 && K2 % 8 == 0, "vpt_gemm_bf16_lora: K % 64 == 0, K2 in 8..256, K2 % 8 == 0");
   VPT_CHECK_ARG(lda2 % 8 == 0 && ldb2 % 8 == 0 && lda2 >= K2 && (b_kmajor ? ldb2 >= K2 : ldb2 >= N),
                 "vpt_gemm_bf16_lora: LoRA leading dims (16-B multiples, >= K2 / N)");
-  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256, "vpt_gemm_bf16_lora: geometry 0, 128 or 256");
+  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256 || geometry == kGeoR2x128,
+                "vpt_gemm_bf16_lora: geometry 0, 128, 256 or 1281");
   return gemm_impl(A, lda, 1, B, ldb, b_kmajor, C, ldc, M, N, K, bias, resid, ldr, out_mode, ACT_NONE, splits, workspace,
                    1.f, geometry, 0, stream, nullptr, 0, nullptr, A2, lda2, B2, ldb2, K2);
 }
@@ -719,7 +724,8 @@ extern "C" int vpt_gemm_bf16_lora_grouped(const void* A, long lda, const void* B
   VPT_CHECK_ARG(K % 64 == 0 && r > 0 && r <= 64 && r % 8 == 0 && g_n % 128 == 0,
                 "vpt_gemm_bf16_lora_grouped: K % 64 == 0, r in 8..64 (r % 8 == 0), g_n % 128 == 0");
   VPT_CHECK_ARG(lda2 % 8 == 0 && lda2 >= G * r, "vpt_gemm_bf16_lora_grouped: lda2 >= G * r (16-B multiple)");
-  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256, "vpt_gemm_bf16_lora_grouped: geometry 0, 128, 256");
+  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256 || geometry == kGeoR2x128,
+                "vpt_gemm_bf16_lora_grouped: geometry 0, 128, 256 or 1281");
   return gemm_impl(A, lda, 1, B, ldb, 1, C, ldc, M, G * g_n, K, bias, resid, ldr, OUT_BF16, ACT_NONE, splits, workspace,
                    1.f, geometry, 0, stream, nullptr, 0, nullptr, A2, lda2, B2s[0], r, r, B2s, G, g_n);
 }
@@ -736,7 +742,8 @@ extern "C" int vpt_gemm_bf16_lora_scaled(const void* A, long lda, const void* B,
   VPT_CHECK_ARG(K % 64 == 0 && K2 > 0 && K2 <= 256 && K2 % 8 == 0, "vpt_gemm_bf16_lora_scaled: K % 64 == 0, K2 in 8..256, K2 % 8 == 0");
   VPT_CHECK_ARG(lda2 % 8 == 0 && ldb2 % 8 == 0 && lda2 >= K2 && (b_kmajor ? ldb2 >= K2 : ldb2 >= N),
                 "vpt_gemm_bf16_lora_scaled: LoRA leading dims (16-B multiples, >= K2 / N)");
-  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256, "vpt_gemm_bf16_lora_scaled: geometry 0, 128 or 256");
+  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256 || geometry == kGeoR2x128,
+                "vpt_gemm_bf16_lora_scaled: geometry 0, 128, 256 or 1281");
   return gemm_impl(A, lda, 1, B, ldb, b_kmajor, C, ldc, M, N, K, bias, resid, ldr, OUT_BF16, ACT_NONE, 1, nullptr,
                    alpha, geometry, 0, stream, nullptr, 0, nullptr, A2, lda2, B2, ldb2, K2, nullptr, 0, 0, alpha_cols);
 }
@@ -750,8 +757,8 @@ extern "C" int vpt_gemm_bf16_lora_grouped_scaled(const void* A, long lda, const 
   VPT_CHECK_ARG(K % 64 == 0 && r > 0 && r <= 64 && r % 8 == 0 && g_n % 128 == 0,
                 "vpt_gemm_bf16_lora_grouped_scaled: K % 64 == 0, r in 8..64 (r % 8 == 0), g_n % 128 == 0");
   VPT_CHECK_ARG(lda2 % 8 == 0 && lda2 >= G * r, "vpt_gemm_bf16_lora_grouped_scaled: lda2 >= G * r (16-B multiple)");
-  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256,
-                "vpt_gemm_bf16_lora_grouped_scaled: geometry 0, 128, 256");
+  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256 || geometry == kGeoR2x128,
+                "vpt_gemm_bf16_lora_grouped_scaled: geometry 0, 128, 256 or 1281");
   return gemm_impl(A, lda, 1, B, ldb, 1, C, ldc, M, G * g_n, K, bias, resid, ldr, OUT_BF16, ACT_NONE, 1, nullptr,
                    alpha, geometry, 0, stream, nullptr, 0, nullptr, A2, lda2, B2s[0], r, r, B2s, G, g_n, alpha_cols);
 }
@@ -767,7 +774,8 @@ extern "C" int vpt_gemm_bf16_lora_stacked(const void* A, long lda, const void* B
                 "vpt_gemm_bf16_lora_stacked: K % 64 == 0, r in 8..64 (r % 8 == 0), g_n % 128 == 0");
   VPT_CHECK_ARG(lda2 % 8 == 0 && lda2 >= (long)G * r, "vpt_gemm_bf16_lora_stacked: lda2 >= G * r (16-B multiple)");
   VPT_CHECK_ARG((long)G * g_n < (1L << 31), "vpt_gemm_bf16_lora_stacked: G * g_n < 2^31");
-  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256, "vpt_gemm_bf16_lora_stacked: geometry 0, 128, 256");
+  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256 || geometry == kGeoR2x128,
+                "vpt_gemm_bf16_lora_stacked: geometry 0, 128, 256 or 1281");
   return gemm_impl(A, lda, 1, B, ldb, 1, C, ldc, M, G * g_n, K, nullptr, nullptr, 0, OUT_BF16, ACT_NONE, splits,
                    workspace, 1.f, geometry, 0, stream, nullptr, 0, nullptr, A2, lda2, B2, r, r, nullptr, G, g_n);
 }
@@ -776,7 +784,8 @@ extern "C" int vpt_gemm_bf16_tiled(const void* A, long lda, int a_kmajor, const 
                                    void* C, long ldc, int M, int N, int K, const void* bias, const void* resid,
                                    long ldr, int out_mode, int act, int splits, void* workspace, float alpha,
                                    int geometry, int ring_grid, void* stream) {
-  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256, "vpt_gemm_bf16_tiled: geometry 0, 128 or 256");
+  VPT_CHECK_ARG(geometry == 0 || geometry == 128 || geometry == 256 || geometry == kGeoR2x128,
+                "vpt_gemm_bf16_tiled: geometry 0, 128, 256 or 1281");
   VPT_CHECK_ARG(ring_grid >= 0 && ring_grid <= 65536, "vpt_gemm_bf16_tiled: ring_grid 0..65536");
   return gemm_impl(A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, M, N, K, bias, resid, ldr, out_mode, act, splits,
                    workspace, alpha, geometry, ring_grid, stream);
@@ -880,8 +889,8 @@ int gemm_impl(const void* A, long lda, int a_kmajor, const void* B, long ldb, in
     g.out_mode = out_mode;
   }
   int geo = pick_geo(M, N, splits, geo_req);
-  if (g.g_n > 0 && g.g_n % 256 != 0) geo = 128;  // grouped extension: a 256-wide tile would straddle two groups
-  if (g.alpha_cols % 256 != 0) geo = 128;         // the ring applies alpha per 256-wide tile
+  if (geo == 256 && g.g_n > 0 && g.g_n % 256 != 0) geo = 128;  // grouped extension: a 256-wide tile would straddle
+  if (geo == 256 && g.alpha_cols % 256 != 0) geo = 128;         // two groups; the ring applies alpha per 256-wide tile
   const bool rs = rsum_out && !a_kmajor && geo == 256 && N % 8 == 0 && workspace != nullptr;
   if (rsum_done) *rsum_done = rs;
   float* rpart = nullptr;

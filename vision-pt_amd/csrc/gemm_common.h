@@ -413,7 +413,8 @@ struct EpiAddr {
   float alpha;  // the output scale of this tile (GemmArgs::alpha / alpha_cols)
 };
 
-__device__ __forceinline__ EpiAddr epi_addr(const GemmArgs& g, const RingItem& it, int wm, int wn, int lane) {
+__device__ __forceinline__ EpiAddr epi_addr(const GemmArgs& g, const RingItem& it, int wm, int wn, int lane,
+                                             int wr = 128) {  // wr: rows of a wave tile (the 128x128 R2 tiles: 64)
   EpiAddr e;
   const int es = g.out_mode == OUT_BF16 ? 2 : 4;
   const int rows_here = min(256, g.M - it.m0);
@@ -422,7 +423,7 @@ __device__ __forceinline__ EpiAddr epi_addr(const GemmArgs& g, const RingItem& i
   const int tcol = wn * 64 + (lane & 7) * 8;  // column within the tile
   e.col_ok = it.n0 + tcol < g.N;
   e.alpha = g.alpha_cols > 0 && it.n0 >= g.alpha_cols ? 1.f : g.alpha;
-  const int lrow = wm * 128 + (lane >> 3);  // tile row of (fragment 0, p = 0)
+  const int lrow = wm * wr + (lane >> 3);  // tile row of (fragment 0, p = 0)
   // lane part of the store offset; fragment i / half p add the wave-uniform soffset (i*16 + p*8) rows
   e.voff = e.col_ok ? (uint32_t)((lrow * (int)g.ldc + tcol) * es) : 0x80000000u;
   e.rstride = (int)g.ldc * es;  // bytes per row

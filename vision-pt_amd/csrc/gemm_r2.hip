@@ -18,10 +18,14 @@ namespace {
 
 constexpr int R2TN = 128;                   // block tile columns
 constexpr int R2NW = 4;                     // waves per block
-constexpr int R2A = 256 * RBK * 2;          // A stage bytes (16 KB)
-constexpr int R2STAGE = R2A + R2TN * RBK * 2;  // + B (8 KB)
 constexpr int R2ST = 3;                     // ring stages
-constexpr int R2LDS = R2ST * R2STAGE;       // 72 KB
+// TM = block tile rows: 256 (the 256x128 ring) or 128 (128x128 tiles, 4 waves of 64x64: the small-grid GEMMs of config 5)
+template <int TM> constexpr int r2_a_bytes() { return TM * RBK * 2; }                     // A stage bytes (16 / 8 KB)
+template <int TM> constexpr int r2_stage() { return r2_a_bytes<TM>() + R2TN * RBK * 2; }  // + B (8 KB)
+template <int TM> constexpr int r2_lds() { return R2ST * r2_stage<TM>(); }                // 72 / 48 KB
+constexpr int R2A = r2_a_bytes<256>();
+constexpr int R2STAGE = r2_stage<256>();
+constexpr int R2LDS = r2_lds<256>();
 // K-step schedule knobs (compile-time; A/B builds of this unit only): PRIO = s_setprio 1 around the MFMAs; SPLIT = the
 // fragment reads in two halves (B + A 0-3, then A 4-7 behind the first 16 MFMAs); DMAMID = tile t+2's DMA issued after
 // the first half of the MFMAs instead of at the top of the step.
@@ -73,18 +77,18 @@ __device__ __forceinline__ void glds_step6(const void* abase, const void* bbase,
       : "memory");
 }
 
-template <bool AK, bool BK_, int SW>
+template <bool AK, bool BK_, int SW, int TM = 256>
 __device__ __forceinline__ void r2_voffs(const GemmArgs& g, long lda, long ldb, int m0, int n0, int nrows_b, int kv,
                                          int wid, int lane, uint32_t (&va)[4], uint32_t (&vb)[2]) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) va[i] = tile_voff<AK, 256, R2NW>(lda, m0, g.M, kv, wid, lane, i);
+  for (int i = 0; i < TM / 64; ++i) va[i] = tile_voff<AK, TM, R2NW>(lda, m0, g.M, kv, wid, lane, i);
 #pragma unroll
   for (int i = 0; i < 2; ++i)
     vb[i] = SW ? tile_voff_sw<R2TN, R2NW>(ldb, n0, g.N / 2, kv, wid, lane, i)
                : tile_voff<BK_, R2TN, R2NW>(ldb, n0, nrows_b, kv, wid, lane, i);
 }
 
-template <bool AK, bool BK_, int SW>
+template <bool AK, bool BK_, int SW, int TM = 256>
 __device__ __forceinline__ R2Item r2_item(const GemmArgs& g, int item, int items, int tiles, int tiles_n, int wid,
                                           int lane) {
   const int q8 = items >> 3, r8 = items & 7, xcd = item & 7;
@@ -92,7 +96,7 @@ __device__ __forceinline__ R2Item r2_item(const GemmArgs& g, int item, int items
   R2Item it;
   it.split = wgid / tiles;
   const int tile = wgid - it.split * tiles;
-  it.m0 = tile / tiles_n * 256;
+  it.m0 = tile / tiles_n * TM;
   it.n0 = tile % tiles_n * (SW ? R2TN / 2 : R2TN);  // SW: first output feature of the tile
   it.kbeg = it.split * g.k_split;
   it.kend = min(g.K, it.kbeg + g.k_split);
@@ -103,17 +107,25 @@ __device__ __forceinline__ R2Item r2_item(const GemmArgs& g, int item, int items
     it.nk += ne;
     it.klast = g.K2 - (ne - 1) * RBK;
   }
-  r2_voffs<AK, BK_, SW>(g, g.lda, g.ldb, it.m0, it.n0, g.N, RBK, wid, lane, it.va, it.vb);
+  r2_voffs<AK, BK_, SW, TM>(g, g.lda, g.ldb, it.m0, it.n0, g.N, RBK, wid, lane, it.va, it.vb);
   return it;
 }
 
-// K tile t of the item by LDS-DMA into ring stage t % 3: this wave's A pieces at 4 wid + i, B pieces at 2 wid + i.
-template <bool AK, bool BK_, int SW>
+// K tile t of the item by LDS-DMA into ring stage t % 3: this wave's A pieces at (TM / 64) wid + i, B pieces at
+// 2 wid + i.
+template <bool AK, bool BK_, int SW, int TM = 256>
+__device__ __forceinline__ void r2_dma(const void* ab, const void* bb, const uint32_t (&va)[4], const uint32_t (&vb)[2],
+                                       uint32_t la, uint32_t lb) {
+  if constexpr (TM == 256) glds_step6(ab, bb, va, vb, la, lb);
+  else glds_step(ab, bb, va[0], va[1], vb[0], vb[1], la, la + 1024, lb, lb + 1024);
+}
+
+template <bool AK, bool BK_, int SW, int TM = 256>
 __device__ __forceinline__ void r2_issue(const GemmArgs& g, const R2Item& it, int t, uint32_t smem0, int wid,
                                          int lane) {
-  const uint32_t st = smem0 + (uint32_t)(t % R2ST) * R2STAGE;
-  const uint32_t la = __builtin_amdgcn_readfirstlane(st + wid * 4096);
-  const uint32_t lb = __builtin_amdgcn_readfirstlane(st + R2A + wid * 2048);
+  const uint32_t st = smem0 + (uint32_t)(t % R2ST) * r2_stage<TM>();
+  const uint32_t la = __builtin_amdgcn_readfirstlane(st + wid * (TM * 16));
+  const uint32_t lb = __builtin_amdgcn_readfirstlane(st + r2_a_bytes<TM>() + wid * 2048);
   const int k0 = it.kbeg + t * RBK;
   if (k0 >= it.kend) {  // K-extension tile (A2 / B2), masked like a partial last tile
     const int e0 = k0 - it.kend, kv = min(RBK, g.K2 - e0);
@@ -121,30 +133,35 @@ __device__ __forceinline__ void r2_issue(const GemmArgs& g, const R2Item& it, in
     const bf16_t* b2 = g.g_n > 0 ? (g.B2g[0] ? g.B2g[grp] : g.B2 + (long)grp * g.g_n * g.ldb2) : g.B2;
     const int nb0 = it.n0 - grp * g.g_n, nrows = g.g_n > 0 ? g.g_n : g.N;
     uint32_t va[4], vb[2];
-    r2_voffs<AK, BK_, 0>(g, g.lda2, g.ldb2, it.m0, nb0, nrows, kv, wid, lane, va, vb);
-    glds_step6(uniform_ptr(tile_ptr<AK>(g.A2 + grp * g.K2, g.lda2, it.m0, e0)),
-               uniform_ptr(tile_ptr<BK_>(b2, g.ldb2, nb0, e0)), va, vb, la, lb);
+    r2_voffs<AK, BK_, 0, TM>(g, g.lda2, g.ldb2, it.m0, nb0, nrows, kv, wid, lane, va, vb);
+    r2_dma<AK, BK_, SW, TM>(uniform_ptr(tile_ptr<AK>(g.A2 + grp * g.K2, g.lda2, it.m0, e0)),
+                            uniform_ptr(tile_ptr<BK_>(b2, g.ldb2, nb0, e0)), va, vb, la, lb);
     return;
   }
   const int kv = min(RBK, it.kend - k0);
   const void* ab = uniform_ptr(tile_ptr<AK>(g.A, g.lda, it.m0, k0));
   const void* bb = uniform_ptr(tile_ptr<BK_>(g.B, g.ldb, SW ? 0 : it.n0, k0));
   if (kv == RBK) {
-    glds_step6(ab, bb, it.va, it.vb, la, lb);
+    r2_dma<AK, BK_, SW, TM>(ab, bb, it.va, it.vb, la, lb);
   } else {
     uint32_t va[4], vb[2];
-    r2_voffs<AK, BK_, SW>(g, g.lda, g.ldb, it.m0, it.n0, g.N, kv, wid, lane, va, vb);
-    glds_step6(ab, bb, va, vb, la, lb);
+    r2_voffs<AK, BK_, SW, TM>(g, g.lda, g.ldb, it.m0, it.n0, g.N, kv, wid, lane, va, vb);
+    r2_dma<AK, BK_, SW, TM>(ab, bb, va, vb, la, lb);
   }
 }
 
-template <bool AK, bool BK_, int SW, int EPI, bool RS>
+template <bool AK, bool BK_, int SW, int EPI, bool RS, int TM = 256>
 __global__ __launch_bounds__(256, 2) void gemm_r2_kernel(GemmArgs g) {
+  static_assert(TM == 256 || (TM == 128 && SW == 0 && !RS && EPI != EPI_QKN && !epi_swb(EPI)),
+                "128-row tiles: plain / residual / accumulate epilogues");
+  constexpr int MI = TM / 32, WR = TM / 2;  // fragments and rows of a wave tile (128 x 64 or 64 x 64)
+  constexpr int PCS = TM / 64 + 2;          // LDS-DMA pieces per wave and K tile (A + B)
+  constexpr int STG = r2_stage<TM>(), AB = r2_a_bytes<TM>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int tiles_n = (g.N + R2TN - 1) / R2TN;
-  const int tiles = ((g.M + 255) / 256) * tiles_n;
+  const int tiles = ((g.M + TM - 1) / TM) * tiles_n;
   const int items = tiles * g.splits;
   if ((int)blockIdx.x >= items) return;
   // The two blocks a CU starts with begin together and, equal in length, would keep reaching their epilogues together.
@@ -155,7 +172,7 @@ __global__ __launch_bounds__(256, 2) void gemm_r2_kernel(GemmArgs g) {
     while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)g.stagger) __builtin_amdgcn_s_sleep(2);
   }
   const uint32_t smem0 = (uint32_t)(uintptr_t)(VPT_LDS char*)smem;
-  const R2Item it = r2_item<AK, BK_, SW>(g, blockIdx.x, items, tiles, tiles_n, wid, lane);
+  const R2Item it = r2_item<AK, BK_, SW, TM>(g, blockIdx.x, items, tiles, tiles_n, wid, lane);
   const int nk = it.nk;
 
   uint4 braw = make_uint4(0, 0, 0, 0), braw2 = make_uint4(0, 0, 0, 0);
@@ -180,9 +197,9 @@ __global__ __launch_bounds__(256, 2) void gemm_r2_kernel(GemmArgs g) {
     if (SW) asm volatile("" : "+v"(bias8b[e]));
   }
 
-  floatx4 acc[8][4];
+  floatx4 acc[8][4];  // [MI][4] used
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   // RS (fused bias gradient): the items of the first N tile also sum their A rows over k (MFMAs against an all-ones
@@ -193,10 +210,12 @@ __global__ __launch_bounds__(256, 2) void gemm_r2_kernel(GemmArgs g) {
   const bool rs_on = RS && it.n0 == 0;
   const int wn_u = __builtin_amdgcn_readfirstlane(wn);
 
-  r2_issue<AK, BK_, SW>(g, it, 0, smem0, wid, lane);
+  r2_issue<AK, BK_, SW, TM>(g, it, 0, smem0, wid, lane);
   if (nk > 1) {
-    r2_issue<AK, BK_, SW>(g, it, 1, smem0, wid, lane);
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // tile 0 landed (this wave); tile 1's six pieces in flight
+    r2_issue<AK, BK_, SW, TM>(g, it, 1, smem0, wid, lane);
+    // tile 0 landed (this wave); tile 1's pieces in flight
+    if constexpr (PCS == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -204,34 +223,34 @@ __global__ __launch_bounds__(256, 2) void gemm_r2_kernel(GemmArgs g) {
 
   for (int kt = 0; kt < nk; ++kt) {
     // tile kt + 2 into the stage of tile kt - 1, which every wave finished reading before the last barrier
-    if (!VPT_R2_DMAMID && kt + 2 < nk) r2_issue<AK, BK_, SW>(g, it, kt + 2, smem0, wid, lane);
-    const char* st = smem + (kt % R2ST) * R2STAGE;
+    if (!VPT_R2_DMAMID && kt + 2 < nk) r2_issue<AK, BK_, SW, TM>(g, it, kt + 2, smem0, wid, lane);
+    const char* st = smem + (kt % R2ST) * STG;
     const bool mask = kt == nk - 1 && it.klast < RBK;
     bf16x8 bfr[4], af[8];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      bfr[j] = read_frag32<BK_, R2TN>(st + R2A, SW ? ((j & 2) ? R2TN / 2 : 0) + wn * 32 + (j & 1) * 16 : wn * 64 + j * 16,
+      bfr[j] = read_frag32<BK_, R2TN>(st + AB, SW ? ((j & 2) ? R2TN / 2 : 0) + wn * 32 + (j & 1) * 16 : wn * 64 + j * 16,
                                       lane);
 #pragma unroll
-    for (int i = 0; i < (VPT_R2_SPLIT ? 4 : 8); ++i) {
-      af[i] = read_frag32<AK, 256>(st, wm * 128 + i * 16, lane);
+    for (int i = 0; i < (VPT_R2_SPLIT ? MI / 2 : MI); ++i) {
+      af[i] = read_frag32<AK, TM>(st, wm * WR + i * 16, lane);
       if (mask) af[i] = mask_k(af[i], 8 * (lane >> 4), it.klast);
     }
     if (VPT_R2_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI / 2; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     if (VPT_R2_SPLIT) {
 #pragma unroll
-      for (int i = 4; i < 8; ++i) {
-        af[i] = read_frag32<AK, 256>(st, wm * 128 + i * 16, lane);
+      for (int i = MI / 2; i < MI; ++i) {
+        af[i] = read_frag32<AK, TM>(st, wm * WR + i * 16, lane);
         if (mask) af[i] = mask_k(af[i], 8 * (lane >> 4), it.klast);
       }
     }
-    if (VPT_R2_DMAMID && kt + 2 < nk) r2_issue<AK, BK_, SW>(g, it, kt + 2, smem0, wid, lane);
+    if (VPT_R2_DMAMID && kt + 2 < nk) r2_issue<AK, BK_, SW, TM>(g, it, kt + 2, smem0, wid, lane);
 #pragma unroll
-    for (int i = 4; i < 8; ++i)
+    for (int i = MI / 2; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     if (rs_on) {
@@ -244,9 +263,13 @@ __global__ __launch_bounds__(256, 2) void gemm_r2_kernel(GemmArgs g) {
     }
     if (VPT_R2_PRIO) __builtin_amdgcn_s_setprio(0);
     if (kt + 1 < nk) {
-      // this wave's pieces of tile kt + 1 landed (tile kt + 2's six younger ones may still fly), then every wave's
-      if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // this wave's pieces of tile kt + 1 landed (tile kt + 2's younger ones may still fly), then every wave's
+      if (kt + 2 < nk) {
+        if constexpr (PCS == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       __syncthreads();
     }
   }
@@ -266,15 +289,29 @@ __global__ __launch_bounds__(256, 2) void gemm_r2_kernel(GemmArgs g) {
   }
   // Epilogue staging: this wave's 4 KB slice of the stage of tile nk - 3 (or an unused stage): every wave finished
   // reading it before the barrier that ended step nk - 2, and no DMA targets it after that.
-  char* stg = smem + (nk % R2ST) * R2STAGE + wid * 4096;
+  char* stg = smem + (nk % R2ST) * STG + wid * 4096;
   RingItem ri;
   ri.m0 = it.m0; ri.n0 = it.n0; ri.split = it.split;
   if (SW) {
     epilogue_ring_swf(g, acc, stg, lane, ri, wm, wn, bias8, bias8b);
     return;
   }
-  EpiAddr ea = epi_addr(g, ri, wm, wn, lane);
+  EpiAddr ea = epi_addr(g, ri, wm, wn, lane, WR);
   EpiPre pre, pre2;
+  if constexpr (TM == 128) {  // 4 fragments per wave
+    if constexpr (epi_frags(EPI) == 4) {
+      epi_preload<EPI, 0>(g, ea, pre);
+      epilogue_ring<EPI, 0, 4>(g, acc, stg, lane, ea, bias8, pre);
+    } else if constexpr (epi_frags(EPI) == 2) {
+      epi_preload<EPI, 0>(g, ea, pre);
+      epilogue_ring<EPI, 0, 2>(g, acc, stg, lane, ea, bias8, pre);
+      epi_preload<EPI, 2>(g, ea, pre);
+      epilogue_ring<EPI, 2, 4>(g, acc, stg, lane, ea, bias8, pre);
+    } else {
+      epilogue_ring<EPI, 0, 4>(g, acc, stg, lane, ea, bias8, pre);
+    }
+    return;
+  }
   if (EPI == EPI_QKN) {
     epilogue_ring_qkn(g, acc, stg, lane, ea, bias8, ri, wm, wn);
   } else if (EPI == EPI_SWB) {
@@ -306,9 +343,9 @@ __global__ __launch_bounds__(256, 2) void gemm_r2_kernel(GemmArgs g) {
   }
 }
 
-template <bool AK, bool BK_, int SW, int EPI, bool RS>
+template <bool AK, bool BK_, int SW, int EPI, bool RS, int TM = 256>
 int r2_launch(const GemmArgs& g, int items, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_r2_kernel<AK, BK_, SW, EPI, RS>), dim3(items), dim3(256), R2LDS, s, g);
+  hipLaunchKernelGGL((gemm_r2_kernel<AK, BK_, SW, EPI, RS, TM>), dim3(items), dim3(256), r2_lds<TM>(), s, g);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }
@@ -337,7 +374,29 @@ int r2_dispatch(const GemmArgs& g, int items, hipStream_t s) {
   return r2_launch<AK, BK_, 0, EPI_PLAIN, false>(g, items, s);
 }
 
+// 128x128 tiles (TM = 128): plain, residual or accumulate epilogue, no fused bias gradient / SwiGLU / QK-norm.
+template <bool AK, bool BK_>
+int r2_128_dispatch(const GemmArgs& g, int items, hipStream_t s) {
+  VPT_CHECK_ARG(g.sw == 0 && g.qk_d == 0 && !g.rsum, "gemm r2 128x128: plain / residual / accumulate epilogues only");
+  const int epi = epi_mode(g);
+  if (epi == EPI_RESID) return r2_launch<AK, BK_, 0, EPI_RESID, false, 128>(g, items, s);
+  if (epi == EPI_ACC) return r2_launch<AK, BK_, 0, EPI_ACC, false, 128>(g, items, s);
+  return r2_launch<AK, BK_, 0, EPI_PLAIN, false, 128>(g, items, s);
+}
+
 }  // namespace
+
+// The 128x128 form of the R2 ring: the config-5 GEMMs whose 256-wide grids cover few CUs (2 blocks per CU, 48 KB of
+// LDS each; the same K order as the 128x128 T128 kernel, so the same sums).
+int launch_r2_128(const GemmArgs& g, bool ak, bool bk, hipStream_t s) {
+  VPT_CHECK_ARG(g.N % 8 == 0, "gemm r2 128x128: N % 8 == 0 (8-column epilogue chunks)");
+  VPT_CHECK_ARG(g.g_n % R2TN == 0 && g.alpha_cols % R2TN == 0, "gemm r2 128x128: groups / alpha columns in 128-column tiles");
+  const int items = ((g.M + 127) / 128) * ((g.N + R2TN - 1) / R2TN) * g.splits;
+  if (ak && bk) return r2_128_dispatch<true, true>(g, items, s);
+  if (ak) return r2_128_dispatch<true, false>(g, items, s);
+  if (bk) return r2_128_dispatch<false, true>(g, items, s);
+  return r2_128_dispatch<false, false>(g, items, s);
+}
 
 // The 256x128 ring for an argument block the 256x256 ring would run (gemm.hip launch_ring: same GemmArgs, one block per
 // item, ring_grid ignored). Tiles never straddle a LoRA group or an alpha column block: g_n, alpha_cols % 128 == 0.

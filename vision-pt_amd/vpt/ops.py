@@ -141,17 +141,22 @@ def workspace(dev, tag: str, n: int, dtype=F32) -> torch.Tensor:
     return buf[:n]
 
 
+GEO_R2_128 = 1281  # 128 x 128 tiles on the R2 ring's pipeline (include/vpt_hip.h vpt_gemm_bf16_tiled)
+LORA_R2_128 = True  # lora_gemm_plan: GEO_R2_128 instead of the two-stage 128 x 128 kernel (A/B knob)
+
+
 def lora_gemm_plan(M: int, N: int, K: int) -> tuple[int, int]:
     """(geometry, splits) for a base+LoRA GEMM: the 256 x 256 ring when its tiles fill the chip (>= 160), a
     K-split ring for small grids over a long reduction (K >= 4096: ~240 work items), otherwise 128 x 128 tiles
-    (2 blocks per CU). Measured at the config-5 shapes (tools/c5_gemm_shapes.py, profiles/r03/)."""
+    (2 blocks per CU; on the R2 pipeline with LORA_R2_128). Measured at the config-5 shapes (tools/c5_gemm_shapes.py,
+    profiles/r03/; tools/c5_geometry_probe.py, profiles/r06/)."""
     t256 = ((M + 255) // 256) * ((N + 255) // 256)
     if t256 >= 160:
         return 256, 1
     if K >= 4096:
         sp = max(2, min(4, round(240 / t256), K // 1024))
         return 256, sp
-    return 128, 1
+    return (GEO_R2_128 if LORA_R2_128 else 128), 1
 
 
 def gemm_lora(a, b, b_kmajor: bool, a2, b2, M: int, N: int, K: int, out, *, bias=None, resid=None, geometry=None,
