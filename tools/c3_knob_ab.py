@@ -18,15 +18,19 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from vpt import engine  # noqa: E402
+from vpt import engine, ops  # noqa: E402
 from vpt.config import JiT_B_16_Config, JiTTrainingConfig  # noqa: E402
 from vpt.jit_train import JiTTrainer  # noqa: E402
 from vpt.optim import RAdamScheduleFreeFlat  # noqa: E402
 
 
+def _where(k):  # "NAME" = vpt.engine.NAME, "ops.NAME" = vpt.ops.NAME
+    return (ops, k[4:]) if k.startswith("ops.") else (engine, k)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("knobs", help="comma-separated vpt.engine globals switched together")
+    ap.add_argument("knobs", help="comma-separated vpt.engine globals switched together (ops.NAME: a vpt.ops global)")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--grad-ckpt", action="store_true", help="gradient checkpointing on")
@@ -71,7 +75,7 @@ def main():
             if not _lib.DIAG:
                 _lib.use_diag()
             continue
-        if k not in vals and not isinstance(getattr(engine, k), bool):
+        if k not in vals and not isinstance(getattr(*_where(k)), bool):
             raise SystemExit(f"{k}: not a boolean knob of vpt.engine (NAME=ON/OFF for other values)")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -95,9 +99,9 @@ def main():
             if k in diag:
                 diag[k](v)
             elif k in vals:
-                setattr(engine, k, vals[k][0 if v else 1])
+                setattr(*_where(k), vals[k][0 if v else 1])
             else:
-                setattr(engine, k, v)
+                setattr(*_where(k), v)
 
     for v in (True, False):
         setk(v)
