@@ -4,6 +4,8 @@ and the 256x128 two-blocks-per-CU ring (R2, diagnostic library switch vpt_gemm_s
 between the two ring geometries. Interleaved rounds, medians of HIP-event times.
 
   python tools/c5_geometry_probe.py [--rounds 5]
+  python tools/c5_geometry_probe.py --plan [--rounds 5]   (production library: 128 / 1281 / 256 ring / ops' plan, more
+                                                           shapes of the C5 step)
 """
 import argparse
 import json
@@ -32,7 +34,10 @@ def timeit(fn, iters=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--plan", action="store_true")
     args = ap.parse_args()
+    if args.plan:
+        return plan_probe(args.rounds)
     _lib.use_diag()
     dev = "cuda"
     res = {}
@@ -64,6 +69,31 @@ def main():
             res[key] = {"us": med, "ring_eq_r2": bool(torch.equal(outs["ring"], outs["r2"])),
                         "t128_vs_ring_maxdiff": (outs["t128"].float() - outs["ring"].float()).abs().max().item()}
             print(json.dumps({key: res[key]}), flush=True)
+    print(json.dumps(res))
+
+
+def plan_probe(rounds):
+    dev = "cuda"
+    res = {}
+    shapes = [(4224, 1280, 1280, True), (4224, 1280, 1280, False), (4224, 5120, 1280, False), (4224, 1280, 5120, True),
+              (4224, 1280, 3840, False), (16896, 640, 640, True), (16896, 640, 640, False), (16896, 640, 2560, True),
+              (16896, 2560, 640, False), (16896, 640, 1920, False), (16896, 1920, 640, True), (16896, 5120, 640, True)]
+    for M, N, K, fwd in shapes:
+        W = (torch.randn(N, K, device=dev) * 0.03).to(torch.bfloat16) if fwd else \
+            (torch.randn(K, N, device=dev) * 0.03).to(torch.bfloat16)
+        a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        a2 = (torch.randn(M, 16, device=dev) * 0.5).to(torch.bfloat16)
+        b2 = ((torch.randn(N, 16, device=dev) if fwd else torch.randn(16, N, device=dev)) * 0.1).to(torch.bfloat16)
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        plan = ops.lora_gemm_plan(M, N, K)
+        kinds = {"t128": (128, 1), "r2_128": (1281, 1), "ring": (256, 1), "plan": plan}
+        t = {k: [] for k in kinds}
+        for _ in range(rounds):
+            for k, (geo, sp) in kinds.items():
+                t[k].append(timeit(lambda: ops.gemm_lora(a, W, fwd, a2, b2, M, N, K, out, geometry=geo, splits=sp)))
+        key = f"{'fwd' if fwd else 'dgrad'} M{M} N{N} K{K}"
+        res[key] = {"plan": list(plan), "us": {k: round(sorted(v)[len(v) // 2], 1) for k, v in t.items()}}
+        print(json.dumps({key: res[key]}), flush=True)
     print(json.dumps(res))
 
 
