@@ -8,7 +8,7 @@ O=$R/gpurun_out/$1
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 CMD="$R/bench.py --workload c5 --steps 2 --warmup 1"
-RX='gemm_ring_kernel|gemm_bf16_kernel|splitk_reduce_kernel|attn_fwd_kernel|attn_bwd'
+RX='gemm_ring_kernel|gemm_r2_kernel|gemm_bf16_kernel|splitk_reduce_kernel|attn_fwd_kernel|attn_bwd'
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktrace -o p -- python3 -u $CMD > $O/ktrace.log 2>&1
 echo ktrace done
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$RX" --output-format csv -d $O/pmc_fetch -o p -- python3 -u $CMD > $O/pmc_fetch.log 2>&1

@@ -19,7 +19,8 @@ import sys
 
 # op -> (kernel-name substrings that belong to it, the substring counted as one launch of the op)
 # A kernel counts toward every op whose members it matches (the R2 ring, gemm_r2.hip, is both a GEMM-family launch and,
-# in production, only the fused SwiGLU-backward dgrad: its own entry).
+# in the JiT step, only the fused SwiGLU-backward dgrad: its own entry; in the config-5 step it is the 128x128 LoRA
+# GEMMs of geometry 1281, the same kernel name, reported as gemm_r2).
 OPS = {
     "gemm": (("gemm_ring_kernel", "gemm_bf16_kernel", "gemm_r2_kernel", "splitk_reduce_kernel"),
              ("gemm_ring_kernel", "gemm_bf16_kernel", "gemm_r2_kernel")),
@@ -31,6 +32,7 @@ OPS = {
     # reduces counted in the family entry above only)
     "gemm_t128": (("gemm_bf16_kernel",), ("gemm_bf16_kernel",)),
     "gemm_ring256": (("gemm_ring_kernel",), ("gemm_ring_kernel",)),
+    "gemm_r2": (("gemm_r2_kernel",), ("gemm_r2_kernel",)),
 }
 
 
