@@ -298,6 +298,22 @@ def test_gemm_r2_128_equals_t128(ops, ak, bk, splits):
         assert torch.equal(out, ref), (out_mode, (out.float() - ref.float()).abs().max().item())
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (37, 136, 96), (130, 264, 40), (257, 1280, 1280), (600, 8, 32)])
+@pytest.mark.parametrize("bk", [True, False])
+def test_gemm_r2_128_small_and_ragged(ops, M, N, K, bk):
+    """Geometry 1281 at tiny and ragged shapes (one row, partial row / column tiles, a partial 32-deep K tile, N = 8)
+    == geometry 128, with bias + residual."""
+    a = rnd(M, K, seed=100)
+    b = rnd(N, K, scale=0.1, seed=101) if bk else rnd(K, N, scale=0.1, seed=101)
+    bias, resid = rnd(N, scale=0.1, seed=102), rnd(M, N, seed=103)
+    ref = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+    ops.gemm(a, True, b, bk, M, N, K, ref, bias=bias, resid=resid, geometry=128)
+    ops.gemm(a, True, b, bk, M, N, K, out, bias=bias, resid=resid, geometry=1281)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref), (out.float() - ref.float()).abs().max().item()
+
+
 def test_gemm_split_matches_unsplit(ops):
     M, N, K = 2048, 384, 256
     dy, x = rnd(M, N, seed=12), rnd(M, K, seed=13)
