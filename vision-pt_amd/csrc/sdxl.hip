@@ -407,6 +407,15 @@ __device__ __forceinline__ float gelu_erf_grad(float g) {  // d/dg gelu = cdf + 
   const float pdf = __expf(-0.5f * g * g) * 0.3989422804014327f;
   return cdf + g * pdf;
 }
+// gelu_erf(g) and gelu_erf_grad(g) from ONE erff (hipcc does not merge the two calls: 3 exponentials per element
+// instead of 2 in the GeGLU backward) -- the same operations, so the same values.
+__device__ __forceinline__ void gelu_erf_both(float g, float& gelu, float& grad) {
+  const float e = erff(g * 0.70710678118654752f);
+  gelu = 0.5f * g * (1.f + e);
+  const float cdf = 0.5f * (1.f + e);
+  const float pdf = __expf(-0.5f * g * g) * 0.3989422804014327f;
+  grad = cdf + g * pdf;
+}
 
 // out[m][j] = h * gelu(gate), h = x12[m][j], gate = x12[m][F + j] (chunk(2, -1) order), bf16 tensors:
 // out = bf16(h * bf16(gelu(gate))).
@@ -438,8 +447,10 @@ __global__ void geglu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __
   unpack8(*reinterpret_cast<const uint4*>(x12 + m * ldx + F + c * 8), g);
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    oh[e] = d[e] * rbf(gelu_erf(g[e]));
-    og[e] = rbf(d[e] * h[e]) * gelu_erf_grad(g[e]);
+    float ge, gd;
+    gelu_erf_both(g[e], ge, gd);
+    oh[e] = d[e] * rbf(ge);
+    og[e] = rbf(d[e] * h[e]) * gd;
   }
   *reinterpret_cast<uint4*>(dx12 + m * lddx + c * 8) = pack8(oh);
   *reinterpret_cast<uint4*>(dx12 + m * lddx + F + c * 8) = pack8(og);
@@ -513,8 +524,10 @@ __global__ __launch_bounds__(64 * GBW) void geglu_bwd_lora_kernel(const bf16_t* 
       unpack8(gt[s2], fg);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        oh[e] = fd[e] * rbf(gelu_erf(fg[e]));
-        og[e] = rbf(fd[e] * fh[e]) * gelu_erf_grad(fg[e]);
+        float ge, gd;
+        gelu_erf_both(fg[e], ge, gd);
+        oh[e] = fd[e] * rbf(ge);
+        og[e] = rbf(fd[e] * fh[e]) * gd;
       }
       ph[s2] = pack8(oh);
       pg[s2] = pack8(og);
