@@ -355,9 +355,17 @@ int vpt_geglu_fwd(const void* x12, long ldx, int F, long M, void* out, void* str
 int vpt_geglu_bwd(const void* dy, const void* x12, long ldx, int F, long M, void* dx12, long lddx, void* stream);
 /* vpt_geglu_bwd (bit-identical dx12, dy [M][F] dense) and, in the same launch, the rank-16 LoRA projection of dx12
  * through up [2F][16] (the ff.net.0.proj adapter): vs[m][j] = bf16(alpha * dx12[m] . up[:, j]) -- within bf16
- * rounding of vpt_lora_proj(dx12, up, w_kmajor = 0) (16 partial sums instead of 4). F % 128 == 0. */
+ * rounding of vpt_lora_proj(dx12, up, w_kmajor = 0) (per-chunk partial sums in a fixed order). F % 128 == 0.
+ * tickets: (M + 15) / 16 u32, zero-filled when allocated and left zero by every launch (one zeroed buffer serves
+ * every shape; one launch at a time per buffer); partials: vpt_geglu_lora_partials_bytes(M, F), 16-B aligned. */
+long vpt_geglu_lora_partials_bytes(int M, int F);
 int vpt_geglu_bwd_lora(const void* dy, const void* x12, long ldx, int F, int M, void* dx12, long lddx, const void* up,
-                       void* vs, long ldvs, float alpha, void* stream);
+                       void* vs, long ldvs, float alpha, void* tickets, void* partials, void* stream);
+/* vpt_geglu_fwd (bit-identical out [M][F]) and, in the same launch, the rank-16 LoRA down-projection of out for the
+ * Linear that consumes it (ff.net.2): ds[m][j] = bf16(alpha * out[m] . down[j, :]), down [16][F] -- within bf16
+ * rounding of vpt_lora_proj(out, down, w_kmajor = 1). F % 128 == 0; tickets / partials as vpt_geglu_bwd_lora. */
+int vpt_geglu_fwd_lora(const void* x12, long ldx, int F, int M, void* out, long ldo, const void* down, void* ds,
+                       long ldds, float alpha, void* tickets, void* partials, void* stream);
 /* NF4 weights in the bitsandbytes 0.48.2 layout (quant_type nf4, blocksize 64, compress_statistics):
  * packed uint8 [n/2] (first element in the high nibble), qabsmax uint8 [n/64], absmax2 f32 [ceil(n/64/256)],
  * code2 f32 [256] (signed dynamic map), offset f32 [1]. Dequant -> bf16 [n] in the original [out][in]

@@ -726,10 +726,35 @@ def test_gemm_lora_scaled_columns(ops, gn, geometry):
     assert (one.float() - y).abs().max().item() <= y.abs().max().item() * 2 ** -7
 
 
-@pytest.mark.parametrize("M,F", [(4100, 5120), (333, 2560)])
+@pytest.mark.parametrize("M,F", [(4224, 5120), (333, 2560), (77, 640), (16, 128)])
+def test_geglu_fwd_lora(ops, M, F):
+    """vpt_geglu_fwd_lora: out bit-identical to vpt_geglu_fwd; ds = alpha * out . down^T within bf16 rounding of
+    vpt_lora_proj (another f32 summation order) and of fp32 math; repeated launches (the tickets reset) bit-identical."""
+    x12 = rnd(M, 2 * F, seed=193)
+    down = rnd(16, F, scale=0.05, seed=194)
+    ds = torch.empty(M, 16, dtype=torch.bfloat16, device=DEV)
+    out = ops.geglu_fwd_lora(x12, down, 0.0625, ds)
+    ref = ops.geglu_fwd(x12)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    dref = torch.empty(M, 16, dtype=torch.bfloat16, device=DEV)
+    ops.lora_proj(ref, down, True, dref, alpha=0.0625)
+    y = (ref.float() @ down.float().t()) * 0.0625
+    torch.cuda.synchronize()
+    assert rel(ds, y) < 5e-3 and rel(ds, dref) < 5e-3
+    assert (ds.float() - dref.float()).abs().max().item() <= y.abs().max().item() * 2 ** -6
+    for _ in range(3):
+        ds2 = torch.full((M, 16), float("nan"), dtype=torch.bfloat16, device=DEV)
+        ops.geglu_fwd_lora(x12, down, 0.0625, ds2)
+        torch.cuda.synchronize()
+        assert torch.equal(ds2, ds)
+
+
+@pytest.mark.parametrize("M,F", [(4100, 5120), (4224, 5120), (333, 2560), (77, 640), (16, 128)])
 def test_geglu_bwd_lora(ops, M, F):
     """vpt_geglu_bwd_lora: dx12 bit-identical to vpt_geglu_bwd; vs = alpha * dx12 . up within bf16 rounding of
-    vpt_lora_proj (another f32 summation order) and of fp32 math."""
+    vpt_lora_proj (another f32 summation order) and of fp32 math. F = 640: 5 chunk pairs over 2 blocks of 4 waves
+    (idle waves); repeated launches on one workspace (the tickets reset) give bit-identical vs."""
     dy, x12 = rnd(M, F, seed=190), rnd(M, 2 * F, seed=191)
     up = rnd(2 * F, 16, scale=0.05, seed=192)
     vs = torch.empty(M, 16, dtype=torch.bfloat16, device=DEV)
@@ -737,6 +762,11 @@ def test_geglu_bwd_lora(ops, M, F):
     ref = ops.geglu_bwd(dy, x12)
     torch.cuda.synchronize()
     assert torch.equal(dx12, ref)
+    for _ in range(3):
+        vs2 = torch.full((M, 16), float("nan"), dtype=torch.bfloat16, device=DEV)
+        ops.geglu_bwd_lora(dy, x12, up, 0.0625, vs2)
+        torch.cuda.synchronize()
+        assert torch.equal(vs2, vs)
     vref = torch.empty(M, 16, dtype=torch.bfloat16, device=DEV)
     ops.lora_proj(ref, up, False, vref, alpha=0.0625)
     y = (ref.float() @ up.float()) * 0.0625

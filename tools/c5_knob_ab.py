@@ -3,7 +3,7 @@ alternating the knob(s) on / off (vpt.sdxl globals read at call time, e.g. FOLD_
 FUSED_LN_BWD_LORA; "ops.NAME" for a vpt.ops global, e.g. ops.LORA_SERIAL_SPLIT), so allocation, clocks and box are shared; medians of ms per step. The step and the optimizer
 keep running across rounds (the values drift; the timing does not depend on them).
 
-  python tools/c5_knob_ab.py FOLD_Q_SCALE [--rounds 6] [--steps 4]
+  python tools/c5_knob_ab.py FOLD_Q_SCALE [--rounds 6] [--steps 4] [--latent 96,176]
 """
 import argparse
 import json
@@ -25,6 +25,7 @@ def main():
     ap.add_argument("knobs", help="comma-separated vpt.sdxl globals switched together")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--latent", default=None, help="H,W of the latent bucket (default: the model's, 128,128)")
     args = ap.parse_args()
     knobs = args.knobs.split(",")
 
@@ -35,7 +36,7 @@ def main():
         if not isinstance(getattr(mod, name), bool):
             raise SystemExit(f"{k}: not a boolean knob of {mod.__name__}")
     m = SDXLFlowMatchQLoRA(B=4, device="cuda", seed=0)
-    lat, ctx, pooled, sizes = m.make_inputs(seed=1)
+    lat, ctx, pooled, sizes = m.make_inputs(seed=1, latent=tuple(map(int, args.latent.split(","))) if args.latent else None)
 
     def setk(v):
         for k in knobs:

@@ -18,6 +18,7 @@ extern "C" const char* vpt_last_error_string(void) { return g_err; }
 // 2: attention takes nk (cross-attention). 3: vpt_radam_sf_step takes (clip_coef, clip_value) before the stream and
 // vpt_ema_update takes one_minus_decay before `first` -- a caller built against ABI 2 must not bind ABI 3.
 // ABI 4: vpt_embed_grad_set takes `accumulate` before dtable.
-extern "C" int vpt_abi_version(void) { return 4; }
+// ABI 5: vpt_geglu_bwd_lora takes tickets + partials (vpt_geglu_lora_partials_bytes).
+extern "C" int vpt_abi_version(void) { return 5; }
 
 extern "C" const char* vpt_build_info(void) { return "vpt_hip gfx950 (CDNA4) bf16-MFMA abi=4"; }

@@ -459,25 +459,42 @@ __global__ void geglu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __
 // GeGLU backward (as geglu_bwd_kernel: bit-identical dx12) and, in the same launch, the rank-16 LoRA projection of
 // its output through the up of the Linear that produced x12 (ff.net.0.proj): vs[m][j] = bf16(alpha * dx12[m] .
 // up[:, j]), up [2F][16] -- the input-gradient operand of that Linear's backward, without re-reading dx12 (2F wide).
-// 16 rows per block, GBW = 16 waves (4 per SIMD: the erf-heavy body needs the occupancy); wave w takes the
-// 128-column chunk pairs c = w, w + GBW, ... (columns [128c, +128) of dh and of dgate). Each lane computes exactly the
-// 8 elements of its MFMA A fragment (row lane & 15, columns 32s + 8 (lane >> 4) of k step s), so dx12 goes from
-// registers to memory and into the MFMAs with no LDS image; the two up chunks are transposed in turn through the
-// wave's LDS image as in lora_proj. The waves' partial sums meet in LDS in wave order (deterministic; a different
-// f32 summation order than vpt_lora_proj -- within bf16 rounding of it).
-constexpr int GBW = 16;
+// Work unit = 16 rows x one 128-column chunk pair c (columns [128c, +128) of dh and of dgate), one per wave; a block
+// is GBW waves = GBW consecutive chunk pairs of one 16-row block, so a launch is (M / 16) x (F / 128 / GBW) small
+// blocks that the dispatcher spreads evenly. (The form with one 16-wave block per 16 rows ran its 264 blocks of
+// config 5's bucketed M = 4224 as two rounds on 256 CUs: 72 us, 48 us at M = 4096; r06tail.) Each lane computes
+// exactly the 8 elements of its MFMA A fragment (row lane & 15, columns 32s + 8 (lane >> 4) of k step s), so dx12
+// goes from registers to memory and into the MFMAs with no LDS image; both halves' up rows are loaded with the
+// chunk and transposed in turn through the wave's LDS image as in lora_proj. Reduction over the chunk pairs: the
+// block's waves meet in LDS in wave order, the block writes its 16 x 16 f32 partial (write-through), and the block
+// of the row block that arrives last (ticket counter, guide 'In-launch split-K reduction', sc1 form) sums the
+// partials in block order, writes vs and resets the counter -- deterministic for any placement; a different f32
+// summation order than vpt_lora_proj (within bf16 rounding of it).
+constexpr int GBW = 4;
 constexpr int GBP = 136;  // padded transposed-up row (bf16)
 
-// up rows [r0, r0 + 128) ([K][16]) -> the wave's image ws [16][GBP] (two rows per lane)
-__device__ __forceinline__ void gb_up_chunk(const bf16_t* __restrict__ up, long r0, bf16_t* ws, int lane) {
+// up rows [r0, r0 + 128) ([K][16]): lane's two rows (lane, lane + 64), 32 B each
+struct UpRows {
+  uint4 v[2][2];
+};
+__device__ __forceinline__ UpRows gb_up_load(const bf16_t* __restrict__ up, long r0, int lane) {
+  UpRows u;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const bf16_t* ur = up + (r0 + lane + 64 * hh) * 16;
+    u.v[hh][0] = *reinterpret_cast<const uint4*>(ur);
+    u.v[hh][1] = *reinterpret_cast<const uint4*>(ur + 8);
+  }
+  return u;
+}
+// ... -> the wave's image ws [16][GBP]
+__device__ __forceinline__ void gb_up_store(const UpRows& u, bf16_t* ws, int lane) {
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
     const int kr = lane + 64 * hh;
-    const bf16_t* ur = up + (r0 + kr) * 16;
-    const uint4 a0 = *reinterpret_cast<const uint4*>(ur);
-    const uint4 a1 = *reinterpret_cast<const uint4*>(ur + 8);
-    const uint32_t v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const uint32_t v[8] = {u.v[hh][0].x, u.v[hh][0].y, u.v[hh][0].z, u.v[hh][0].w,
+                           u.v[hh][1].x, u.v[hh][1].y, u.v[hh][1].z, u.v[hh][1].w};
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       ws[(2 * e) * GBP + kr] = (bf16_t)(v[e] & 0xffff);
@@ -488,26 +505,82 @@ __device__ __forceinline__ void gb_up_chunk(const bf16_t* __restrict__ up, long 
   __builtin_amdgcn_wave_barrier();
 }
 
+// The in-launch reduction of a row block's chunk partials (geglu_bwd_lora / geglu_fwd_lora): the block's GBW waves
+// meet in LDS in wave order, wave 0 writes the block's 16 x 16 f32 partial (sc1 store: write-through, visible to a
+// reducer on any XCD) to part[rb][b] and counts it in on the row block's ticket (guide 'In-launch split-K reduction',
+// sc1 form); the block that draws the last ticket resets it and returns true, its wave 0 holding in s the nb partials
+// summed in block order (sc1 loads) -- deterministic for any placement. Other blocks / waves return false.
+__device__ __forceinline__ bool rowblock_reduce(floatx4 acc, floatx4 (&red)[GBW][64], float* __restrict__ part,
+                                                unsigned* __restrict__ cnt, int rb, int b, int nb, int wid, int lane,
+                                                floatx4& s) {
+  typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+  red[wid][lane] = acc;
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      part + (long)rb * nb * 256, (short)0, nb * 1024, 0x00020000);
+  if (wid == 0) {
+#pragma unroll
+    for (int w2 = 1; w2 < GBW; ++w2) acc += red[w2][lane];
+    __builtin_amdgcn_raw_buffer_store_b128(
+        u32x4_t{__float_as_uint(acc[0]), __float_as_uint(acc[1]), __float_as_uint(acc[2]), __float_as_uint(acc[3])},
+        rs, lane * 16 + b * 1024, 0, 16);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 1");  // the store's data registers stay untouched after issue (store_b128_padded)
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial is in memory before the ticket
+  }
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(&red[0][0]);  // red is consumed
+  if (threadIdx.x == 0)
+    *flag = __hip_atomic_fetch_add(cnt + rb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nb - 1);
+  __syncthreads();
+  if (!*flag || wid != 0) return false;
+  if (lane == 0) __hip_atomic_store(cnt + rb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+  // block order, 8 partials per round trip; offsets past the row block's nb partials read 0 (buffer range check)
+  // and add exact zeros after the last one
+  for (int b0 = 0; b0 < nb; b0 += 8) {
+    u32x4_t u[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) u[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16 + (b0 + k) * 1024, 0, 16);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const floatx4 v = {__uint_as_float(u[k][0]), __uint_as_float(u[k][1]), __uint_as_float(u[k][2]),
+                         __uint_as_float(u[k][3])};
+      s = (b0 + k == 0) ? v : s + v;
+    }
+  }
+  return true;
+}
+
+// part: [M / 16 * nb][64] floatx4 block partials; cnt: [M / 16] tickets, zero on entry and on exit
 __global__ __launch_bounds__(64 * GBW) void geglu_bwd_lora_kernel(const bf16_t* __restrict__ dy,
                                                                  const bf16_t* __restrict__ x12, long ldx, int F, int M,
                                                                  bf16_t* __restrict__ dx12, long lddx,
                                                                  const bf16_t* __restrict__ up, bf16_t* __restrict__ vs,
-                                                                 long ldvs, float alpha) {
+                                                                 long ldvs, float alpha, float* __restrict__ part,
+                                                                 unsigned* __restrict__ cnt) {
   __shared__ __attribute__((aligned(16))) bf16_t wsa[GBW][16 * GBP];
   __shared__ __attribute__((aligned(16))) floatx4 red[GBW][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g4 = lane >> 4, i = lane & 15;
   bf16_t* ws = wsa[wid];
-  const long row0 = (long)blockIdx.x * 16;
+  const int nchp = F / 128, nb = (nchp + GBW - 1) / GBW;
+  const int rb = blockIdx.x / nb, b = blockIdx.x - rb * nb;
+  const long row0 = (long)rb * 16;
   const long row = row0 + i;
   const bool row_ok = row < M;
   const long rowc = row_ok ? row : (long)M - 1;
-  const bf16_t* dyr = dy + rowc * F + 8 * g4;
-  const bf16_t* xr = x12 + rowc * ldx + 8 * g4;
-  bf16_t* dxr = dx12 + rowc * lddx + 8 * g4;
-  const int nchp = F / 128;
+  const int c = b * GBW + wid;  // this wave's chunk pair
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int c = wid; c < nchp; c += GBW) {
-    uint4 d[4], h[4], gt[4], ph[4], pg[4];
+  if (c < nchp) {
+    const bf16_t* dyr = dy + rowc * F + 8 * g4;
+    const bf16_t* xr = x12 + rowc * ldx + 8 * g4;
+    bf16_t* dxr = dx12 + rowc * lddx + 8 * g4;
+#ifndef VPT_GB_ABL
+#define VPT_GB_ABL 0  // timing ablations (lib variants only, wrong results): 1 = every chunk reads up rows 0..255
+#endif
+    const UpRows uh = gb_up_load(up, VPT_GB_ABL == 1 ? 0L : (long)c * 128, lane);      // the dh half's up rows
+    const UpRows ug = gb_up_load(up, VPT_GB_ABL == 1 ? 128L : (long)F + c * 128, lane);  // the dgate half's
+    uint4 d[4], h[4], gt[4], pg[4];
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2) {
       const int col = c * 128 + 32 * s2;
@@ -515,7 +588,7 @@ __global__ __launch_bounds__(64 * GBW) void geglu_bwd_lora_kernel(const bf16_t* 
       h[s2] = *reinterpret_cast<const uint4*>(xr + col);
       gt[s2] = *reinterpret_cast<const uint4*>(xr + F + col);
     }
-    gb_up_chunk(up, (long)c * 128, ws, lane);  // the dh half's up rows, while the loads above land
+    gb_up_store(uh, ws, lane);
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2) {
       float fd[8], fh[8], fg[8], oh[8], og[8];
@@ -529,32 +602,83 @@ __global__ __launch_bounds__(64 * GBW) void geglu_bwd_lora_kernel(const bf16_t* 
         oh[e] = fd[e] * rbf(ge);
         og[e] = rbf(fd[e] * fh[e]) * gd;
       }
-      ph[s2] = pack8(oh);
+      const uint4 ph = pack8(oh);
       pg[s2] = pack8(og);
       const int col = c * 128 + 32 * s2;
       if (row_ok) {
-        *reinterpret_cast<uint4*>(dxr + col) = ph[s2];
+        *reinterpret_cast<uint4*>(dxr + col) = ph;
         *reinterpret_cast<uint4*>(dxr + F + col) = pg[s2];
       }
       const uint4 bh = *reinterpret_cast<const uint4*>(&ws[i * GBP + 32 * s2 + 8 * g4]);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(ph[s2]), as_frag(bh), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(ph), as_frag(bh), acc, 0, 0, 0);
     }
-    gb_up_chunk(up, (long)F + c * 128, ws, lane);  // the dgate half's
+    gb_up_store(ug, ws, lane);
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2) {
       const uint4 bg = *reinterpret_cast<const uint4*>(&ws[i * GBP + 32 * s2 + 8 * g4]);
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(pg[s2]), as_frag(bg), acc, 0, 0, 0);
     }
   }
-  red[wid][lane] = acc;
-  __syncthreads();
-  if (wid != 0) return;
-#pragma unroll
-  for (int w2 = 1; w2 < GBW; ++w2) acc += red[w2][lane];
+  floatx4 s;
+  if (!rowblock_reduce(acc, red, part, cnt, rb, b, nb, wid, lane, s)) return;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const long m = row0 + 4 * g4 + r;
-    if (m < M) vs[m * ldvs + i] = f2bf(acc[r] * alpha);
+    if (m < M) vs[m * ldvs + i] = f2bf(s[r] * alpha);
+  }
+}
+
+// GeGLU forward (as geglu_fwd_kernel: bit-identical out) and, in the same launch, the rank-16 LoRA down-projection of
+// its output for the Linear that consumes it (ff.net.2): ds[m][j] = bf16(alpha * out[m] . down[j, :]), down [16][F]
+// -- that Linear's forward operand, without re-reading out. Work unit = 16 rows x one 128-column chunk, one per wave,
+// GBW consecutive chunks per block; each lane computes exactly the 8 outputs of its MFMA A fragment, and its B
+// fragment is 16 B of down row (lane & 15) straight from memory (k-major: no LDS image). The chunks' partials meet as
+// in geglu_bwd_lora (rowblock_reduce: fixed order; a different f32 summation order than vpt_lora_proj).
+__global__ __launch_bounds__(64 * GBW) void geglu_fwd_lora_kernel(const bf16_t* __restrict__ x12, long ldx, int F,
+                                                                 int M, bf16_t* __restrict__ out, long ldo,
+                                                                 const bf16_t* __restrict__ down,
+                                                                 bf16_t* __restrict__ ds, long ldds, float alpha,
+                                                                 float* __restrict__ part,
+                                                                 unsigned* __restrict__ cnt) {
+  __shared__ __attribute__((aligned(16))) floatx4 red[GBW][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g4 = lane >> 4, i = lane & 15;
+  const int nch = F / 128, nb = (nch + GBW - 1) / GBW;
+  const int rb = blockIdx.x / nb, b = blockIdx.x - rb * nb;
+  const long row0 = (long)rb * 16;
+  const long row = row0 + i;
+  const bool row_ok = row < M;
+  const long rowc = row_ok ? row : (long)M - 1;
+  const int c = b * GBW + wid;  // this wave's chunk
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (c < nch) {
+    const bf16_t* xr = x12 + rowc * ldx + c * 128 + 8 * g4;
+    const bf16_t* dr = down + (long)i * F + c * 128 + 8 * g4;
+    bf16_t* orow = out + rowc * ldo + c * 128 + 8 * g4;
+    uint4 h[4], gt[4], wd[4];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      h[s2] = *reinterpret_cast<const uint4*>(xr + 32 * s2);
+      gt[s2] = *reinterpret_cast<const uint4*>(xr + F + 32 * s2);
+      wd[s2] = *reinterpret_cast<const uint4*>(dr + 32 * s2);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      float fh[8], fg[8], o[8];
+      unpack8(h[s2], fh);
+      unpack8(gt[s2], fg);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = fh[e] * rbf(gelu_erf(fg[e]));
+      const uint4 po = pack8(o);
+      if (row_ok) *reinterpret_cast<uint4*>(orow + 32 * s2) = po;
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(po), as_frag(wd[s2]), acc, 0, 0, 0);
+    }
+  }
+  floatx4 s;
+  if (!rowblock_reduce(acc, red, part, cnt, rb, b, nb, wid, lane, s)) return;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const long m = row0 + 4 * g4 + r;
+    if (m < M) ds[m * ldds + i] = f2bf(s[r] * alpha);
   }
 }
 
@@ -934,15 +1058,55 @@ extern "C" int vpt_geglu_fwd(const void* x12, long ldx, int F, long M, void* out
   return VPT_OK;
 }
 
+// Workspaces of vpt_geglu_bwd_lora / vpt_geglu_fwd_lora: tickets = (M + 15) / 16 u32 row-block counters, zero when
+// allocated and left zero by every launch (a launch touches only its own row blocks' counters, so one zeroed buffer
+// serves every shape); partials = vpt_geglu_lora_partials_bytes(M, F), uninitialised.
+extern "C" long vpt_geglu_lora_partials_bytes(int M, int F) {
+  if (M <= 0 || F <= 0) return 0;
+  return (long)((M + 15) / 16) * ((F / 128 + GBW - 1) / GBW) * 1024;
+}
+
+namespace {
+int geglu_lora_check(const char* fn, int F, int M, const void* tickets, const void* partials) {
+  VPT_CHECK_ARG(tickets && partials, fn);
+  VPT_CHECK_ARG(((uintptr_t)tickets & 3) == 0 && ((uintptr_t)partials & 15) == 0, fn);
+  const long R = (M + 15) / 16, nb = (F / 128 + GBW - 1) / GBW;
+  VPT_CHECK_ARG(R * nb < (1L << 31) && nb * 1024 < (1L << 30), fn);
+  return VPT_OK;
+}
+}  // namespace
+
+extern "C" int vpt_geglu_fwd_lora(const void* x12, long ldx, int F, int M, void* out, long ldo, const void* down,
+                                  void* ds, long ldds, float alpha, void* tickets, void* partials, void* stream) {
+  VPT_CHECK_ARG(x12 && out && down && ds, "vpt_geglu_fwd_lora: null pointer");
+  VPT_CHECK_ARG(F > 0 && F % 128 == 0 && ldx % 8 == 0 && ldo % 8 == 0 && ldx >= 2L * F && ldo >= F && ldds >= 16,
+                "vpt_geglu_fwd_lora: F % 128 == 0, 16-B leading dims (x12 >= 2F, out >= F)");
+  if (M <= 0) return VPT_OK;
+  if (int rc = geglu_lora_check("vpt_geglu_fwd_lora: tickets / partials (null, misaligned or too many blocks)", F, M,
+                                tickets, partials))
+    return rc;
+  const long R = (M + 15) / 16, nb = (F / 128 + GBW - 1) / GBW;
+  hipLaunchKernelGGL(geglu_fwd_lora_kernel, dim3((unsigned)(R * nb)), dim3(64 * GBW), 0, (hipStream_t)stream,
+                     (const bf16_t*)x12, ldx, F, M, (bf16_t*)out, ldo, (const bf16_t*)down, (bf16_t*)ds, ldds, alpha,
+                     (float*)partials, (unsigned*)tickets);
+  VPT_LAUNCH_CHECK();
+  return VPT_OK;
+}
+
 extern "C" int vpt_geglu_bwd_lora(const void* dy, const void* x12, long ldx, int F, int M, void* dx12, long lddx,
-                                  const void* up, void* vs, long ldvs, float alpha, void* stream) {
+                                  const void* up, void* vs, long ldvs, float alpha, void* tickets, void* partials,
+                                  void* stream) {
   VPT_CHECK_ARG(dy && x12 && dx12 && up && vs, "vpt_geglu_bwd_lora: null pointer");
   VPT_CHECK_ARG(F > 0 && F % 128 == 0 && ldx % 8 == 0 && lddx % 8 == 0 && ldx >= 2L * F && lddx >= 2L * F && ldvs >= 16,
                 "vpt_geglu_bwd_lora: F % 128 == 0, 16-B leading dims >= 2F");
   if (M <= 0) return VPT_OK;
-  hipLaunchKernelGGL(geglu_bwd_lora_kernel, dim3((M + 15) / 16), dim3(64 * GBW), 0, (hipStream_t)stream,
+  if (int rc = geglu_lora_check("vpt_geglu_bwd_lora: tickets / partials (null, misaligned or too many blocks)", F, M,
+                                tickets, partials))
+    return rc;
+  const long R = (M + 15) / 16, nb = (F / 128 + GBW - 1) / GBW;
+  hipLaunchKernelGGL(geglu_bwd_lora_kernel, dim3((unsigned)(R * nb)), dim3(64 * GBW), 0, (hipStream_t)stream,
                      (const bf16_t*)dy, (const bf16_t*)x12, ldx, F, M, (bf16_t*)dx12, lddx, (const bf16_t*)up,
-                     (bf16_t*)vs, ldvs, alpha);
+                     (bf16_t*)vs, ldvs, alpha, (float*)partials, (unsigned*)tickets);
   VPT_LAUNCH_CHECK();
   return VPT_OK;
 }

@@ -86,7 +86,9 @@ SIGNATURES: dict[str, list] = {
     "vpt_layernorm_bwd_lora": [P, L, P, L, P, P, P, P, L, P, L, I, I, P, P, L, F, P],
     "vpt_geglu_fwd": [P, L, I, L, P, P],
     "vpt_geglu_bwd": [P, P, L, I, L, P, L, P],
-    "vpt_geglu_bwd_lora": [P, P, L, I, I, P, L, P, P, L, F, P],
+    "vpt_geglu_bwd_lora": [P, P, L, I, I, P, L, P, P, L, F, P, P, P],
+    "vpt_geglu_lora_partials_bytes": [I, I],
+    "vpt_geglu_fwd_lora": [P, L, I, I, P, L, P, P, L, F, P, P, P],
     "vpt_nf4_dequant": [P, P, P, P, P, L, P, P],
     "vpt_nf4_dequant_batch": [P, I, P],
     "vpt_scale_bf16_2d": [P, L, L, I, F, P, L, P],
@@ -149,6 +151,7 @@ DIAG_SIGNATURES: dict[str, list] = {
 }
 _RESTYPES = {
     "vpt_lora_wgrad_workspace": C.c_long,
+    "vpt_geglu_lora_partials_bytes": C.c_long,
     "vpt_gemm_workspace_bytes": C.c_long,
     "vpt_linear_wgrad_workspace_bytes": C.c_long,
     "vpt_attn_fused_workspace_bytes": C.c_long,
@@ -159,7 +162,7 @@ _RESTYPES = {
     "vpt_build_info": C.c_char_p,
 }
 # Entry points that return a value (size / count / string) rather than a status code.
-_VALUE_FNS = {"vpt_attn_bwd_queue_bytes", "vpt_grad_norm_blocks", "vpt_velocity_loss_blocks", "vpt_lora_wgrad_workspace", "vpt_lora_wgrad_splits", "vpt_gemm_workspace_bytes", "vpt_linear_wgrad_workspace_bytes", "vpt_attn_fused_workspace_bytes", "vpt_cover_resize_crop_workspace", "vpt_gemm_swiglu_bwd_workspace", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
+_VALUE_FNS = {"vpt_attn_bwd_queue_bytes", "vpt_grad_norm_blocks", "vpt_velocity_loss_blocks", "vpt_lora_wgrad_workspace", "vpt_geglu_lora_partials_bytes", "vpt_lora_wgrad_splits", "vpt_gemm_workspace_bytes", "vpt_linear_wgrad_workspace_bytes", "vpt_attn_fused_workspace_bytes", "vpt_cover_resize_crop_workspace", "vpt_gemm_swiglu_bwd_workspace", "vpt_rmsnorm_bwd_blocks", "vpt_layernorm_bwd_blocks", "vpt_qknorm_rope_blocks", "vpt_loss_blocks",
               "vpt_colsum_blocks", "vpt_attn_q_scale", "vpt_attn_bwd_dw_rows", "vpt_last_error_string", "vpt_abi_version", "vpt_build_info"}
 
 
@@ -176,7 +179,7 @@ def _load(path: Path, diag: bool = False) -> C.CDLL:
     return lib
 
 
-ABI_VERSION = 4  # the signatures in SIGNATURES / include/vpt_hip.h
+ABI_VERSION = 5  # the signatures in SIGNATURES / include/vpt_hip.h
 
 
 def load_library(path: Path | str, diag: bool = False) -> C.CDLL:

@@ -141,6 +141,20 @@ def workspace(dev, tag: str, n: int, dtype=F32) -> torch.Tensor:
     return buf[:n]
 
 
+_TICKETS: dict = {}  # (device, stream) -> zero-filled u32 tickets of the in-launch row-block reductions
+
+
+def tickets(dev, n: int) -> torch.Tensor:
+    """Row-block tickets for a kernel whose in-launch reduction counts blocks on them (vpt_geglu_bwd_lora /
+    vpt_geglu_fwd_lora): zero when allocated, left zero by every launch, so one buffer serves every shape; one per
+    (device, current stream), so launches on one stream reuse it in order and two streams never share tickets."""
+    key = (str(dev), stream())
+    buf = _TICKETS.get(key)
+    if buf is None or buf.numel() < n:
+        buf = _TICKETS[key] = torch.zeros(max(n, 1024), dtype=torch.int32, device=dev)
+    return buf
+
+
 GEO_R2_128 = 1281  # 128 x 128 tiles on the R2 ring's pipeline (include/vpt_hip.h vpt_gemm_bf16_tiled)
 LORA_R2_128 = True  # lora_gemm_plan: GEO_R2_128 instead of the two-stage 128 x 128 kernel (A/B knob)
 
@@ -880,6 +894,21 @@ def geglu_fwd(x12, out=None):
     return out
 
 
+def geglu_fwd_lora(x12, down, alpha: float, ds, out=None):
+    """geglu_fwd and, in the same launch, ds = bf16(alpha * out . down^T) (down [16, F]; csrc/sdxl.hip
+    geglu_fwd_lora_kernel). Returns out."""
+    M, F2 = x12.shape
+    _chk(down, BF16, "down")
+    if not (down.is_contiguous() and down.shape == (16, F2 // 2) and ds.stride(1) == 1 and ds.shape[1] >= 16):
+        raise ValueError("geglu_fwd_lora: contiguous down [16, F], row-major ds with 16 columns")
+    out = torch.empty(M, F2 // 2, dtype=BF16, device=x12.device) if out is None else out
+    tk = tickets(x12.device, (M + 15) // 16)
+    part = workspace(x12.device, "geglu_lora", int(call("vpt_geglu_lora_partials_bytes", M, F2 // 2)) // 4)
+    call("vpt_geglu_fwd_lora", x12.data_ptr(), x12.stride(0), F2 // 2, M, out.data_ptr(), out.stride(0),
+         down.data_ptr(), ds.data_ptr(), ds.stride(0), float(alpha), tk.data_ptr(), part.data_ptr(), stream())
+    return out
+
+
 def geglu_bwd(dy, x12, dx12=None):
     M, F2 = x12.shape
     dx12 = torch.empty_like(x12) if dx12 is None else dx12
@@ -897,8 +926,11 @@ def geglu_bwd_lora(dy, x12, up, alpha: float, vs, dx12=None):
             and vs.shape[1] >= 16):
         raise ValueError("geglu_bwd_lora: dense dy [M, F], contiguous up [2F, 16], row-major vs with 16 columns")
     dx12 = torch.empty_like(x12) if dx12 is None else dx12
+    tk = tickets(x12.device, (M + 15) // 16)
+    part = workspace(x12.device, "geglu_lora", int(call("vpt_geglu_lora_partials_bytes", M, F2 // 2)) // 4)
     call("vpt_geglu_bwd_lora", dy.data_ptr(), x12.data_ptr(), x12.stride(0), F2 // 2, M, dx12.data_ptr(),
-         dx12.stride(0), up.data_ptr(), vs.data_ptr(), vs.stride(0), float(alpha), stream())
+         dx12.stride(0), up.data_ptr(), vs.data_ptr(), vs.stride(0), float(alpha), tk.data_ptr(), part.data_ptr(),
+         stream())
     return dx12
 
 

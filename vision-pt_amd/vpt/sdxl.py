@@ -274,6 +274,8 @@ FUSED_LN_BWD_LORA = True  # the backward half alone
 FOLD_Q_SCALE = True
 # True = the GeGLU backward also emits ff.net.0.proj's input-gradient LoRA operand (ops.geglu_bwd_lora)
 FUSED_GEGLU_LORA = True
+# True = the GeGLU forward also emits ff.net.2's LoRA down-projection (ops.geglu_fwd_lora)
+FUSED_GEGLU_LORA_FWD = True
 # True = inside a training step's backward (lora_side_scope), each block's batched adapter-gradient launches
 # (ops.lora_wgrad_batch) run on a side stream beside the input-gradient chain (nothing in the chain reads an adapter
 # gradient); the scope's exit joins the side stream, before anything reads the adapter gradients. Measured -1.5 % per
@@ -491,8 +493,14 @@ class SDXLTransformerBlock:
         x2 = L["attn2.to_out.0"].forward(o2, save, resid=x1, W=Wb.get("attn2.to_out.0"))
         h3, m3, r3, ds3 = self._ln_lora(x2, "norm3", ["ff.net.0.proj"])
         x12 = L["ff.net.0.proj"].forward(h3, save, W=Wb.get("ff.net.0.proj"), ds=ds3)
-        gg = ops.geglu_fwd(x12)
-        y = L["ff.net.2"].forward(gg, save, resid=x2, W=Wb.get("ff.net.2"))
+        f2 = L["ff.net.2"]
+        ds_f2 = None
+        if FUSED_GEGLU_LORA_FWD and f2.skinny and x12.shape[1] % 256 == 0:
+            ds_f2 = torch.empty(x12.shape[0], 16, dtype=BF16, device=self.device)
+            gg = ops.geglu_fwd_lora(x12, f2.down, f2.scale, ds_f2)
+        else:
+            gg = ops.geglu_fwd(x12)
+        y = f2.forward(gg, save, resid=x2, W=Wb.get("ff.net.2"), ds=ds_f2)
         self._st = dict(B=B, n=n, nc=nc, x=x, x1=x1, x2=x2, m=(m1, m2, m3), r=(r1, r2, r3), q=q, k=k, v=v, o1=o1,
                         lse1=lse1, q2=q2, k2=k2, v2=v2, o2=o2, lse2=lse2, x12=x12) if save else None
         return y
@@ -515,9 +523,8 @@ class SDXLTransformerBlock:
         Wb = dequant_bases(L, [t for t in TARGETS if need_dctx or t not in ("attn2.to_k", "attn2.to_v")], self.device)
         dgg = L["ff.net.2"].backward(dy, W=Wb.get("ff.net.2"))
         f0 = L["ff.net.0.proj"]
-        # fused at the 1280-channel stages (F = 5120: 52 vs 73 us for the pair, M = 4096); at F = 2560 its 20 chunk
-        # pairs over 16 waves run slower than the pair (128 vs 120 us, M = 16384; profiles/r03/r03zn_*)
-        if FUSED_GEGLU_LORA and f0.skinny and st["x12"].shape[1] % 256 == 0 and st["x12"].shape[1] >= 8192:
+        # fused: 49 vs 70 us for the pair at M = 4224, F = 5120; 108 vs 118 us at M = 16896, F = 2560 (r06gd)
+        if FUSED_GEGLU_LORA and f0.skinny and st["x12"].shape[1] % 256 == 0:
             vs_f0 = torch.empty(dgg.shape[0], 16, dtype=BF16, device=self.device)
             dx12 = ops.geglu_bwd_lora(dgg, st["x12"], f0.up, f0.scale, vs_f0)
         else:
