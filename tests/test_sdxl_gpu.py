@@ -641,6 +641,27 @@ def test_sdxl_block_fused_ln_lora_bitwise(ops, monkeypatch):
     assert torch.equal(c0, c1) and torch.equal(g0, g1)
 
 
+def test_sdxl_stack_fused_ln_bwd_prev_bitwise(ops, monkeypatch):
+    """Two-block stacks: each block's norm1 backward emitting the previous block's ff.net.2 input-gradient LoRA operand
+    (FUSED_LN_BWD_PREV, ops.layernorm_bwd_lora) gives a step bit-identical to the separate lora_proj."""
+    from vpt import sdxl
+    from vpt.sdxl_train import SDXLStacksQLoRA
+    res = []
+    for fused in (True, False):
+        monkeypatch.setattr(sdxl, "FUSED_LN_BWD_PREV", fused)
+        m = SDXLStacksQLoRA(B=2, stacks=[("a", 640, 10, 2, 16), ("b", 1280, 20, 2, 8)], n_ctx=77, seed=3)
+        g = torch.Generator(device=DEV).manual_seed(9)
+        with torch.no_grad():
+            m.params.copy_((torch.randn(m.params.shape, device=DEV, generator=g) * 0.03).bfloat16())
+        xs, ctx, gs = m.make_inputs(seed=4)
+        m.opt.step = lambda: None  # compare gradients, not the update
+        dctx = m.step(xs, ctx, gs)
+        torch.cuda.synchronize()
+        res.append((dctx.clone(), m.grads.clone()))
+    (c0, g0), (c1, g1) = res
+    assert torch.equal(c0, c1) and torch.equal(g0, g1)
+
+
 def test_nf4_dequant_batch_bit_exact(ops):
     """vpt_nf4_dequant_batch (several tensors of different sizes in one launch, the last block of each partial)
     against the oracle's dequantisation of each: bit-identical."""

@@ -276,6 +276,9 @@ FOLD_Q_SCALE = True
 FUSED_GEGLU_LORA = True
 # True = the GeGLU forward also emits ff.net.2's LoRA down-projection (ops.geglu_fwd_lora)
 FUSED_GEGLU_LORA_FWD = True
+# True = a transformer block's norm1 backward also emits the input-gradient LoRA operand of the previous block's
+# ff.net.2 (whose output gradient that dx is; ops.layernorm_bwd_lora, bit-identical to the separate lora_proj)
+FUSED_LN_BWD_PREV = True
 # True = inside a training step's backward (lora_side_scope), each block's batched adapter-gradient launches
 # (ops.lora_wgrad_batch) run on a side stream beside the input-gradient chain (nothing in the chain reads an adapter
 # gradient); the scope's exit joins the side stream, before anything reads the adapter gradients. Measured -1.5 % per
@@ -347,6 +350,7 @@ class SDXLTransformerBlock:
         self.norm = {k: (sd[f"{k}.weight"].to(device, BF16).contiguous(), sd[f"{k}.bias"].to(device, BF16).contiguous())
                      for k in ("norm1", "norm2", "norm3")}
         self._st = None
+        self.vs_prev = None  # the previous block's ff.net.2 vs from the last backward (backward(prev_ff2=...))
         # (k, v, ctx key) of the cross-attention, projected for the next forward by the caller (SDXLStacksQLoRA.
         # precompute_ctx_kv: every block's over one fixed context in stacked GEMMs); used only by a forward over
         # the context it was projected from (_ctx_key); None: projected here
@@ -389,11 +393,11 @@ class SDXLTransformerBlock:
             return y, m, r, ds
         return (*ops.layernorm_fwd(x, *self.norm[norm]), None)
 
-    def _ln_bwd_lora(self, dy, x, mean, rstd, norm: str, dres, target: str):
+    def _ln_bwd_lora(self, dy, x, mean, rstd, norm: str, dres, target):
         """LayerNorm backward of `norm` and the input-gradient LoRA operand vs = s * dx . up of `target` (the
-        LoRALinear that consumes dx as its output gradient) in one launch (ops.layernorm_bwd_lora): (dx, vs); vs None
-        where the fused form does not apply."""
-        lin = self.lin[target]
+        LoRALinear that consumes dx as its output gradient: a name in this block, or the LoRALinear itself) in one
+        launch (ops.layernorm_bwd_lora): (dx, vs); vs None where the fused form does not apply."""
+        lin = self.lin[target] if isinstance(target, str) else target
         if FUSED_LN_LORA and FUSED_LN_BWD_LORA and lin.skinny and lin.up.is_contiguous() and x.shape[1] % 128 == 0:
             vs = torch.empty(x.shape[0], 16, dtype=BF16, device=x.device)
             dx = ops.layernorm_bwd_lora(dy, x, mean, rstd, self.norm[norm][0], lin.up, lin.scale, vs, dres=dres)
@@ -505,15 +509,20 @@ class SDXLTransformerBlock:
                         lse1=lse1, q2=q2, k2=k2, v2=v2, o2=o2, lse2=lse2, x12=x12) if save else None
         return y
 
-    def backward(self, dy: torch.Tensor, need_dctx: bool = True):
+    def backward(self, dy: torch.Tensor, need_dctx: bool = True, vs: torch.Tensor | None = None,
+                 prev_ff2: "LoRALinearNF4 | None" = None):
         """Returns (dx, dctx); accumulates every adapter's g_down / g_up (norms and NF4 bases frozen). The ten
         targets' adapter-gradient reduces run as one batched launch at the end (ops.lora_wgrad_batch).
         need_dctx=False: the context needs no gradient (the reference's text-encoder states are produced under
-        no_grad, train/sdxl/flow_match.py:115-124), so the to_k / to_v input-gradient GEMMs are skipped."""
+        no_grad, train/sdxl/flow_match.py:115-124), so the to_k / to_v input-gradient GEMMs are skipped.
+        vs: ff.net.2's input-gradient LoRA operand s * dy . up, already computed by the caller (the next block's
+        norm1 backward). prev_ff2: the ff.net.2 of the block before this one, which consumes dx as its output
+        gradient -- its vs is then emitted by this block's norm1 backward (ops.layernorm_bwd_lora) into
+        self.vs_prev (None where the fused form does not apply)."""
         with ops.lora_wgrad_batch(side=lora_side(self.device)):
-            return self._backward(dy, need_dctx)
+            return self._backward(dy, need_dctx, vs, prev_ff2)
 
-    def _backward(self, dy: torch.Tensor, need_dctx: bool = True):
+    def _backward(self, dy: torch.Tensor, need_dctx: bool = True, vs_ff2=None, prev_ff2=None):
         st, L = self._st, self.lin
         B, n, nc = st["B"], st["n"], st["nc"]
         m1, m2, m3 = st["m"]
@@ -521,7 +530,7 @@ class SDXLTransformerBlock:
         # the bases of the input-gradient GEMMs about to run, one launch (to_k / to_v of the context only when
         # the context needs a gradient)
         Wb = dequant_bases(L, [t for t in TARGETS if need_dctx or t not in ("attn2.to_k", "attn2.to_v")], self.device)
-        dgg = L["ff.net.2"].backward(dy, W=Wb.get("ff.net.2"))
+        dgg = L["ff.net.2"].backward(dy, W=Wb.get("ff.net.2"), vs=vs_ff2)
         f0 = L["ff.net.0.proj"]
         # fused: 49 vs 70 us for the pair at M = 4224, F = 5120; 108 vs 118 us at M = 16896, F = 2560 (r06gd)
         if FUSED_GEGLU_LORA and f0.skinny and st["x12"].shape[1] % 256 == 0:
@@ -561,7 +570,11 @@ class SDXLTransformerBlock:
             dh1 = ops.add_bf16(ops.add_bf16(L["attn1.to_q"].backward(dq, W=Wb.get("attn1.to_q")),
                                             L["attn1.to_k"].backward(dk, W=Wb.get("attn1.to_k"))),
                                L["attn1.to_v"].backward(dv, W=Wb.get("attn1.to_v")))
-        dx = ops.layernorm_bwd(dh1, st["x"], m1, r1, self.norm["norm1"][0], dres=dx1)
+        self.vs_prev = None
+        if prev_ff2 is not None and FUSED_LN_BWD_PREV:
+            dx, self.vs_prev = self._ln_bwd_lora(dh1, st["x"], m1, r1, "norm1", dx1, prev_ff2)
+        else:
+            dx = ops.layernorm_bwd(dh1, st["x"], m1, r1, self.norm["norm1"][0], dres=dx1)
         return dx, dctx
 
     def lora_grads(self) -> dict[str, torch.Tensor]:
@@ -650,8 +663,11 @@ class SDXLSpatialTransformer:
         du = ops.transpose_add(dy, B, C, HW)                                  # tokens [B, HW, C]
         dt = self.proj_out.backward(du.view(B * HW, C))
         dctx = None
-        for blk in reversed(self.blocks):
-            dt, dc = blk.backward(dt, need_dctx)
+        vs = None  # ff.net.2's vs of the block below, emitted by the norm1 backward of the block above
+        for i in reversed(range(len(self.blocks))):
+            blk = self.blocks[i]
+            dt, dc = blk.backward(dt, need_dctx, vs=vs, prev_ff2=self.blocks[i - 1].lin["ff.net.2"] if i else None)
+            vs = blk.vs_prev
             if need_dctx:
                 dctx = dc if dctx is None else ops.add_bf16(dctx, dc)
         dtok = self.proj_in.backward(dt)
