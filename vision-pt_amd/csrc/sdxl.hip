@@ -472,6 +472,9 @@ __global__ void geglu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __
 // summation order than vpt_lora_proj (within bf16 rounding of it).
 constexpr int GBW = 4;
 constexpr int GBP = 136;  // padded transposed-up row (bf16)
+#ifndef VPT_GB_ABL
+#define VPT_GB_ABL 0  // timing ablations (lib variants only, wrong results): 1 = every chunk reads up rows 0..255
+#endif
 
 // up rows [r0, r0 + 128) ([K][16]): lane's two rows (lane, lane + 64), 32 B each
 struct UpRows {
@@ -575,9 +578,6 @@ __global__ __launch_bounds__(64 * GBW) void geglu_bwd_lora_kernel(const bf16_t* 
     const bf16_t* dyr = dy + rowc * F + 8 * g4;
     const bf16_t* xr = x12 + rowc * ldx + 8 * g4;
     bf16_t* dxr = dx12 + rowc * lddx + 8 * g4;
-#ifndef VPT_GB_ABL
-#define VPT_GB_ABL 0  // timing ablations (lib variants only, wrong results): 1 = every chunk reads up rows 0..255
-#endif
     const UpRows uh = gb_up_load(up, VPT_GB_ABL == 1 ? 0L : (long)c * 128, lane);      // the dh half's up rows
     const UpRows ug = gb_up_load(up, VPT_GB_ABL == 1 ? 128L : (long)F + c * 128, lane);  // the dgate half's
     uint4 d[4], h[4], gt[4], pg[4];
