@@ -19,6 +19,9 @@ extern "C" const char* vpt_last_error_string(void) { return g_err; }
 // vpt_ema_update takes one_minus_decay before `first` -- a caller built against ABI 2 must not bind ABI 3.
 // ABI 4: vpt_embed_grad_set takes `accumulate` before dtable.
 // ABI 5: vpt_geglu_bwd_lora takes tickets + partials (vpt_geglu_lora_partials_bytes).
-extern "C" int vpt_abi_version(void) { return 5; }
+#define VPT_ABI_VERSION 5
+#define VPT_STR2(x) #x
+#define VPT_STR(x) VPT_STR2(x)
+extern "C" int vpt_abi_version(void) { return VPT_ABI_VERSION; }
 
-extern "C" const char* vpt_build_info(void) { return "vpt_hip gfx950 (CDNA4) bf16-MFMA abi=4"; }
+extern "C" const char* vpt_build_info(void) { return "vpt_hip gfx950 (CDNA4) bf16-MFMA abi=" VPT_STR(VPT_ABI_VERSION); }
