@@ -475,6 +475,9 @@ constexpr int GBP = 136;  // padded transposed-up row (bf16)
 #ifndef VPT_GB_ABL
 #define VPT_GB_ABL 0  // timing ablations (lib variants only, wrong results): 1 = every chunk reads up rows 0..255
 #endif
+#ifndef VPT_GB_UG_LATE
+#define VPT_GB_UG_LATE 0  // A/B: the dgate half's up rows loaded after the dh half's MFMAs (fewer VGPRs)
+#endif
 
 // up rows [r0, r0 + 128) ([K][16]): lane's two rows (lane, lane + 64), 32 B each
 struct UpRows {
@@ -579,7 +582,9 @@ __global__ __launch_bounds__(64 * GBW) void geglu_bwd_lora_kernel(const bf16_t* 
     const bf16_t* xr = x12 + rowc * ldx + 8 * g4;
     bf16_t* dxr = dx12 + rowc * lddx + 8 * g4;
     const UpRows uh = gb_up_load(up, VPT_GB_ABL == 1 ? 0L : (long)c * 128, lane);      // the dh half's up rows
+#if !VPT_GB_UG_LATE
     const UpRows ug = gb_up_load(up, VPT_GB_ABL == 1 ? 128L : (long)F + c * 128, lane);  // the dgate half's
+#endif
     uint4 d[4], h[4], gt[4], pg[4];
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2) {
@@ -612,6 +617,9 @@ __global__ __launch_bounds__(64 * GBW) void geglu_bwd_lora_kernel(const bf16_t* 
       const uint4 bh = *reinterpret_cast<const uint4*>(&ws[i * GBP + 32 * s2 + 8 * g4]);
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(ph), as_frag(bh), acc, 0, 0, 0);
     }
+#if VPT_GB_UG_LATE
+    const UpRows ug = gb_up_load(up, VPT_GB_ABL == 1 ? 128L : (long)F + c * 128, lane);
+#endif
     gb_up_store(ug, ws, lane);
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2) {
