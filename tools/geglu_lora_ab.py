@@ -53,8 +53,18 @@ def main():
                 _lib.use_library(lb)
                 for c, fn in cases.items():
                     t[(v, c)].append(timeit(fn))
+        outs = {}
+        for v, lb in libs.items():  # each build's outputs, compared bitwise with the first build's
+            _lib.use_library(lb)
+            vb, vf = torch.empty_like(vs), torch.empty_like(vs)
+            dx = ops.geglu_bwd_lora(dy, x12, up, 0.0625, vb)
+            gf = ops.geglu_fwd_lora(x12, down, 0.0625, vf)
+            torch.cuda.synchronize()
+            outs[v] = (vb, vf, dx, gf)
         _lib.use_library(libs[next(iter(libs))])
         res[f"{M}x{F}"] = {f"{v}:{c}": round(sorted(x)[len(x) // 2], 1) for (v, c), x in t.items()}
+        first = outs[next(iter(outs))]
+        res[f"{M}x{F}"]["bitwise_equal"] = {v: all(torch.equal(a, b) for a, b in zip(o, first)) for v, o in outs.items()}
         print(json.dumps({f"{M}x{F}": res[f"{M}x{F}"]}), flush=True)
     print(json.dumps(res))
 

@@ -475,6 +475,12 @@ constexpr int GBP = 136;  // padded transposed-up row (bf16)
 #ifndef VPT_GB_ABL
 #define VPT_GB_ABL 0  // timing ablations (lib variants only, wrong results): 1 = every chunk reads up rows 0..255
 #endif
+#ifndef VPT_GF_COAL
+#define VPT_GF_COAL 1  // 1: geglu_fwd_lora moves x12 / out in row segments, A fragments through LDS (0: fragment-direct)
+#endif
+#ifndef VPT_GB_COAL
+#define VPT_GB_COAL 1  // 1: geglu_bwd_lora moves dy / x12 / dx12 in row segments, A fragments through LDS (0: fragment-direct)
+#endif
 #ifndef VPT_GB_UG_LATE
 #define VPT_GB_UG_LATE 0  // A/B: the dgate half's up rows loaded after the dh half's MFMAs (fewer VGPRs)
 #endif
@@ -577,6 +583,65 @@ __global__ __launch_bounds__(64 * GBW) void geglu_bwd_lora_kernel(const bf16_t* 
   const long rowc = row_ok ? row : (long)M - 1;
   const int c = b * GBW + wid;  // this wave's chunk pair
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#if VPT_GB_COAL
+  // dy / x12 / dx12 moved in full 256-B row segments (16 lanes per row, 4 rows per instruction); the A fragments read
+  // back from an LDS image of the wave's 16 x 128 dh tile, then of its dgate tile (same image, same MFMA order)
+  __shared__ __attribute__((aligned(16))) bf16_t gbt[GBW][16 * GBP];
+  if (c < nchp) {
+    bf16_t* t = gbt[wid];
+    const int lr = lane >> 4, lc = (lane & 15) * 8;
+    const UpRows uh = gb_up_load(up, VPT_GB_ABL == 1 ? 0L : (long)c * 128, lane);      // the dh half's up rows
+    const UpRows ug = gb_up_load(up, VPT_GB_ABL == 1 ? 128L : (long)F + c * 128, lane);  // the dgate half's
+    uint4 d[4], h[4], gt[4], pg[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const long r = row0 + 4 * q + lr;
+      const long rc = r < M ? r : (long)M - 1;
+      d[q] = *reinterpret_cast<const uint4*>(dy + rc * F + c * 128 + lc);
+      h[q] = *reinterpret_cast<const uint4*>(x12 + rc * ldx + c * 128 + lc);
+      gt[q] = *reinterpret_cast<const uint4*>(x12 + rc * ldx + F + c * 128 + lc);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const long r = row0 + 4 * q + lr;
+      float fd[8], fh[8], fg[8], oh[8], og[8];
+      unpack8(d[q], fd);
+      unpack8(h[q], fh);
+      unpack8(gt[q], fg);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float ge, gd;
+        gelu_erf_both(fg[e], ge, gd);
+        oh[e] = fd[e] * rbf(ge);
+        og[e] = rbf(fd[e] * fh[e]) * gd;
+      }
+      const uint4 ph = pack8(oh);
+      pg[q] = pack8(og);
+      if (r < M) {
+        *reinterpret_cast<uint4*>(dx12 + r * lddx + c * 128 + lc) = ph;
+        *reinterpret_cast<uint4*>(dx12 + r * lddx + F + c * 128 + lc) = pg[q];
+      }
+      *reinterpret_cast<uint4*>(t + (4 * q + lr) * GBP + lc) = ph;
+    }
+    gb_up_store(uh, ws, lane);  // its lgkmcnt(0) wait also lands the dh tile
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const uint4 a = *reinterpret_cast<const uint4*>(t + i * GBP + 32 * s2 + 8 * g4);
+      const uint4 bh = *reinterpret_cast<const uint4*>(&ws[i * GBP + 32 * s2 + 8 * g4]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), as_frag(bh), acc, 0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *reinterpret_cast<uint4*>(t + (4 * q + lr) * GBP + lc) = pg[q];
+    gb_up_store(ug, ws, lane);  // ... and the dgate tile
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const uint4 a = *reinterpret_cast<const uint4*>(t + i * GBP + 32 * s2 + 8 * g4);
+      const uint4 bg = *reinterpret_cast<const uint4*>(&ws[i * GBP + 32 * s2 + 8 * g4]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), as_frag(bg), acc, 0, 0, 0);
+    }
+  }
+#else
   if (c < nchp) {
     const bf16_t* dyr = dy + rowc * F + 8 * g4;
     const bf16_t* xr = x12 + rowc * ldx + 8 * g4;
@@ -627,6 +692,7 @@ __global__ __launch_bounds__(64 * GBW) void geglu_bwd_lora_kernel(const bf16_t* 
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(pg[s2]), as_frag(bg), acc, 0, 0, 0);
     }
   }
+#endif
   floatx4 s;
   if (!rowblock_reduce(acc, red, part, cnt, rb, b, nb, wid, lane, s)) return;
 #pragma unroll
@@ -658,6 +724,44 @@ __global__ __launch_bounds__(64 * GBW) void geglu_fwd_lora_kernel(const bf16_t* 
   const long rowc = row_ok ? row : (long)M - 1;
   const int c = b * GBW + wid;  // this wave's chunk
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#if VPT_GF_COAL
+  // x12 / out moved in full 256-B row segments (16 lanes per row, 4 rows per instruction) and the A fragments
+  // read back from an LDS image of the wave's 16 x 128 output tile
+  __shared__ __attribute__((aligned(16))) bf16_t gft[GBW][16 * GBP];
+  if (c < nch) {
+    bf16_t* t = gft[wid];
+    const int lr = lane >> 4, lc = (lane & 15) * 8;
+    const bf16_t* dr = down + (long)i * F + c * 128 + 8 * g4;
+    uint4 h[4], gt[4], wd[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const long r = row0 + 4 * q + lr;
+      const bf16_t* xr = x12 + (r < M ? r : (long)M - 1) * ldx + c * 128 + lc;
+      h[q] = *reinterpret_cast<const uint4*>(xr);
+      gt[q] = *reinterpret_cast<const uint4*>(xr + F);
+      wd[q] = *reinterpret_cast<const uint4*>(dr + 32 * q);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const long r = row0 + 4 * q + lr;
+      float fh[8], fg[8], o[8];
+      unpack8(h[q], fh);
+      unpack8(gt[q], fg);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = fh[e] * rbf(gelu_erf(fg[e]));
+      const uint4 po = pack8(o);
+      if (r < M) *reinterpret_cast<uint4*>(out + r * ldo + c * 128 + lc) = po;
+      *reinterpret_cast<uint4*>(t + (4 * q + lr) * GBP + lc) = po;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const uint4 a = *reinterpret_cast<const uint4*>(t + i * GBP + 32 * s2 + 8 * g4);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), as_frag(wd[s2]), acc, 0, 0, 0);
+    }
+  }
+#else
   if (c < nch) {
     const bf16_t* xr = x12 + rowc * ldx + c * 128 + 8 * g4;
     const bf16_t* dr = down + (long)i * F + c * 128 + 8 * g4;
@@ -681,6 +785,7 @@ __global__ __launch_bounds__(64 * GBW) void geglu_fwd_lora_kernel(const bf16_t* 
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(po), as_frag(wd[s2]), acc, 0, 0, 0);
     }
   }
+#endif
   floatx4 s;
   if (!rowblock_reduce(acc, red, part, cnt, rb, b, nb, wid, lane, s)) return;
 #pragma unroll
