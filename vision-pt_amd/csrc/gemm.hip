@@ -1360,6 +1360,9 @@ constexpr int LKP = LKC + 8;     // padded LDS row (bf16): conflict-free b128 ro
 // W = up [K][16]: each chunk transposed through the wave's LDS image.
 constexpr int LPD = 4;
 constexpr int LKS = 4;
+#ifndef VPT_LP_COAL
+#define VPT_LP_COAL 0  // A/B: activation rows loaded in 256-B segments, A fragments through LDS
+#endif
 // Grouped (blockIdx.y = group gy): X + gy * xgoff, W + gy * wgoff, output columns 16 gy .. 16 gy + 15 -- the
 // q / k / v projections of one input (or of the three column blocks of one gradient) in one launch.
 __global__ __launch_bounds__(64 * LKS) void lora_proj_kernel(const bf16_t* __restrict__ X, long ldx, long xgoff,
@@ -1367,13 +1370,23 @@ __global__ __launch_bounds__(64 * LKS) void lora_proj_kernel(const bf16_t* __res
                                                              bf16_t* __restrict__ Y, long ldy, int M, int K, float alpha) {
   __shared__ __attribute__((aligned(16))) bf16_t wsa[LKS][16 * LKP];
   __shared__ __attribute__((aligned(16))) floatx4 red[LKS][64];
+#if VPT_LP_COAL
+  __shared__ __attribute__((aligned(16))) bf16_t xta[LKS][16 * LKP];  // the wave's 16 x 128 activation chunk
+#endif
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
   X += blockIdx.y * xgoff;
   W += blockIdx.y * wgoff;
   Y += blockIdx.y * 16;
   bf16_t* ws = wsa[wid];
   const int row = blockIdx.x * 16 + j;
+#if VPT_LP_COAL
+  // rows in full 256-B segments (16 lanes per row, 4 rows per load), A fragments read back through LDS
+  const bf16_t* xr = X + (long)min(blockIdx.x * 16 + g, M - 1) * ldx + (lane & 15) * 8;
+  const long xq = 4 * ldx;  // next 4 rows
+  const int lastq = (M - 1 - (int)blockIdx.x * 16 - g) / 4;  // loads past M re-read row M - 1
+#else
   const bf16_t* xr = X + (long)min(row, M - 1) * ldx + 8 * g;
+#endif
   const bf16_t* wr = W + (long)j * K + 8 * g;  // down: row j
   const int nch = K / LKC;
   const int ncw = (nch - wid + LKS - 1) / LKS;  // chunks wid, wid + LKS, ... of this wave
@@ -1385,7 +1398,11 @@ __global__ __launch_bounds__(64 * LKS) void lora_proj_kernel(const bf16_t* __res
       const int c = wid + LKS * u;
 #pragma unroll
       for (int s = 0; s < LKC / 32; ++s) {
+#if VPT_LP_COAL
+        xb[u][s] = *reinterpret_cast<const uint4*>(xr + (s <= lastq ? s : lastq) * xq + c * LKC);
+#else
         xb[u][s] = *reinterpret_cast<const uint4*>(xr + c * LKC + 32 * s);
+#endif
         if (w_kmajor) wb[u][s] = *reinterpret_cast<const uint4*>(wr + c * LKC + 32 * s);
       }
     }
@@ -1412,17 +1429,34 @@ __global__ __launch_bounds__(64 * LKS) void lora_proj_kernel(const bf16_t* __res
           __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
           __builtin_amdgcn_wave_barrier();
         }
+#if VPT_LP_COAL
+        bf16_t* xt = xta[wid];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int s = 0; s < LKC / 32; ++s) *reinterpret_cast<uint4*>(xt + (4 * s + g) * LKP + (lane & 15) * 8) = xb[u][s];
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+        __builtin_amdgcn_wave_barrier();
+#endif
 #pragma unroll
         for (int s = 0; s < LKC / 32; ++s) {
           const bf16x8 bf = w_kmajor ? as_frag(wb[u][s])
                                      : as_frag(*reinterpret_cast<const uint4*>(&ws[j * LKP + 32 * s + 8 * g]));
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(xb[u][s]), bf, acc, 0, 0, 0);
+#if VPT_LP_COAL
+          const bf16x8 af = as_frag(*reinterpret_cast<const uint4*>(xt + j * LKP + 32 * s + 8 * g));
+#else
+          const bf16x8 af = as_frag(xb[u][s]);
+#endif
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc, 0, 0, 0);
         }
         if (t + LPD < ncw) {
           const int cn = c + LKS * LPD;
 #pragma unroll
           for (int s = 0; s < LKC / 32; ++s) {
+#if VPT_LP_COAL
+            xb[u][s] = *reinterpret_cast<const uint4*>(xr + (s <= lastq ? s : lastq) * xq + cn * LKC);
+#else
             xb[u][s] = *reinterpret_cast<const uint4*>(xr + cn * LKC + 32 * s);
+#endif
             if (w_kmajor) wb[u][s] = *reinterpret_cast<const uint4*>(wr + cn * LKC + 32 * s);
           }
         }
